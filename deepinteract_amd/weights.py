@@ -1,0 +1,209 @@
+"""Seeded, reproducible LitGINI weights under the reference's state-dict key names.
+
+No trained checkpoint exists offline (Zenodo, README.md:249-252), so parity runs on seeded
+weights. Each tensor is drawn from its own ``torch.Generator('cpu')`` seeded from
+``(seed, crc32(key))``: the values do not depend on key order and are identical on any host
+(torch's CPU Mersenne-Twister is platform independent). BatchNorm running stats and affine
+parameters are randomised so that every folded BatchNorm is non-trivial.
+
+Key layout mirrors ``LitGINI`` (deepinteract_modules.py:1478-1625), including the ResBlock
+quirk that ONE BatchNorm1d instance is registered three times (``res_block.1/.4/.7``,
+deepinteract_modules.py:468-479): the three keys always carry identical values.
+"""
+from __future__ import annotations
+
+import hashlib
+import math
+import zlib
+from collections import OrderedDict
+
+import torch
+
+from .config import GeoTConfig, NUM_RBF
+
+
+def _linear(keys, name, out_f, in_f, bias):
+    keys.append((f"{name}.weight", (out_f, in_f), "lin_w"))
+    if bias:
+        keys.append((f"{name}.bias", (out_f,), "bias"))
+
+
+def _bn(keys, name, c):
+    keys.append((f"{name}.weight", (c,), "bn_w"))
+    keys.append((f"{name}.bias", (c,), "bn_b"))
+    keys.append((f"{name}.running_mean", (c,), "bn_mean"))
+    keys.append((f"{name}.running_var", (c,), "bn_var"))
+    keys.append((f"{name}.num_batches_tracked", (), "bn_nbt"))
+
+
+def _conf_keys(keys, p, cfg: GeoTConfig):
+    H, S, G = cfg.num_gnn_hidden_channels, cfg.shared_embed_size, cfg.geo_embed_size
+    _linear(keys, f"{p}.dist_linear_0", G, NUM_RBF, False)
+    _linear(keys, f"{p}.dist_linear_1", H, G, False)
+    _linear(keys, f"{p}.dir_linear_0", G, 3, False)
+    _linear(keys, f"{p}.dir_linear_1", S, G, False)
+    _linear(keys, f"{p}.orient_linear_0", G, 4, False)
+    _linear(keys, f"{p}.orient_linear_1", S, G, False)
+    _linear(keys, f"{p}.amide_linear_0", G, 1, False)
+    _linear(keys, f"{p}.amide_linear_1", S, G, False)
+    _linear(keys, f"{p}.nbr_linear", H, H, True)
+    _linear(keys, f"{p}.orig_msg_linear", H, H, True)
+    _linear(keys, f"{p}.downward_proj", S, H, False)
+    _linear(keys, f"{p}.upward_proj", H, S, False)
+    _linear(keys, f"{p}.res_connect_linear", H, H, True)
+    for kind, n in (("pre_res_blocks", cfg.num_pre_res_blocks), ("post_res_blocks", cfg.num_post_res_blocks)):
+        for b in range(n):
+            rb = f"{p}.{kind}.{b}.res_block"
+            for i in (0, 3, 6):
+                _linear(keys, f"{rb}.{i}", H, H, True)
+                _bn(keys, f"{rb}.{i + 1}", H)
+    _linear(keys, f"{p}.final_dist_linear", H, NUM_RBF, False)
+    _linear(keys, f"{p}.final_dir_linear", H, 3, False)
+    _linear(keys, f"{p}.final_orient_linear", H, 4, False)
+    _linear(keys, f"{p}.final_amide_linear", H, 1, False)
+    _linear(keys, f"{p}.final_linear", H, H, True)
+
+
+def geot_keys(cfg: GeoTConfig = GeoTConfig()):
+    """(key, shape, kind) for node_in_embedding + gnn_module.0 (DGLGeometricTransformer)."""
+    H = cfg.num_gnn_hidden_channels
+    keys = []
+    _linear(keys, "node_in_embedding", H, cfg.num_node_input_feats, False)
+    ie = "gnn_module.0.init_edge_module"
+    keys.append((f"{ie}.node_embedding.weight", (cfg.node_count_limit, H), "emb"))
+    for suffix in ("0", "1"):
+        _linear(keys, f"{ie}.edge_messages_linear_{suffix}", H, 2, False)
+        _linear(keys, f"{ie}.dist_linear_{suffix}", H, NUM_RBF, False)
+        _linear(keys, f"{ie}.dir_linear_{suffix}", H, 3, False)
+        _linear(keys, f"{ie}.orient_linear_{suffix}", H, 4, False)
+        _linear(keys, f"{ie}.amide_linear_{suffix}", H, 1, False)
+        if suffix == "0":
+            _linear(keys, f"{ie}.combined_linear_0", H, 7 * H, False)
+    _linear(keys, f"{ie}.combined_linear_1", 28, H, False)
+    _linear(keys, f"{ie}.combined_linear_2", H, 28, False)
+    L = cfg.num_gnn_layers
+    for li in range(L):
+        p = f"gnn_module.0.gt_block.{li}"
+        final = li == L - 1
+        _conf_keys(keys, f"{p}.conformation_module", cfg)
+        _bn(keys, f"{p}.batch_norm1_node_feats", H)
+        _bn(keys, f"{p}.batch_norm1_edge_feats", H)
+        for q in ("Q", "K", "V", "edge_feats_projection"):
+            _linear(keys, f"{p}.mha_module.{q}", H, H, False)
+        _linear(keys, f"{p}.O_node_feats", H, H, True)
+        if not final:
+            _linear(keys, f"{p}.O_edge_feats", H, H, True)
+        _linear(keys, f"{p}.node_feats_MLP.0", 2 * H, H, False)
+        _linear(keys, f"{p}.node_feats_MLP.3", H, 2 * H, False)
+        _bn(keys, f"{p}.batch_norm2_node_feats", H)
+        if not final:
+            _bn(keys, f"{p}.batch_norm2_edge_feats", H)
+            _linear(keys, f"{p}.edge_feats_MLP.0", 2 * H, H, False)
+            _linear(keys, f"{p}.edge_feats_MLP.3", H, 2 * H, False)
+    return keys
+
+
+def _conv(keys, name, o, i, k):
+    keys.append((f"{name}.weight", (o, i, k, k), "conv_w"))
+    keys.append((f"{name}.bias", (o,), "conv_b"))
+
+
+def _inorm(keys, name, c):
+    keys.append((f"{name}.weight", (c,), "bn_w"))
+    keys.append((f"{name}.bias", (c,), "bn_b"))
+
+
+def head_keys(cfg: GeoTConfig = GeoTConfig()):
+    """(key, shape, kind) for interact_module = ResNet2DInputWithOptAttention
+    (deepinteract_modules.py:1155-1248, ResNet :973-1106, SEBlock :954-970)."""
+    C, H = cfg.num_interact_hidden_channels, cfg.num_gnn_hidden_channels
+    keys = []
+    p = "interact_module"
+    _conv(keys, f"{p}.conv2d_1", C, 2 * H, 1)
+    _inorm(keys, f"{p}.inorm_1", C)
+
+    def resnet(prefix, mname, chunks, inorm, extra):
+        _conv(keys, f"{prefix}.resnet_{mname}_init_proj", C, C, 1)
+        blocks = [f"{i}_{d}" for i in range(chunks) for d in (1, 2, 4, 8)]
+        if extra:
+            blocks += ["extra0", "extra1"]
+        for b in blocks:
+            r = f"{prefix}.resnet_{mname}_{b}"
+            if inorm:
+                _inorm(keys, f"{r}_inorm_1", C)
+                _inorm(keys, f"{r}_inorm_2", C // 2)
+                _inorm(keys, f"{r}_inorm_3", C // 2)
+            _conv(keys, f"{r}_conv2d_1", C // 2, C, 1)
+            _conv(keys, f"{r}_conv2d_2", C // 2, C // 2, 3)
+            _conv(keys, f"{r}_conv2d_3", C, C // 2, 1)
+            _linear(keys, f"{r}_se_block.linear1", C // 16, C, True)
+            _linear(keys, f"{r}_se_block.linear2", C, C // 16, True)
+
+    resnet(f"{p}.base_resnet", "base_resnet", cfg.num_interact_layers, True, False)
+    resnet(f"{p}.phase2_resnet", "bin_resnet", 1, False, True)
+    _conv(keys, f"{p}.phase2_conv", cfg.num_classes, C, 1)
+    return keys
+
+
+def _canonical_key(key: str) -> str:
+    # the shared ResBlock BatchNorm: .4 and .7 alias .1
+    for alias in (".res_block.4.", ".res_block.7."):
+        if alias in key:
+            return key.replace(alias, ".res_block.1.")
+    return key
+
+
+def _draw(key: str, shape, kind: str, seed: int) -> torch.Tensor:
+    g = torch.Generator(device="cpu")
+    g.manual_seed((seed * 1_000_003 + zlib.crc32(_canonical_key(key).encode())) % (2 ** 63))
+
+    def u(lo, hi):
+        return lo + (hi - lo) * torch.rand(shape, generator=g, dtype=torch.float64)
+
+    if kind == "lin_w":
+        out_f, in_f = shape
+        b = math.sqrt(6.0 / (in_f + out_f))
+        t = u(-b, b)
+    elif kind == "bias":
+        t = u(-0.1, 0.1)
+    elif kind == "bn_w":
+        t = u(0.8, 1.2)
+    elif kind == "bn_b":
+        t = u(-0.1, 0.1)
+    elif kind == "bn_mean":
+        t = u(-0.2, 0.2)
+    elif kind == "bn_var":
+        t = u(0.6, 1.4)
+    elif kind == "bn_nbt":
+        return torch.tensor(0, dtype=torch.long)
+    elif kind == "emb":
+        t = u(-math.sqrt(3.0), math.sqrt(3.0))
+    elif kind in ("conv_w", "conv_b"):
+        fan_in = None
+        t = None
+        if kind == "conv_w":
+            fan_in = shape[1] * shape[2] * shape[3]
+        else:
+            fan_in = shape[0]  # bias bound uses the weight's fan-in below
+        b = 1.0 / math.sqrt(fan_in)
+        t = u(-b, b)
+    else:
+        raise ValueError(kind)
+    return t.to(torch.float32)
+
+
+def seeded_state_dict(seed: int = 0, cfg: GeoTConfig = GeoTConfig(), with_head: bool = True):
+    """Reference-keyed LitGINI state dict with seeded values (fp32, CPU)."""
+    sd = OrderedDict()
+    keys = geot_keys(cfg) + (head_keys(cfg) if with_head else [])
+    for key, shape, kind in keys:
+        sd[key] = _draw(key, shape, kind, seed)
+    return sd
+
+
+def state_dict_sha256(sd) -> str:
+    h = hashlib.sha256()
+    for k in sorted(sd):
+        h.update(k.encode())
+        h.update(sd[k].detach().cpu().contiguous().numpy().tobytes())
+    return h.hexdigest()
