@@ -1,0 +1,265 @@
+"""Benchmark: complexes/s of the GeoT forward (both chains) + L1xL2 pair tensor.
+
+Workload (BASELINE.json configs[2], the metric's config): synthetic DIPS-Plus-sized heterodimers,
+2 x 1000 residues, k = 20, 2 GeoT layers, 128 hidden, 4 heads, bf16 storage / fp32 accumulation;
+1024 complexes per GPU per step, processed in micro-batches (a [256,1000,1000] bf16 pair tensor
+is 512 MB, so the 1024 outputs cannot be resident at once; each micro-batch's pair tensors are
+written to a rotating HBM buffer). The timed region starts with every complex's graph tensors
+(node [N,113], edge [E,28], ids) resident in HBM and ends with the outputs in HBM.
+
+Multi-GPU (torchrun): complexes are sharded, each rank owns its 1024; no collective in the timed
+region (weak scaling); value = total complexes / max-over-ranks time.
+
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "complexes/sec GeoT+pair-tensor fwd (2×1k res, k=20, 1/8 GPU); % HBM peak"
+HBM_PEAK_GBS = 8000.0
+MFMA_PEAK_TFLOPS = {"bf16": 2500.0, "f32": 157.3}
+# SURVEY.md §8d algorithmic MAC per unit (edge or node), per launch kind
+EDGE_MAC = {"init_edge": 129_024, "edge_layer": 456_656, "edge_layer_final": 374_736}
+H = 128
+
+
+def node_mac(kind):
+    q = 3 * H * H
+    if kind == "node_embed":
+        return 113 * H + q
+    if kind == "node_layer":
+        return H * H + 2 * H * 2 * H + q
+    if kind == "node_layer_final":
+        return H * H + 2 * H * 2 * H
+    raise KeyError(kind)
+
+
+def algorithmic_bytes_per_complex(n1, n2, k, s):
+    """B = sum_chains [N*113*4 + E*28*4 + E*4 + E*2*nb*4 + N*128*s + E*128*s] + 256*L1*L2*s."""
+    b = 0
+    for n in (n1, n2):
+        e = n * k
+        b += n * 113 * 4 + e * 28 * 4 + e * 4 + e * 2 * 2 * 4 + n * 128 * s + e * 128 * s
+    return b + 256 * n1 * n2 * s
+
+
+def kernel_units(kind, nodes, edges, l1l2):
+    """(algorithmic FLOPs, algorithmic HBM bytes) of one launch."""
+    if kind in EDGE_MAC:
+        return 2.0 * EDGE_MAC[kind] * edges, None
+    if kind.startswith("node"):
+        return 2.0 * node_mac(kind) * nodes, None
+    if kind == "pair_tensor":
+        return None, l1l2
+    raise KeyError(kind)
+
+
+def dist_setup():
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if ws > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(local)
+    return ws, rank, local
+
+
+def barrier(ws):
+    if ws > 1:
+        import torch.distributed as dist
+        dist.barrier()
+
+
+def max_over_ranks(ws, x):
+    if ws == 1:
+        return x
+    import torch.distributed as dist
+    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def load_pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary (separate
+    --pmc passes, FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM), or None."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as fh:
+            d = json.load(fh)
+        return d.get(kernel, {}).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def cpu_baseline(n_res, k, sample, threads):
+    """Oracle (CPU restatement, DGL-style op-for-op, fp32) on C3-shaped complexes."""
+    from deepinteract_amd import synth
+    from deepinteract_amd.weights import seeded_state_dict
+    from oracle import geot_oracle as O
+    torch.set_num_threads(threads)
+    sd = seeded_state_dict(0, with_head=False)
+    ch1, ch2 = synth.synthetic_complex(3, n_res, n_res)
+    g1 = O.build_graph(ch1, k=k, seed=1)
+    g2 = O.build_graph(ch2, k=k, seed=2)
+
+    def one():
+        with torch.inference_mode():
+            n1, _ = O.geot_forward(sd, g1)
+            n2, _ = O.geot_forward(sd, g2)
+            t = O.pair_tensor(n1, n2)
+        return t
+
+    one()  # warm-up
+    t0 = time.perf_counter()
+    for _ in range(sample):
+        one()
+    dt = time.perf_counter() - t0
+    return sample / dt, dt
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--complexes", type=int, default=1024, help="complexes per GPU per step")
+    ap.add_argument("--micro-batch", type=int, default=8)
+    ap.add_argument("--residues", type=int, default=1000)
+    ap.add_argument("--knn", type=int, default=20)
+    ap.add_argument("--pool", type=int, default=16, help="distinct synthetic complexes replicated in HBM")
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
+    ap.add_argument("--cpu-sample", type=int, default=2)
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    ws, rank, local = dist_setup()
+    dev = torch.device("cuda", local)
+    from deepinteract_amd import synth
+    from deepinteract_amd.builder import build_graph_batch
+    from deepinteract_amd.engine import GeoTEngine, PairTensorOp
+    from deepinteract_amd.graph import concat_batches
+    from deepinteract_amd.weights import seeded_state_dict
+
+    n_res, k, M = args.residues, args.knn, args.micro_batch
+    assert args.complexes % M == 0
+    sd = seeded_state_dict(0, with_head=False)
+    eng = GeoTEngine(sd, args.dtype, device=dev)
+    pair = PairTensorOp(dev)
+
+    # ---- inputs: a pool of distinct complexes built on the device (kNN + features + ids) ----
+    P = min(args.pool, args.complexes)
+    pool = []
+    torch.cuda.synchronize()
+    tb = time.perf_counter()
+    for c in range(P):
+        ch1, ch2 = synth.synthetic_complex(1000 * rank + c, n_res, n_res)
+        pool.append((ch1, ch2))
+    t_synth = time.perf_counter() - tb
+    torch.cuda.synchronize()
+    tb = time.perf_counter()
+    pool_gb = [build_graph_batch([a, b], k=k, seed=c + 1, device=dev) for c, (a, b) in enumerate(pool)]
+    torch.cuda.synchronize()
+    t_build = time.perf_counter() - tb
+    # resident batch: complexes -> micro-batches (copies of pool complexes, distinct HBM buffers)
+    n_mb = args.complexes // M
+    mbs = [concat_batches([pool_gb[(m * M + j) % P] for j in range(M)]) for m in range(n_mb)]
+    del pool_gb
+    gb0 = mbs[0]
+    h1r = [gb0.node_off[2 * j] for j in range(M)]
+    h2r = [gb0.node_off[2 * j + 1] for j in range(M)]
+    l1 = [n_res] * M
+    l2 = [n_res] * M
+    tdt = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+    esz = 2 if args.dtype == "bf16" else 4
+    pair_buf = torch.empty(M * 2 * H * n_res * n_res, dtype=tdt, device=dev)
+
+    def step(events=None):
+        for gb in mbs:
+            h, _ = eng.forward(gb, clone=False, events=events)
+            pair(h, h1r, h2r, l1, l2, out=pair_buf, events=events)
+
+    for _ in range(args.warmup):
+        step()
+    events = {}
+    barrier(ws)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(events)
+    torch.cuda.synchronize()
+    barrier(ws)
+    elapsed = time.perf_counter() - t0
+    elapsed = max_over_ranks(ws, elapsed)
+    total = args.complexes * args.steps * ws
+    value = total / elapsed
+
+    # ---- per-kernel timing (HIP events on the launch stream, inside the timed region) -------
+    nodes, edges = gb0.num_nodes, gb0.num_edges
+    l1l2 = sum(2 * H * a * b * esz for a, b in zip(l1, l2))
+    kern = {}
+    for name, pairs in events.items():
+        ms = [s.elapsed_time(e) for s, e in pairs]
+        avg_s = float(np.mean(ms)) / 1e3
+        flops, byts = kernel_units(name, nodes, edges, l1l2)
+        rec = {"launches": len(ms), "avg_us": avg_s * 1e6, "total_ms": float(np.sum(ms))}
+        if flops is not None:
+            rec["tflops"] = flops / avg_s / 1e12
+        if byts is not None:
+            rec["gbs"] = byts / avg_s / 1e9
+        kern[name] = rec
+    dom = max(kern, key=lambda n: kern[n]["total_ms"])
+    d = kern[dom]
+    if "tflops" in d:
+        roof = {"kernel": dom, "bound": "mfma", "achieved": round(d["tflops"], 2),
+                "peak": MFMA_PEAK_TFLOPS[args.dtype], "unit": "TFLOP/s"}
+    else:
+        roof = {"kernel": dom, "bound": "hbm", "achieved": round(d["gbs"], 1), "peak": HBM_PEAK_GBS, "unit": "GB/s"}
+    roof["frac"] = round(roof["achieved"] / roof["peak"], 4)
+    traffic = load_pmc_traffic(dom)
+    roof["traffic"] = traffic
+    bytes_c = algorithmic_bytes_per_complex(n_res, n_res, k, esz)
+    hbm_frac = bytes_c * value / ws / (HBM_PEAK_GBS * 1e9)
+
+    out = {
+        "metric": METRIC, "value": round(value, 2), "unit": "complexes/s", "n_gpus": ws,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
+        "data": "synthetic (seeded random-walk chains, on-device graph build; seeded random weights)",
+        "config": {"workload": f"C3: 2x{n_res}-residue heterodimers, k={k}, 2 GeoT layers, 128 hidden, 4 heads; "
+                               f"GeoT fwd (both chains) + [256,{n_res},{n_res}] pair tensor",
+                   "complexes_per_gpu_per_step": args.complexes, "micro_batch": M, "residues": [n_res, n_res],
+                   "knn": k, "parallelism": f"complex-sharded dp{ws}"},
+        "hbm_frac_of_peak": round(hbm_frac, 4),
+        "roofline": roof,
+        "kernels": {n: {kk: round(v, 3) if isinstance(v, float) else v for kk, v in r.items()} for n, r in kern.items()},
+        "builder": {"complexes": P, "build_s": round(t_build, 4), "synth_host_s": round(t_synth, 3)},
+    }
+    if rank == 0 and ws == 1 and not args.no_cpu:
+        threads = min(16, os.cpu_count() or 1)
+        cps, dt = cpu_baseline(n_res, k, args.cpu_sample, threads)
+        out["cpu_baseline"] = {"value": round(cps, 4), "unit": "complexes/s", "cores": threads, "kind": "port",
+                               "sample": f"{args.cpu_sample} C3 complexes (2x{n_res} res, k={k}) after 1 warm-up, "
+                                         f"oracle fp32 GeoT both chains + pair tensor, {dt:.1f}s"}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if ws > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,81 @@
+"""ctypes binding of the C ABI in include/deepinteract_amd.h.
+
+The product path has no fallback: if the HIP library cannot be loaded every op raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+from . import build as _build
+
+DI_F32, DI_BF16 = 0, 1
+
+
+class DiGraph(ctypes.Structure):
+    _fields_ = [("num_nodes", ctypes.c_int32), ("num_edges", ctypes.c_int32),
+                ("src", ctypes.c_void_p), ("dst", ctypes.c_void_p), ("nbr", ctypes.c_void_p),
+                ("node_pos", ctypes.c_void_p), ("in_ptr", ctypes.c_void_p)]
+
+
+class DiGeoArgs(ctypes.Structure):
+    _fields_ = [("num_graphs", ctypes.c_int32), ("k", ctypes.c_int32), ("max_nodes", ctypes.c_int32),
+                ("node_off", ctypes.c_void_p), ("backbone", ctypes.c_void_p), ("amide_norm", ctypes.c_void_p),
+                ("dips", ctypes.c_void_p), ("knn_idx", ctypes.c_void_p), ("knn_d2", ctypes.c_void_p),
+                ("node_f", ctypes.c_void_p), ("edge_f", ctypes.c_void_p), ("stats", ctypes.c_void_p)]
+
+
+class DiPairDesc(ctypes.Structure):
+    _fields_ = [("h1_row", ctypes.c_int64), ("h2_row", ctypes.c_int64), ("out_off", ctypes.c_int64),
+                ("l1", ctypes.c_int32), ("l2", ctypes.c_int32)]
+
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int32
+_SIGS = {
+    "di_abi_version": ([], ctypes.c_int),
+    "di_blob_bytes": ([ctypes.c_int, ctypes.c_int, ctypes.c_int], ctypes.c_int64),
+    "di_node_embed": ([ctypes.POINTER(DiGraph), _I, _I, _P, _P, _P, _P, _P, _P], ctypes.c_int),
+    "di_init_edge": ([ctypes.POINTER(DiGraph), _I, _P, _P, _P, _P, _P, _P, _P, _P], ctypes.c_int),
+    "di_edge_layer": ([ctypes.POINTER(DiGraph), _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
+                      ctypes.c_int),
+    "di_node_layer": ([ctypes.POINTER(DiGraph), _I, _I, _P, _P, _P, _P, _P, _P, _P, _P], ctypes.c_int),
+    "di_pair_tensor": ([_I, _P, _I, _I, _I, _I, _I, _P, _P, _P], ctypes.c_int),
+    "di_knn_topk": ([_I, _P, _P, _I, _I, _P, _P, _P], ctypes.c_int),
+    "di_geo_feats": ([ctypes.POINTER(DiGeoArgs), _P], ctypes.c_int),
+    "di_build_nbr_ids": ([_I, _P, _P, _P, ctypes.c_uint64, _P, _P], ctypes.c_int),
+}
+
+_lib = None
+
+
+def library_path() -> str:
+    return _build.LIB
+
+
+def load(build_if_missing: bool = True):
+    """Load (building first if needed) the HIP library; raises if it is unavailable."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    # torch ships its own libamdhip64.so.7: load it first so this library binds to the SAME HIP
+    # runtime (same SONAME) instead of pulling /opt/rocm's copy into the process.
+    import torch  # noqa: F401
+    if not os.path.exists(_build.LIB) or (build_if_missing and not _build.up_to_date()):
+        if not build_if_missing:
+            raise RuntimeError(f"deepinteract_amd HIP library missing: {_build.LIB}")
+        _build.build()
+    lib = ctypes.CDLL(_build.LIB)
+    for name, (argtypes, restype) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.argtypes = argtypes
+        fn.restype = restype
+    if lib.di_abi_version() != 1:
+        raise RuntimeError("deepinteract_amd ABI version mismatch")
+    _lib = lib
+    return lib
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        raise RuntimeError(f"{what} failed with code {rc}")

@@ -1,0 +1,67 @@
+"""Build the in-tree HIP shared library for gfx950: deepinteract_amd/lib/libdeepinteract_amd.so.
+
+Plain ``hipcc -shared -fPIC --offload-arch=gfx950`` over every csrc/*.hip file (one
+translation unit each, compiled in parallel, then linked). The .so lives in-tree so it
+travels to the GPU box with the repo snapshot.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import glob
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+LIBDIR = os.path.join(HERE, "lib")
+LIB = os.path.join(LIBDIR, "libdeepinteract_amd.so")
+ARCH = os.environ.get("DI_OFFLOAD_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
+          f"-I{os.path.join(os.path.dirname(HERE), 'include')}"]
+
+
+def _sources():
+    return sorted(glob.glob(os.path.join(CSRC, "*.hip")))
+
+
+def _deps():
+    return _sources() + sorted(glob.glob(os.path.join(CSRC, "*.h"))) + \
+        [os.path.join(os.path.dirname(HERE), "include", "deepinteract_amd.h")]
+
+
+def up_to_date() -> bool:
+    if not os.path.exists(LIB):
+        return False
+    t = os.path.getmtime(LIB)
+    return all(os.path.getmtime(p) <= t for p in _deps())
+
+
+def build(force: bool = False, verbose: bool = True) -> str:
+    if not force and up_to_date():
+        return LIB
+    os.makedirs(os.path.join(LIBDIR, "obj"), exist_ok=True)
+    objs = []
+
+    def compile_one(src):
+        obj = os.path.join(LIBDIR, "obj", os.path.basename(src).replace(".hip", ".o"))
+        cmd = [HIPCC, *CFLAGS, "-c", src, "-o", obj]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr}")
+        return obj
+
+    with cf.ThreadPoolExecutor(max_workers=min(8, len(_sources()))) as ex:
+        objs = list(ex.map(compile_one, _sources()))
+    cmd = [HIPCC, "-shared", f"--offload-arch={ARCH}", "-o", LIB, *objs]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"link failed:\n{r.stderr}")
+    if verbose:
+        print(f"built {LIB}", file=sys.stderr)
+    return LIB
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv)

@@ -1,0 +1,259 @@
+// Shared device toolkit for the GeoT kernels (gfx950 / CDNA4).
+//
+// "Row-on-lane" activation engine
+// -------------------------------
+// Every GeoT kernel is a chain of small dense layers applied row-wise (one row = one edge or
+// one node). A wave owns 16 rows: the row sits on the MFMA *column* (lane & 15) and the
+// features sit in the accumulator registers, i.e. each activation is held TRANSPOSED, exactly
+// as v_mfma_f32_16x16x{32_bf16,4_f32} writes its C/D tile (col = lane&15, row = 4*(lane>>4)+reg):
+//
+//     feature(block b, reg r, lane-group g = lane>>4) = 16*b + 4*g + r        (4 regs / block)
+//
+// A linear layer Y^T = W . X^T takes W as the A operand (streamed from LDS, packed on the host
+// in fragment order) and the previous accumulator X^T directly as the B operand: no LDS round
+// trip and no lane shuffles between chained layers (cdna_hip_programming.md §3, "An accumulator
+// tile as the next MFMA's operand"). A 128-feature activation costs 32 VGPRs per lane.
+// 16x16 tiles read exactly as many LDS weight bytes per MAC as 32x32 tiles (1 KiB of A per
+// 16K MAC) at half the activation registers, which is what sets occupancy here.
+//
+// The k-permutation implied by using an accumulator as B is baked into the host-side packing
+// (deepinteract_amd/packing.py). One packed block = 16 output rows x 32 input features =
+// 512 elements for both dtypes:
+//   bf16 16x16x32: [lane 0..63][j 0..7]          W[16bo + (lane&15)][32s + 16(j>>2) + 4(lane>>4) + (j&3)]
+//   f32  16x16x4 : [sub 0..1][lane 0..63][r 0..3] W[16bo + (lane&15)][32s + 16 sub + 4(lane>>4) + r]
+// Per-feature vectors (biases) are packed [b][g][r] (4 floats per lane group).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace di {
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef float floatx2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef uint16_t u16;
+
+constexpr int HID = 128;          // num_gnn_hidden_channels
+constexpr int NFEAT_E = 28;       // edge feature columns (FEATURE_INDICES)
+constexpr int NFEAT_N = 113;      // node feature columns
+constexpr int BLK = 512;          // elements per packed (16 out x 32 in) weight block
+constexpr int MAT128 = 32;        // blocks of a 128x128 matrix
+constexpr int ROWS_PER_WAVE = 16;
+constexpr int WAVES = 4;
+constexpr int ROWS_PER_BLOCK = ROWS_PER_WAVE * WAVES;
+constexpr int THREADS = 64 * WAVES;
+
+// ------------------------------------------------------------------ dtype traits
+struct F32T {
+  using T = float;
+  static constexpr bool kBF16 = false;
+};
+struct BF16T {
+  using T = u16;  // raw bf16 bits in memory
+  static constexpr bool kBF16 = true;
+};
+
+__device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
+  bf16x2 v = __builtin_convertvector((floatx2){a, b}, bf16x2);
+  return __builtin_bit_cast(uint32_t, v);
+}
+
+// 4 consecutive elements -> floatx4
+__device__ __forceinline__ floatx4 ld4(const float* p) { return *reinterpret_cast<const floatx4*>(p); }
+__device__ __forceinline__ floatx4 ld4(const u16* p) {
+  uint2 u = *reinterpret_cast<const uint2*>(p);
+  floatx4 r;
+  r[0] = __builtin_bit_cast(float, u.x << 16);
+  r[1] = __builtin_bit_cast(float, u.x & 0xffff0000u);
+  r[2] = __builtin_bit_cast(float, u.y << 16);
+  r[3] = __builtin_bit_cast(float, u.y & 0xffff0000u);
+  return r;
+}
+__device__ __forceinline__ void st4(float* p, floatx4 v) { *reinterpret_cast<floatx4*>(p) = v; }
+__device__ __forceinline__ void st4(u16* p, floatx4 v) {
+  uint2 u;
+  u.x = pack_bf16x2(v[0], v[1]);
+  u.y = pack_bf16x2(v[2], v[3]);
+  *reinterpret_cast<uint2*>(p) = u;
+}
+
+template <bool FAST>
+__device__ __forceinline__ float expf_(float x) {
+  if constexpr (FAST) return __expf(x);
+  else return expf(x);
+}
+template <bool FAST>
+__device__ __forceinline__ float silu(float x) { return x / (1.0f + expf_<FAST>(-x)); }
+
+// ------------------------------------------------------------------ activations
+template <int NB>  // NB blocks of 16 features
+struct Act {
+  floatx4 v[NB];
+};
+
+template <int NB>
+__device__ __forceinline__ void zero(Act<NB>& a) {
+#pragma unroll
+  for (int b = 0; b < NB; ++b) a.v[b] = (floatx4){0.f, 0.f, 0.f, 0.f};
+}
+
+// a = per-feature vector (packed [b][g][4], fp32)
+template <int NB>
+__device__ __forceinline__ void init_vec(Act<NB>& a, const float* vec, int g) {
+#pragma unroll
+  for (int b = 0; b < NB; ++b) a.v[b] = ld4(vec + (b * 4 + g) * 4);
+}
+
+template <int NB>
+__device__ __forceinline__ void add_vec(Act<NB>& a, const float* vec, int g) {
+#pragma unroll
+  for (int b = 0; b < NB; ++b) a.v[b] += ld4(vec + (b * 4 + g) * 4);
+}
+
+// row-major row (features 0 .. 16*NB-1) -> activation
+template <int NB, typename T>
+__device__ __forceinline__ void load_row(Act<NB>& a, const T* row, int g) {
+#pragma unroll
+  for (int b = 0; b < NB; ++b) a.v[b] = ld4(row + 16 * b + 4 * g);
+}
+
+template <int NB, typename T>
+__device__ __forceinline__ void add_row(Act<NB>& a, const T* row, int g) {
+#pragma unroll
+  for (int b = 0; b < NB; ++b) a.v[b] += ld4(row + 16 * b + 4 * g);
+}
+
+template <int NB, typename T>
+__device__ __forceinline__ void store_row(const Act<NB>& a, T* row, int g) {
+#pragma unroll
+  for (int b = 0; b < NB; ++b) st4(row + 16 * b + 4 * g, a.v[b]);
+}
+
+// edge feature row G [28] (fp32, 112-B rows) as a 32-feature activation, features 28..31 = 0
+__device__ __forceinline__ void load_edge_geo(Act<2>& a, const float* row, int g) {
+  a.v[0] = ld4(row + 4 * g);
+  a.v[1] = g == 3 ? (floatx4){0.f, 0.f, 0.f, 0.f} : ld4(row + 16 + 4 * g);
+}
+
+template <int NB, bool FAST>
+__device__ __forceinline__ void silu_(Act<NB>& a) {
+#pragma unroll
+  for (int b = 0; b < NB; ++b)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) a.v[b][r] = silu<FAST>(a.v[b][r]);
+}
+
+template <int NB>
+__device__ __forceinline__ void add_(Act<NB>& a, const Act<NB>& b_) {
+#pragma unroll
+  for (int b = 0; b < NB; ++b) a.v[b] += b_.v[b];
+}
+template <int NB>
+__device__ __forceinline__ void mul_(Act<NB>& a, const Act<NB>& b_) {
+#pragma unroll
+  for (int b = 0; b < NB; ++b) a.v[b] *= b_.v[b];
+}
+
+// ------------------------------------------------------------------ MFMA operands
+// NS = number of 32-feature k-steps (= NB / 2)
+template <class DT, int NS>
+struct Op;
+template <int NS>
+struct Op<BF16T, NS> {
+  bf16x8 f[NS];
+};
+template <int NS>
+struct Op<F32T, NS> {
+  floatx4 f[2 * NS];
+};
+
+template <int NS>
+__device__ __forceinline__ void make_op(Op<BF16T, NS>& o, const Act<2 * NS>& a) {
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    uint4 u;
+    u.x = pack_bf16x2(a.v[2 * s][0], a.v[2 * s][1]);
+    u.y = pack_bf16x2(a.v[2 * s][2], a.v[2 * s][3]);
+    u.z = pack_bf16x2(a.v[2 * s + 1][0], a.v[2 * s + 1][1]);
+    u.w = pack_bf16x2(a.v[2 * s + 1][2], a.v[2 * s + 1][3]);
+    o.f[s] = __builtin_bit_cast(bf16x8, u);
+  }
+}
+template <int NS>
+__device__ __forceinline__ void make_op(Op<F32T, NS>& o, const Act<2 * NS>& a) {
+#pragma unroll
+  for (int b = 0; b < 2 * NS; ++b) o.f[b] = a.v[b];
+}
+
+// out (NBO 16-row blocks) += W (NBO x NS packed blocks, in LDS) . op (NS 32-feature k-steps)
+template <int NBO, int NS>
+__device__ __forceinline__ void mma(Act<NBO>& out, const Op<BF16T, NS>& op, const u16* w, int lane) {
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+#pragma unroll
+    for (int bo = 0; bo < NBO; ++bo) {
+      const bf16x8 af = *reinterpret_cast<const bf16x8*>(w + (bo * NS + s) * BLK + lane * 8);
+      out.v[bo] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, op.f[s], out.v[bo], 0, 0, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);  // bound the LDS fragments in flight (register pressure)
+  }
+}
+template <int NBO, int NS>
+__device__ __forceinline__ void mma(Act<NBO>& out, const Op<F32T, NS>& op, const float* w, int lane) {
+#pragma unroll
+  for (int s = 0; s < NS; ++s)
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub) {
+#pragma unroll
+      for (int bo = 0; bo < NBO; ++bo) {
+        const floatx4 a4 = *reinterpret_cast<const floatx4*>(w + (bo * NS + s) * BLK + sub * 256 + lane * 4);
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          out.v[bo] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[r], op.f[2 * s + sub][r], out.v[bo], 0, 0, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+// convenience: out += W . a   (a has 2*NS blocks)
+template <class DT, int NBO, int NS>
+__device__ __forceinline__ void linear(Act<NBO>& out, const Act<2 * NS>& a, const typename DT::T* w, int lane) {
+  Op<DT, NS> op;
+  make_op(op, a);
+  mma<NBO, NS>(out, op, w, lane);
+}
+
+// ------------------------------------------------------------------ weight staging
+// Copy `nblk` packed blocks (512 elements each) from global memory to LDS with LDS-DMA
+// (global_load_lds_dwordx4: 1 KiB per wave-instruction, lane-linear destination = the packed
+// order). Called by all threads; the trailing barrier (s_waitcnt vmcnt(0) + s_barrier) waits
+// for the DMA.
+template <typename T>
+__device__ __forceinline__ void stage(T* lds, const T* g, int nblk) {
+  __syncthreads();  // previous readers of the buffer are done
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int nkib = nblk * BLK * (int)sizeof(T) / 1024;
+  for (int i = wave; i < nkib; i += WAVES) {
+    const char* src = reinterpret_cast<const char*>(g) + i * 1024 + lane * 16;
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                     (__attribute__((address_space(3))) void*)(reinterpret_cast<char*>(lds) + i * 1024),
+                                     16, 0, 0);
+  }
+  __syncthreads();
+}
+
+// sum of the 32 features of head h (= blocks 2h, 2h+1) for this lane's row
+template <int NB>
+__device__ __forceinline__ float head_sum(const Act<NB>& a, int h) {
+  float s = 0.f;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) s += a.v[2 * h][r];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) s += a.v[2 * h + 1][r];
+  s += __shfl_xor(s, 16);
+  s += __shfl_xor(s, 32);
+  return s;
+}
+
+}  // namespace di

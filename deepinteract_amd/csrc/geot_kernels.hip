@@ -1,0 +1,511 @@
+// GeoT forward kernels for gfx950 (MI355X): node embedding, InitEdge, fused edge layer,
+// fused node layer. Device engine: common.h ("row-on-lane" transposed activations,
+// MFMA 16x16 chains with weights streamed through LDS by LDS-DMA).
+//
+// Reference semantics (paths relative to /root/reference/project/utils/):
+//   node embedding            deepinteract_modules.py:1541-1543, 1663-1664
+//   InitEdgeModule            deepinteract_modules.py:198-264
+//   ConformationModule        deepinteract_modules.py:373-455 (+ ResBlock :458-497)
+//   attention edge UDFs       deepinteract_modules.py:76-96, graph_utils.py:21-63
+//   GT layer residual / FFN   deepinteract_modules.py:669-727 (intermediate), :892-946 (final)
+// Algebraic rewrites (exact in real arithmetic, fp32-rounding-level differences only):
+//   * eval BatchNorm folded into the following/preceding linear (host packing);
+//   * nbr_linear applied once per edge (Fn = F W^T + b) and gathered, instead of per gathered row;
+//   * two-stage geometric embeddings (W1 . W0 . g) pre-multiplied on the host;
+//   * InitEdge's emb[src]/emb[dst] slots of combined_linear_0 precomputed per node position
+//     (pos tables [2304,128]); the 4 final gates summed before multiplying (a*x+b*x = (a+b)*x).
+#include "common.h"
+#include "layout.h"
+#include "../../include/deepinteract_amd.h"
+
+namespace di {
+
+struct EmbedArgs {
+  int Nt;
+  int in_dim;
+  const float* node_f;
+  const void* wmat;
+  const float* wvec;
+  void* h_out;
+  void* qkv_out;
+};
+
+struct InitArgs {
+  int Et;
+  const float* edge_f;
+  const int* src;
+  const int* dst;
+  const int* node_pos;
+  const void* wmat;
+  const float* wvec;
+  const float* pos_src;
+  const float* pos_dst;
+  void* f_out;
+  void* fn_out;
+};
+
+struct EdgeArgs {
+  int Et;
+  const float* edge_f;
+  const int* src;
+  const int* dst;
+  const int* nbr;
+  const void* f_in;
+  const void* fn_in;
+  const void* qkv;
+  const void* wmat;
+  const float* wvec;
+  float* alpha_out;
+  void* f_out;
+  void* fn_out;
+};
+
+struct NodeArgs {
+  int Nt;
+  const int* src;
+  const int* in_ptr;
+  const float* alpha;
+  const void* h_in;
+  const void* qkv;
+  const void* wmat;
+  const float* wvec;
+  void* h_out;
+  void* qkv_out;
+};
+
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+__device__ __forceinline__ int row_id() {
+  return blockIdx.x * ROWS_PER_BLOCK + (threadIdx.x >> 6) * ROWS_PER_WAVE + (threadIdx.x & 15);
+}
+
+// ================================================================ node embedding (+ Q/K/V of layer 0)
+template <class DT>
+__global__ __launch_bounds__(THREADS) void k_node_embed(EmbedArgs a) {
+  using T = typename DT::T;
+  __shared__ __attribute__((aligned(16))) T wst[MAT128 * BLK];
+  const int lane = lane_id(), g = lane >> 4;
+  const int r = row_id();
+  const bool valid = r < a.Nt;
+  const int v = valid ? r : a.Nt - 1;
+  const T* W = reinterpret_cast<const T*>(a.wmat);
+
+  Act<8> x;  // in_dim (113 raw DIPS-Plus + geometric features) input columns, zero padded to 128
+  const float* row = a.node_f + (int64_t)v * a.in_dim;
+#pragma unroll
+  for (int b = 0; b < 8; ++b)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int f = 16 * b + 4 * g + q;
+      x.v[b][q] = f < a.in_dim ? row[f] : 0.f;
+    }
+  stage(wst, W + EM_EMB * BLK, MAT128);
+  Act<8> h;
+  zero(h);
+  linear<DT, 8, 4>(h, x, wst, lane);
+  if (valid) store_row(h, reinterpret_cast<T*>(a.h_out) + (int64_t)v * HID, g);
+  T* qkv = reinterpret_cast<T*>(a.qkv_out);
+#pragma unroll 1
+  for (int q = 0; q < 3; ++q) {
+    stage(wst, W + (EM_Q + MAT128 * q) * BLK, MAT128);
+    Act<8> t;
+    init_vec(t, a.wvec + EMV_Q + 128 * q, g);
+    linear<DT, 8, 4>(t, h, wst, lane);
+    if (valid) store_row(t, qkv + (int64_t)v * 3 * HID + q * HID, g);
+  }
+}
+
+// ================================================================ InitEdgeModule (+ layer-0 nbr_linear)
+template <class DT>
+__global__ __launch_bounds__(THREADS) void k_init_edge(InitArgs a) {
+  using T = typename DT::T;
+  constexpr bool FAST = DT::kBF16;
+  __shared__ __attribute__((aligned(16))) T wst[40 * BLK];
+  const int lane = lane_id(), g = lane >> 4;
+  const int r = row_id();
+  const bool valid = r < a.Et;
+  const int e = valid ? r : a.Et - 1;
+  const T* W = reinterpret_cast<const T*>(a.wmat);
+
+  Act<2> geo;
+  load_edge_geo(geo, a.edge_f + (int64_t)e * NFEAT_E, g);
+  Op<DT, 1> gop;
+  make_op(gop, geo);
+
+  // combined_linear_0 over [emb[src], emb[dst], em0, silu(d0), silu(r0), silu(o0), silu(a0)]
+  Act<8> acc;
+  load_row(acc, a.pos_src + (int64_t)a.node_pos[a.src[e]] * HID, g);
+  add_row(acc, a.pos_dst + (int64_t)a.node_pos[a.dst[e]] * HID, g);
+#pragma unroll 1
+  for (int t = 0; t < 5; ++t) {
+    stage(wst, W + (IE_T0 + 40 * t) * BLK, 40);
+    Act<8> y;
+    zero(y);
+    mma<8, 1>(y, gop, wst, lane);
+    if (t > 0) silu_<8, FAST>(y);
+    linear<DT, 8, 4>(acc, y, wst + 8 * BLK, lane);
+  }
+  silu_<8, FAST>(acc);  // combined_edge_logits
+  // gating: (em1 + silu(d1) + silu(r1) + silu(o1) + silu(a1)) * c
+  stage(wst, W + IE_GEO1 * BLK, 40);
+  Act<8> gs;
+  zero(gs);
+#pragma unroll 1
+  for (int t = 0; t < 5; ++t) {
+    Act<8> y;
+    zero(y);
+    mma<8, 1>(y, gop, wst + 8 * t * BLK, lane);
+    if (t > 0) silu_<8, FAST>(y);
+    add_(gs, y);
+  }
+  mul_(acc, gs);
+  // combined_linear_2(combined_linear_1(.)) : 128 -> 28 (padded 32) -> 128
+  stage(wst, W + IE_C1 * BLK, 16);
+  Act<2> z;
+  zero(z);
+  linear<DT, 2, 4>(z, acc, wst, lane);
+  Act<8> f;
+  zero(f);
+  linear<DT, 8, 1>(f, z, wst + 8 * BLK, lane);
+  if (valid) store_row(f, reinterpret_cast<T*>(a.f_out) + (int64_t)e * HID, g);
+  // layer-0 nbr_linear, applied once per edge (gathered by the conformation module)
+  stage(wst, W + IE_NBR * BLK, MAT128);
+  Act<8> fn;
+  init_vec(fn, a.wvec + IEV_NBR, g);
+  linear<DT, 8, 4>(fn, f, wst, lane);
+  if (valid) store_row(fn, reinterpret_cast<T*>(a.fn_out) + (int64_t)e * HID, g);
+}
+
+// ================================================================ fused edge layer
+template <class DT>
+__device__ __forceinline__ void res_block(Act<8>& x, const typename DT::T* W, const float* V, int idx,
+                                          typename DT::T* wst, int lane, int g) {
+  constexpr bool FAST = DT::kBF16;
+  Act<8> y = x;
+#pragma unroll 1
+  for (int l = 0; l < 3; ++l) {
+    stage(wst, W + (EL_RES + MAT128 * (3 * idx + l)) * BLK, MAT128);
+    Act<8> t;
+    init_vec(t, V + ELV_RES + 128 * (3 * idx + l), g);
+    linear<DT, 8, 4>(t, y, wst, lane);
+    silu_<8, FAST>(t);
+    y = t;
+  }
+  add_(x, y);
+}
+
+template <class DT, bool FINAL>
+__global__ __launch_bounds__(THREADS) void k_edge_layer(EdgeArgs a) {
+  using T = typename DT::T;
+  constexpr bool FAST = DT::kBF16;
+  __shared__ __attribute__((aligned(16))) T lds[60 * BLK];
+  T* wst = lds;                 // 32-block staging buffer
+  T* wg = lds + MAT128 * BLK;   // resident geometric projections (28 blocks)
+  const int lane = lane_id(), g = lane >> 4;
+  const int r = row_id();
+  const bool valid = r < a.Et;
+  const int e = valid ? r : a.Et - 1;
+  const T* W = reinterpret_cast<const T*>(a.wmat);
+  const float* V = a.wvec;
+  const T* f_in = reinterpret_cast<const T*>(a.f_in);
+  const T* fn_in = reinterpret_cast<const T*>(a.fn_in);
+  const T* qkv = reinterpret_cast<const T*>(a.qkv);
+  const T* f_row = f_in + (int64_t)e * HID;
+
+  stage(wg, W + EL_MG * BLK, 28);
+  Act<2> geo;
+  load_edge_geo(geo, a.edge_f + (int64_t)e * NFEAT_E, g);
+  Op<DT, 1> gop;
+  make_op(gop, geo);
+
+  // ---- neighbour-edge messages (conformation_module_message_func :384-418)
+  Act<4> gate;  // dir . orient . amide embeddings (64)
+  {
+    Act<4> t1;
+    zero(gate);
+    mma<4, 1>(gate, gop, wg + 8 * BLK, lane);
+    zero(t1);
+    mma<4, 1>(t1, gop, wg + 12 * BLK, lane);
+    mul_(gate, t1);
+    zero(t1);
+    mma<4, 1>(t1, gop, wg + 16 * BLK, lane);
+    mul_(gate, t1);
+  }
+  stage(wst, W + EL_DOWN * BLK, 16);
+  Act<4> s;
+  zero(s);
+#pragma unroll 1
+  for (int j = 0; j < 4; ++j) {
+    const int ne = a.nbr[(int64_t)e * 4 + j];
+    Act<8> x;
+    load_row(x, fn_in + (int64_t)ne * HID, g);
+    Act<8> dg;
+    zero(dg);
+    mma<8, 1>(dg, gop, wg, lane);  // dist_linear_1(dist_linear_0(dist))
+#pragma unroll
+    for (int b = 0; b < 8; ++b)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) x.v[b][q] = silu<FAST>(x.v[b][q]) * dg.v[b][q];
+    Act<4> y;
+    zero(y);
+    linear<DT, 4, 4>(y, x, wst, lane);  // downward_proj
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) s.v[b][q] += silu<FAST>(y.v[b][q]) * gate.v[b][q];
+  }
+  stage(wst, W + EL_UP * BLK, 16);
+  Act<8> x;
+  zero(x);
+  linear<DT, 8, 2>(x, s, wst, lane);  // upward_proj
+  silu_<8, FAST>(x);
+  add_vec(x, V + ELV_OM, g);
+  stage(wst, W + EL_OM * BLK, MAT128);
+  {
+    Act<8> f;
+    load_row(f, f_row, g);
+    linear<DT, 8, 4>(x, f, wst, lane);  // orig_msg_linear(res) + nbr
+  }
+  res_block<DT>(x, W, V, 0, wst, lane, g);
+  res_block<DT>(x, W, V, 1, wst, lane, g);
+  {
+    stage(wst, W + EL_RC * BLK, MAT128);
+    Act<8> y;
+    init_vec(y, V + ELV_RC, g);
+    linear<DT, 8, 4>(y, x, wst, lane);
+    silu_<8, FAST>(y);
+    load_row(x, f_row, g);
+    add_(x, y);
+  }
+  res_block<DT>(x, W, V, 2, wst, lane, g);
+  res_block<DT>(x, W, V, 3, wst, lane, g);
+  {
+    Act<8> fg;
+    zero(fg);
+    mma<8, 1>(fg, gop, wg + 20 * BLK, lane);
+    mul_(x, fg);
+    stage(wst, W + EL_F * BLK, MAT128);
+    Act<8> y;
+    init_vec(y, V + ELV_F, g);
+    linear<DT, 8, 4>(y, x, wst, lane);
+    silu_<8, FAST>(y);
+    load_row(x, f_row, g);
+    add_(x, y);  // conformation output
+  }
+  // ---- attention scores (propagate_attention :76-91)
+  stage(wst, W + EL_P * BLK, MAT128);
+  Act<8> p;
+  init_vec(p, V + ELV_P, g);
+  linear<DT, 8, 4>(p, x, wst, lane);  // edge_feats_projection(BN1e(conf))
+  {
+    const int sn = a.src[e], dn = a.dst[e];
+    Act<8> kq, qd;
+    load_row(kq, qkv + (int64_t)sn * 3 * HID + HID, g);
+    load_row(qd, qkv + (int64_t)dn * 3 * HID, g);
+    const float scale = 5.656854249492381f;  // np.sqrt(32)
+#pragma unroll
+    for (int b = 0; b < 8; ++b)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        float sc = (kq.v[b][q] * qd.v[b][q]) / scale;
+        sc = fminf(fmaxf(sc, -5.f), 5.f);
+        p.v[b][q] = sc * p.v[b][q];  // score = e_out
+      }
+  }
+  floatx4 al;
+#pragma unroll
+  for (int h = 0; h < 4; ++h) al[h] = expf_<FAST>(fminf(fmaxf(head_sum(p, h), -5.f), 5.f));
+  if (valid && g == 0) st4(a.alpha_out + (int64_t)e * 4, al);
+
+  if constexpr (!FINAL) {
+    // ---- edge output: e = in + O_e(e_out); e = e + FFN(BN2e(e)) (:697-724)
+    stage(wst, W + EL_OE * BLK, MAT128);
+    Act<8> e1;
+    init_vec(e1, V + ELV_OE, g);
+    linear<DT, 8, 4>(e1, p, wst, lane);
+    add_row(e1, f_row, g);
+    Act<8> o;
+    zero(o);
+#pragma unroll 1
+    for (int half = 0; half < 2; ++half) {
+      stage(wst, W + (EL_F1 + MAT128 * half) * BLK, MAT128);
+      Act<8> t;
+      init_vec(t, V + ELV_F1 + 128 * half, g);
+      linear<DT, 8, 4>(t, e1, wst, lane);
+      silu_<8, FAST>(t);
+      stage(wst, W + (EL_F2 + MAT128 * half) * BLK, MAT128);
+      linear<DT, 8, 4>(o, t, wst, lane);
+    }
+    add_(e1, o);
+    if (valid) store_row(e1, reinterpret_cast<T*>(a.f_out) + (int64_t)e * HID, g);
+    stage(wst, W + EL_NN * BLK, MAT128);
+    Act<8> fn;
+    init_vec(fn, V + ELV_NN, g);
+    linear<DT, 8, 4>(fn, e1, wst, lane);
+    if (valid) store_row(fn, reinterpret_cast<T*>(a.fn_out) + (int64_t)e * HID, g);
+  }
+}
+
+// ================================================================ fused node layer
+template <class DT, bool FINAL>
+__global__ __launch_bounds__(THREADS) void k_node_layer(NodeArgs a) {
+  using T = typename DT::T;
+  constexpr bool FAST = DT::kBF16;
+  __shared__ __attribute__((aligned(16))) T wst[MAT128 * BLK];
+  const int lane = lane_id(), g = lane >> 4;
+  const int r = row_id();
+  const bool valid = r < a.Nt;
+  const int v = valid ? r : a.Nt - 1;
+  const T* W = reinterpret_cast<const T*>(a.wmat);
+  const float* V = a.wvec;
+  const T* qkv = reinterpret_cast<const T*>(a.qkv);
+
+  // send_and_recv(u_mul_e('V_h','score'), sum) and (copy_e('score'), sum); h = wV / (z + 1e-6)
+  Act<8> wv;
+  zero(wv);
+  floatx4 z = {0.f, 0.f, 0.f, 0.f};
+  const int e0 = a.in_ptr[v], e1 = a.in_ptr[v + 1];
+#pragma unroll 1
+  for (int e = e0; e < e1; ++e) {
+    const floatx4 al = ld4(a.alpha + (int64_t)e * 4);
+    Act<8> vv;
+    load_row(vv, qkv + (int64_t)a.src[e] * 3 * HID + 2 * HID, g);
+#pragma unroll
+    for (int b = 0; b < 8; ++b) wv.v[b] += al[b >> 1] * vv.v[b];
+    z += al;
+  }
+#pragma unroll
+  for (int b = 0; b < 8; ++b) {
+    const float d = z[b >> 1] + 1e-6f;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) wv.v[b][q] = wv.v[b][q] / d;
+  }
+  // n = in1 + O_node(h)
+  stage(wst, W + NL_ON * BLK, MAT128);
+  Act<8> n;
+  init_vec(n, V + NLV_ON, g);
+  linear<DT, 8, 4>(n, wv, wst, lane);
+  add_row(n, reinterpret_cast<const T*>(a.h_in) + (int64_t)v * HID, g);
+  // n = n + W2 silu(W1 BN2(n))
+  Act<8> o;
+  zero(o);
+#pragma unroll 1
+  for (int half = 0; half < 2; ++half) {
+    stage(wst, W + (NL_F1 + MAT128 * half) * BLK, MAT128);
+    Act<8> t;
+    init_vec(t, V + NLV_F1 + 128 * half, g);
+    linear<DT, 8, 4>(t, n, wst, lane);
+    silu_<8, FAST>(t);
+    stage(wst, W + (NL_F2 + MAT128 * half) * BLK, MAT128);
+    linear<DT, 8, 4>(o, t, wst, lane);
+  }
+  add_(n, o);
+  if (valid) store_row(n, reinterpret_cast<T*>(a.h_out) + (int64_t)v * HID, g);
+  if constexpr (!FINAL) {
+    T* qo = reinterpret_cast<T*>(a.qkv_out);
+#pragma unroll 1
+    for (int q = 0; q < 3; ++q) {
+      stage(wst, W + (NL_Q + MAT128 * q) * BLK, MAT128);
+      Act<8> t;
+      init_vec(t, V + NLV_Q + 128 * q, g);
+      linear<DT, 8, 4>(t, n, wst, lane);
+      if (valid) store_row(t, qo + (int64_t)v * 3 * HID + q * HID, g);
+    }
+  }
+}
+
+}  // namespace di
+
+// ================================================================ C ABI
+using namespace di;
+
+static inline int grid_rows(int n) { return (n + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK; }
+
+static inline int launch_status() {
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? DI_OK : (int)e;
+}
+
+extern "C" int di_abi_version(void) { return DI_ABI_VERSION; }
+
+extern "C" int64_t di_blob_bytes(int kind, di_dtype dtype, int vec) {
+  const int64_t esz = dtype == DI_BF16 ? 2 : 4;
+  int64_t blk = 0, nvec = 0;
+  switch (kind) {
+    case 0: blk = EM_NBLK; nvec = EMV_N; break;
+    case 1: blk = IE_NBLK; nvec = IEV_N; break;
+    case 2: blk = EL_NBLK; nvec = ELV_N; break;
+    case 3: blk = EL_NBLK_FINAL; nvec = ELV_N_FINAL; break;
+    case 4: blk = NL_NBLK; nvec = NLV_N; break;
+    case 5: blk = NL_NBLK_FINAL; nvec = NLV_N_FINAL; break;
+    default: return -1;
+  }
+  return vec ? nvec * 4 : blk * BLK * esz;
+}
+
+extern "C" int di_node_embed(const di_graph* g, di_dtype dt, int32_t in_dim, const float* node_f, const void* wmat,
+                             const float* wvec, void* h_out, void* qkv_out, void* stream) {
+  if (!g || !node_f || !wmat || !wvec || !h_out || !qkv_out || g->num_nodes <= 0 || in_dim <= 0 || in_dim > HID)
+    return DI_EINVAL;
+  EmbedArgs a{g->num_nodes, in_dim, node_f, wmat, wvec, h_out, qkv_out};
+  hipStream_t s = (hipStream_t)stream;
+  if (dt == DI_BF16)
+    hipLaunchKernelGGL(k_node_embed<BF16T>, dim3(grid_rows(a.Nt)), dim3(THREADS), 0, s, a);
+  else
+    hipLaunchKernelGGL(k_node_embed<F32T>, dim3(grid_rows(a.Nt)), dim3(THREADS), 0, s, a);
+  return launch_status();
+}
+
+extern "C" int di_init_edge(const di_graph* g, di_dtype dt, const float* edge_f, const void* wmat,
+                            const float* wvec, const float* pos_src_tab, const float* pos_dst_tab,
+                            void* f_out, void* fn_out, void* stream) {
+  if (!g || !edge_f || !wmat || !wvec || !pos_src_tab || !pos_dst_tab || !f_out || !fn_out ||
+      g->num_edges <= 0)
+    return DI_EINVAL;
+  InitArgs a{g->num_edges, edge_f, g->src, g->dst, g->node_pos, wmat, wvec, pos_src_tab, pos_dst_tab,
+             f_out, fn_out};
+  hipStream_t s = (hipStream_t)stream;
+  if (dt == DI_BF16)
+    hipLaunchKernelGGL(k_init_edge<BF16T>, dim3(grid_rows(a.Et)), dim3(THREADS), 0, s, a);
+  else
+    hipLaunchKernelGGL(k_init_edge<F32T>, dim3(grid_rows(a.Et)), dim3(THREADS), 0, s, a);
+  return launch_status();
+}
+
+extern "C" int di_edge_layer(const di_graph* g, di_dtype dt, int final_layer, const float* edge_f,
+                             const void* f_in, const void* fn_in, const void* qkv, const void* wmat,
+                             const float* wvec, float* alpha_out, void* f_out, void* fn_out,
+                             void* stream) {
+  if (!g || !edge_f || !f_in || !fn_in || !qkv || !wmat || !wvec || !alpha_out || g->num_edges <= 0)
+    return DI_EINVAL;
+  if (!final_layer && (!f_out || !fn_out)) return DI_EINVAL;
+  EdgeArgs a{g->num_edges, edge_f, g->src, g->dst, g->nbr, f_in, fn_in, qkv, wmat, wvec, alpha_out,
+             f_out, fn_out};
+  hipStream_t s = (hipStream_t)stream;
+  dim3 grid(grid_rows(a.Et)), block(THREADS);
+  if (dt == DI_BF16) {
+    if (final_layer) hipLaunchKernelGGL((k_edge_layer<BF16T, true>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((k_edge_layer<BF16T, false>), grid, block, 0, s, a);
+  } else {
+    if (final_layer) hipLaunchKernelGGL((k_edge_layer<F32T, true>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((k_edge_layer<F32T, false>), grid, block, 0, s, a);
+  }
+  return launch_status();
+}
+
+extern "C" int di_node_layer(const di_graph* g, di_dtype dt, int final_layer, const float* alpha,
+                             const void* h_in, const void* qkv, const void* wmat, const float* wvec,
+                             void* h_out, void* qkv_out, void* stream) {
+  if (!g || !alpha || !h_in || !qkv || !wmat || !wvec || !h_out || g->num_nodes <= 0) return DI_EINVAL;
+  if (!final_layer && !qkv_out) return DI_EINVAL;
+  NodeArgs a{g->num_nodes, g->src, g->in_ptr, alpha, h_in, qkv, wmat, wvec, h_out, qkv_out};
+  hipStream_t s = (hipStream_t)stream;
+  dim3 grid(grid_rows(a.Nt)), block(THREADS);
+  if (dt == DI_BF16) {
+    if (final_layer) hipLaunchKernelGGL((k_node_layer<BF16T, true>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((k_node_layer<BF16T, false>), grid, block, 0, s, a);
+  } else {
+    if (final_layer) hipLaunchKernelGGL((k_node_layer<F32T, true>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((k_node_layer<F32T, false>), grid, block, 0, s, a);
+  }
+  return launch_status();
+}

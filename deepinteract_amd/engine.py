@@ -1,0 +1,186 @@
+"""GeoT forward on the HIP kernels (host sequencing of the C ABI).
+
+Per batch of chains (one launch per stage covers every chain of the batch):
+
+    di_node_embed                    h0, QKV(layer 0)
+    di_init_edge                     F0 = InitEdge(G), Fn0 = nbr_linear_0(F0)
+    for layer l < L-1:
+        di_edge_layer(intermediate)  alpha_l, F_{l+1}, Fn_{l+1}
+        di_node_layer(intermediate)  h_{l+1}, QKV(layer l+1)
+    di_edge_layer(final)             alpha_{L-1}
+    di_node_layer(final)             h_L
+
+This mirrors DGLGeometricTransformer.forward (deepinteract_modules.py:1426-1466): the
+returned edge features are the last INTERMEDIATE layer's (the final layer updates nodes only).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib
+from .config import GeoTConfig
+from .graph import GraphBatch
+from .packing import PackedGeoT
+
+_TORCH_DT = {"f32": torch.float32, "bf16": torch.bfloat16}
+_DI_DT = {"f32": _lib.DI_F32, "bf16": _lib.DI_BF16}
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+class _Ticker:
+    """Records (start, end) event pairs around consecutive launches on the current stream."""
+
+    def __init__(self, events):
+        self.events, self.name, self.start = events, None, None
+
+    def __call__(self, name):
+        if self.events is None:
+            return
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record()
+        if self.name is not None:
+            self.events.setdefault(self.name, []).append((self.start, ev))
+        self.name, self.start = name, ev
+
+
+class GeoTEngine:
+    """Holds packed device weights; runs the GeoT forward for a GraphBatch."""
+
+    def __init__(self, state_dict, dtype: str = "f32", cfg: GeoTConfig = GeoTConfig(), device="cuda"):
+        if not torch.cuda.is_available():
+            raise RuntimeError("deepinteract_amd GeoT kernels need a ROCm GPU (no CPU fallback)")
+        self.lib = _lib.load()
+        self.dtype, self.cfg = dtype, cfg
+        self.device = torch.device(device)
+        self.packed = PackedGeoT(state_dict, dtype, cfg, self.device)
+        self._check_blob_sizes()
+        self._ws = None
+        self._ws_key = None
+
+    def _check_blob_sizes(self):
+        p, dt = self.packed, _DI_DT[self.dtype]
+        L = p.num_layers
+        blobs = [(0, p.embed)] + [(1, p.init)] + \
+            [(3 if li == L - 1 else 2, p.edge[li]) for li in range(L)] + \
+            [(5 if li == L - 1 else 4, p.node[li]) for li in range(L)]
+        for kind, (mat, vec) in blobs:
+            want_m = self.lib.di_blob_bytes(kind, dt, 0)
+            want_v = self.lib.di_blob_bytes(kind, dt, 1)
+            got_m = mat.numel() * mat.element_size()
+            got_v = vec.numel() * vec.element_size()
+            if want_m != got_m or want_v != got_v:
+                raise RuntimeError(f"weight blob {kind} size mismatch: {got_m}/{got_v} vs {want_m}/{want_v}")
+
+    def workspace(self, num_nodes: int, num_edges: int):
+        key = (num_nodes, num_edges)
+        if self._ws_key != key:
+            dt, dev, H = _TORCH_DT[self.dtype], self.device, self.cfg.num_gnn_hidden_channels
+            self._ws = {
+                "h": [torch.empty(num_nodes, H, dtype=dt, device=dev) for _ in range(2)],
+                "qkv": [torch.empty(num_nodes, 3 * H, dtype=dt, device=dev) for _ in range(2)],
+                "f": [torch.empty(num_edges, H, dtype=dt, device=dev) for _ in range(2)],
+                "fn": [torch.empty(num_edges, H, dtype=dt, device=dev) for _ in range(2)],
+                "alpha": torch.empty(num_edges, 4, dtype=torch.float32, device=dev),
+            }
+            self._ws_key = key
+        return self._ws
+
+    def forward(self, gb: GraphBatch, clone: bool = True, events=None):
+        """-> (node feats [Nt,128], edge feats [Et,128]) in the engine dtype.
+
+        events: optional dict kernel-name -> list; (start, end) torch.cuda.Event pairs are recorded
+        around every launch on the launch stream (for per-kernel timing in bench.py)."""
+        lib, p, dt = self.lib, self.packed, _DI_DT[self.dtype]
+        ws = self.workspace(gb.num_nodes, gb.num_edges)
+        g = ctypes.byref(gb.c_graph)
+        st = _stream()
+        h, qkv, f, fn, alpha = ws["h"], ws["qkv"], ws["f"], ws["fn"], ws["alpha"]
+        tick = _Ticker(events)
+        tick("node_embed")
+        _lib.check(lib.di_node_embed(g, dt, gb.node_f.shape[1], _ptr(gb.node_f), _ptr(p.embed[0]), _ptr(p.embed[1]),
+                                     _ptr(h[0]), _ptr(qkv[0]), st), "di_node_embed")
+        tick("init_edge")
+        _lib.check(lib.di_init_edge(g, dt, _ptr(gb.edge_f), _ptr(p.init[0]), _ptr(p.init[1]),
+                                    _ptr(p.pos_src), _ptr(p.pos_dst), _ptr(f[0]), _ptr(fn[0]), st),
+                   "di_init_edge")
+        L = p.num_layers
+        cur = 0
+        for li in range(L):
+            final = li == L - 1
+            nxt = 1 - cur
+            em, ev = p.edge[li]
+            tick("edge_layer_final" if final else "edge_layer")
+            _lib.check(lib.di_edge_layer(g, dt, int(final), _ptr(gb.edge_f), _ptr(f[cur]), _ptr(fn[cur]),
+                                         _ptr(qkv[cur]), _ptr(em), _ptr(ev), _ptr(alpha),
+                                         _ptr(None if final else f[nxt]), _ptr(None if final else fn[nxt]),
+                                         st), "di_edge_layer")
+            nm, nv = p.node[li]
+            tick("node_layer_final" if final else "node_layer")
+            _lib.check(lib.di_node_layer(g, dt, int(final), _ptr(alpha), _ptr(h[cur]), _ptr(qkv[cur]),
+                                         _ptr(nm), _ptr(nv), _ptr(h[nxt]), _ptr(None if final else qkv[nxt]),
+                                         st), "di_node_layer")
+            if not final:
+                f_out = nxt
+            cur = nxt
+        tick(None)
+        node_out = h[cur]
+        edge_out = f[f_out] if L > 1 else f[0]
+        if clone:
+            return node_out.clone(), edge_out.clone()
+        return node_out, edge_out
+
+
+class PairTensorOp:
+    """construct_interact_tensor (deepinteract_utils.py:158-172) for a batch of complexes."""
+
+    def __init__(self, device="cuda"):
+        self.lib = _lib.load()
+        self.device = torch.device(device)
+        self._desc_cache = {}
+
+    def descs(self, h1_rows, h2_rows, l1s, l2s, hidden):
+        key = (tuple(h1_rows), tuple(h2_rows), tuple(l1s), tuple(l2s), hidden)
+        if key not in self._desc_cache:
+            arr = (_lib.DiPairDesc * len(l1s))()
+            off = 0
+            offs = []
+            for i, (a, b, l1, l2) in enumerate(zip(h1_rows, h2_rows, l1s, l2s)):
+                arr[i] = _lib.DiPairDesc(a, b, off, l1, l2)
+                offs.append(off)
+                off += 2 * hidden * l1 * l2
+            t = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8).to(self.device)
+            self._desc_cache[key] = (t, offs, off)
+        return self._desc_cache[key]
+
+    def __call__(self, h, h1_rows, h2_rows, l1s, l2s, out=None, events=None):
+        """h: [rows, H] node features (both chains of every complex). Returns a flat buffer and
+        the per-complex [1, 2H, L1, L2] views."""
+        hidden = h.shape[1]
+        dt = _lib.DI_BF16 if h.dtype == torch.bfloat16 else _lib.DI_F32
+        if h.dtype not in (torch.float32, torch.bfloat16):
+            raise TypeError(h.dtype)
+        d, offs, total = self.descs(h1_rows, h2_rows, l1s, l2s, hidden)
+        if out is None:
+            out = torch.empty(total, dtype=h.dtype, device=h.device)
+        elif out.numel() < total:
+            raise ValueError("pair-tensor output buffer too small")
+        vec = 16 // h.element_size()
+        aligned = all((l1 * l2) % vec == 0 for l1, l2 in zip(l1s, l2s)) and all(o % vec == 0 for o in offs) \
+            and out.data_ptr() % 16 == 0
+        tick = _Ticker(events)
+        tick("pair_tensor")
+        _lib.check(self.lib.di_pair_tensor(dt, _ptr(d), len(l1s), max(l1s), max(l2s), hidden, int(aligned),
+                                           _ptr(h.contiguous()), _ptr(out), _stream()), "di_pair_tensor")
+        tick(None)
+        views = [out[o:o + 2 * hidden * l1 * l2].view(1, 2 * hidden, l1, l2)
+                 for o, l1, l2 in zip(offs, l1s, l2s)]
+        return out, views

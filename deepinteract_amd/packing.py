@@ -1,0 +1,267 @@
+"""Host-side weight preparation: BatchNorm folding, algebraic pre-multiplication and packing
+into the MFMA fragment order the kernels stream (see csrc/common.h and csrc/layout.h).
+
+Everything is computed in float64 from a reference-keyed LitGINI state dict
+(deepinteract_modules.py:1478-1625 key names) and rounded once to the storage dtype.
+This is model-load-time work (like a checkpoint conversion), never on the timed path.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from .config import GeoTConfig
+
+BN_EPS = 1e-5
+BLK = 512
+
+# ---- csrc/layout.h mirror -------------------------------------------------------------------
+EM_NBLK, EMV_N = 128, 384
+IE_NBLK, IEV_N = 288, 128
+EL_NBLK, ELV_N = 764, 2560
+EL_NBLK_FINAL, ELV_N_FINAL = 572, 2048
+NL_NBLK, NLV_N = 256, 768
+NL_NBLK_FINAL, NLV_N_FINAL = 160, 384
+BLOB_SIZES = {0: (EM_NBLK, EMV_N), 1: (IE_NBLK, IEV_N), 2: (EL_NBLK, ELV_N),
+              3: (EL_NBLK_FINAL, ELV_N_FINAL), 4: (NL_NBLK, NLV_N), 5: (NL_NBLK_FINAL, NLV_N_FINAL)}
+
+
+def _np(t):
+    return t.detach().cpu().to(torch.float64).numpy()
+
+
+def pad2(w, rows, cols):
+    out = np.zeros((rows, cols), dtype=np.float64)
+    out[:w.shape[0], :w.shape[1]] = w
+    return out
+
+
+def _pack_index(dtype: str):
+    """(row, col) index arrays of one packed block, in storage order."""
+    lane = np.arange(64)
+    if dtype == "bf16":
+        j = np.arange(8)
+        row = np.broadcast_to((lane & 15)[:, None], (64, 8))
+        col = 16 * (j[None, :] >> 2) + 4 * (lane[:, None] >> 4) + (j[None, :] & 3)
+        return row.reshape(-1), col.reshape(-1)
+    sub, r = np.arange(2), np.arange(4)
+    row = np.broadcast_to((lane & 15)[None, :, None], (2, 64, 4))
+    col = 16 * sub[:, None, None] + 4 * (lane[None, :, None] >> 4) + r[None, None, :]
+    return row.reshape(-1), col.reshape(-1)
+
+
+def pack_matrix(w, dtype: str) -> np.ndarray:
+    """W [Nout, Kin] -> (Nout/16)*(Kin/32) blocks of 512 elements, block order (bo, s)."""
+    w = np.asarray(w, dtype=np.float64)
+    nout, kin = w.shape
+    assert nout % 16 == 0 and kin % 32 == 0, (nout, kin)
+    r, c = _pack_index(dtype)
+    nbo, ns = nout // 16, kin // 32
+    blocks = np.empty((nbo, ns, BLK), dtype=np.float64)
+    for bo in range(nbo):
+        for s in range(ns):
+            blocks[bo, s] = w[16 * bo + r, 32 * s + c]
+    return blocks.reshape(-1)
+
+
+def bn_affine(sd, name):
+    g, b = _np(sd[f"{name}.weight"]), _np(sd[f"{name}.bias"])
+    m, v = _np(sd[f"{name}.running_mean"]), _np(sd[f"{name}.running_var"])
+    s = g / np.sqrt(v + BN_EPS)
+    return s, b - m * s
+
+
+def lin(sd, name):
+    w = _np(sd[f"{name}.weight"])
+    b = _np(sd[f"{name}.bias"]) if f"{name}.bias" in sd else np.zeros(w.shape[0])
+    return w, b
+
+
+def fold_bn_before(w, b, s, t):
+    """Linear(BN(x)) = (W diag s) x + (W t + b)."""
+    return w * s[None, :], w @ t + b
+
+
+def fold_bn_after(w, b, s, t):
+    """BN(Linear(x)) = (diag s W) x + (s b + t)."""
+    return w * s[:, None], s * b + t
+
+
+class BlobBuilder:
+    def __init__(self, dtype: str, nblk: int, nvec: int):
+        self.dtype, self.nblk, self.nvec = dtype, nblk, nvec
+        self.mat = np.zeros(nblk * BLK, dtype=np.float64)
+        self.vec = np.zeros(nvec, dtype=np.float64)
+        self.used = np.zeros(nblk, dtype=bool)
+
+    def put(self, blk_off: int, w):
+        p = pack_matrix(w, self.dtype)
+        n = p.size // BLK
+        assert blk_off + n <= self.nblk, (blk_off, n, self.nblk)
+        assert not self.used[blk_off:blk_off + n].any(), blk_off
+        self.used[blk_off:blk_off + n] = True
+        self.mat[blk_off * BLK:(blk_off + n) * BLK] = p
+
+    def putv(self, off: int, v):
+        v = np.asarray(v, dtype=np.float64).reshape(-1)
+        assert off + v.size <= self.nvec
+        self.vec[off:off + v.size] = v
+
+    def finish(self):
+        assert self.used.all(), np.nonzero(~self.used)[0][:8]
+        t = torch.from_numpy(self.mat).to(torch.float32)
+        if self.dtype == "bf16":
+            t = t.to(torch.bfloat16)
+        return t, torch.from_numpy(self.vec).to(torch.float32)
+
+
+# ---- per-kernel blobs ---------------------------------------------------------------------------
+def _qkv(sd, li):
+    p = f"gnn_module.0.gt_block.{li}"
+    s, t = bn_affine(sd, f"{p}.batch_norm1_node_feats")
+    out = []
+    for q in ("Q", "K", "V"):
+        w, b = lin(sd, f"{p}.mha_module.{q}")
+        out.append(fold_bn_before(w, b, s, t))
+    return out
+
+
+def embed_blob(sd, dtype):
+    bb = BlobBuilder(dtype, EM_NBLK, EMV_N)
+    bb.put(0, pad2(_np(sd["node_in_embedding.weight"]), 128, 128))
+    for i, (w, b) in enumerate(_qkv(sd, 0)):
+        bb.put(32 + 32 * i, w)
+        bb.putv(128 * i, b)
+    return bb.finish()
+
+
+GEO_COLS = {"edge_messages": (0, 2), "dist": (2, 20), "dir": (20, 23), "orient": (23, 27), "amide": (27, 28)}
+GEO_ORDER = ("edge_messages", "dist", "dir", "orient", "amide")
+
+
+def _geo_rows(w, kind):
+    """[out, k_kind] weight placed on its columns of the 28 (padded 32) edge features."""
+    lo, hi = GEO_COLS[kind]
+    full = np.zeros((w.shape[0], 32))
+    full[:, lo:hi] = w
+    return full
+
+
+def init_blob(sd, dtype):
+    p = "gnn_module.0.init_edge_module"
+    bb = BlobBuilder(dtype, IE_NBLK, IEV_N)
+    wc0 = _np(sd[f"{p}.combined_linear_0.weight"])  # [128, 896]
+    for t, kind in enumerate(GEO_ORDER):
+        bb.put(40 * t, _geo_rows(_np(sd[f"{p}.{kind}_linear_0.weight"]), kind))
+        bb.put(40 * t + 8, wc0[:, 256 + 128 * t: 384 + 128 * t])
+        bb.put(200 + 8 * t, _geo_rows(_np(sd[f"{p}.{kind}_linear_1.weight"]), kind))
+    bb.put(240, pad2(_np(sd[f"{p}.combined_linear_1.weight"]), 32, 128))
+    bb.put(248, pad2(_np(sd[f"{p}.combined_linear_2.weight"]), 128, 32))
+    w, b = lin(sd, "gnn_module.0.gt_block.0.conformation_module.nbr_linear")
+    bb.put(256, w)
+    bb.putv(0, b)
+    mat, vec = bb.finish()
+    emb = _np(sd[f"{p}.node_embedding.weight"])
+    pos_src = torch.from_numpy(emb @ wc0[:, 0:128].T).to(torch.float32)
+    pos_dst = torch.from_numpy(emb @ wc0[:, 128:256].T).to(torch.float32)
+    return mat, vec, pos_src, pos_dst
+
+
+def edge_blob(sd, li, final, dtype, cfg: GeoTConfig):
+    p = f"gnn_module.0.gt_block.{li}"
+    c = f"{p}.conformation_module"
+    bb = BlobBuilder(dtype, EL_NBLK_FINAL if final else EL_NBLK, ELV_N_FINAL if final else ELV_N)
+    two = lambda a, b: _np(sd[f"{c}.{a}.weight"]) @ _np(sd[f"{c}.{b}.weight"])  # noqa: E731
+    mg = np.zeros((448, 32))
+    mg[0:128] = _geo_rows(two("dist_linear_1", "dist_linear_0"), "dist")
+    mg[128:192] = _geo_rows(two("dir_linear_1", "dir_linear_0"), "dir")
+    mg[192:256] = _geo_rows(two("orient_linear_1", "orient_linear_0"), "orient")
+    mg[256:320] = _geo_rows(two("amide_linear_1", "amide_linear_0"), "amide")
+    for kind, name in (("dist", "final_dist_linear"), ("dir", "final_dir_linear"),
+                       ("orient", "final_orient_linear"), ("amide", "final_amide_linear")):
+        mg[320:448] += _geo_rows(_np(sd[f"{c}.{name}.weight"]), kind)
+    bb.put(0, mg)
+    bb.put(28, _np(sd[f"{c}.downward_proj.weight"]))
+    bb.put(44, _np(sd[f"{c}.upward_proj.weight"]))
+    w, b = lin(sd, f"{c}.orig_msg_linear")
+    bb.put(60, w)
+    bb.putv(0, b)
+    i = 0
+    for kind in ("pre_res_blocks", "post_res_blocks"):
+        for rb in range(2):
+            r = f"{c}.{kind}.{rb}.res_block"
+            s, t = bn_affine(sd, f"{r}.1")  # one BatchNorm instance reused 3x (:468-479)
+            for l in (0, 3, 6):
+                w, b = lin(sd, f"{r}.{l}")
+                w, b = fold_bn_after(w, b, s, t)
+                bb.put(92 + 32 * i, w)
+                bb.putv(128 + 128 * i, b)
+                i += 1
+    w, b = lin(sd, f"{c}.res_connect_linear")
+    bb.put(476, w)
+    bb.putv(1664, b)
+    w, b = lin(sd, f"{c}.final_linear")
+    bb.put(508, w)
+    bb.putv(1792, b)
+    s, t = bn_affine(sd, f"{p}.batch_norm1_edge_feats")
+    w, b = fold_bn_before(*lin(sd, f"{p}.mha_module.edge_feats_projection"), s, t)
+    bb.put(540, w)
+    bb.putv(1920, b)
+    if not final:
+        w, b = lin(sd, f"{p}.O_edge_feats")
+        bb.put(572, w)
+        bb.putv(2048, b)
+        s, t = bn_affine(sd, f"{p}.batch_norm2_edge_feats")
+        w1, b1 = fold_bn_before(*lin(sd, f"{p}.edge_feats_MLP.0"), s, t)
+        bb.put(604, w1[:128])
+        bb.put(636, w1[128:])
+        bb.putv(2176, b1)
+        w2 = _np(sd[f"{p}.edge_feats_MLP.3.weight"])
+        bb.put(668, w2[:, :128])
+        bb.put(700, w2[:, 128:])
+        w, b = lin(sd, f"gnn_module.0.gt_block.{li + 1}.conformation_module.nbr_linear")
+        bb.put(732, w)
+        bb.putv(2432, b)
+    return bb.finish()
+
+
+def node_blob(sd, li, final, dtype):
+    p = f"gnn_module.0.gt_block.{li}"
+    bb = BlobBuilder(dtype, NL_NBLK_FINAL if final else NL_NBLK, NLV_N_FINAL if final else NLV_N)
+    w, b = lin(sd, f"{p}.O_node_feats")
+    bb.put(0, w)
+    bb.putv(0, b)
+    s, t = bn_affine(sd, f"{p}.batch_norm2_node_feats")
+    w1, b1 = fold_bn_before(*lin(sd, f"{p}.node_feats_MLP.0"), s, t)
+    bb.put(32, w1[:128])
+    bb.put(64, w1[128:])
+    bb.putv(128, b1)
+    w2 = _np(sd[f"{p}.node_feats_MLP.3.weight"])
+    bb.put(96, w2[:, :128])
+    bb.put(128, w2[:, 128:])
+    if not final:
+        for i, (w, b) in enumerate(_qkv(sd, li + 1)):
+            bb.put(160 + 32 * i, w)
+            bb.putv(384 + 128 * i, b)
+    return bb.finish()
+
+
+class PackedGeoT:
+    """All device-ready weight blobs of one DGLGeometricTransformer (+ node_in_embedding)."""
+
+    def __init__(self, sd, dtype: str = "f32", cfg: GeoTConfig = GeoTConfig(), device="cpu"):
+        assert dtype in ("f32", "bf16")
+        self.dtype, self.cfg = dtype, cfg
+        L = cfg.num_gnn_layers
+        dev = torch.device(device)
+        mv = lambda pair: tuple(x.to(dev).contiguous() for x in pair)  # noqa: E731
+        self.embed = mv(embed_blob(sd, dtype))
+        im, iv, ps, pd = init_blob(sd, dtype)
+        self.init = mv((im, iv))
+        self.pos_src, self.pos_dst = ps.to(dev).contiguous(), pd.to(dev).contiguous()
+        self.edge = [mv(edge_blob(sd, li, li == L - 1, dtype, cfg)) for li in range(L)]
+        self.node = [mv(node_blob(sd, li, li == L - 1, dtype)) for li in range(L)]
+
+    @property
+    def num_layers(self):
+        return len(self.edge)

@@ -1,0 +1,124 @@
+/*
+ * deepinteract_amd — C ABI of the MI355X (gfx950) GeoT hot path.
+ *
+ * Plain pointers and sizes only: every pointer argument is a DEVICE pointer unless stated;
+ * every call is asynchronous on `stream` (a hipStream_t passed as void*); no call allocates
+ * device memory; every call returns 0 or a hipError_t code (>0) or a negative DI_E* code.
+ *
+ * Each entry point replaces one piece of the reference's DGL/ATen hot path (file:line cited
+ * relative to /root/reference/project/utils/):
+ *
+ *   di_node_embed   LitGINI.gnn_forward node_in_embedding            deepinteract_modules.py:1663-1664
+ *                   + layer-0 Q/K/V of MultiHeadGeometricAttention   deepinteract_modules.py:101-103
+ *   di_init_edge    InitEdgeModule.forward / message UDF             deepinteract_modules.py:198-264
+ *   di_edge_layer   ConformationModule (:373-455) + attention edge UDFs (:76-91, graph_utils.py:21-63)
+ *                   + O_edge/edge FFN of GeometricTransformerModule  deepinteract_modules.py:669-727
+ *   di_node_layer   send_and_recv(u_mul_e/copy_e, sum) gSpMM         deepinteract_modules.py:93-96,116
+ *                   + O_node / node FFN                               deepinteract_modules.py:696-723, 923-943
+ *   di_pair_tensor  construct_interact_tensor (pad=False)            deepinteract_utils.py:158-172
+ *   di_knn_topk     dgl.knn_graph + topk(pairwise_squared_distance)  graph_utils.py:107-108
+ *   di_geo_feats    GeometricProteinFeatures('full') + edge/node feature assembly
+ *                                                                    protein_feature_utils.py:322-377,
+ *                                                                    deepinteract_utils.py:474-530
+ *   di_build_nbr_ids  per-edge neighbour-edge ids                    deepinteract_utils.py:534-553
+ */
+#ifndef DEEPINTERACT_AMD_H
+#define DEEPINTERACT_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DI_ABI_VERSION 1
+
+/* activation / weight storage type of the GeoT kernels (accumulation is always fp32) */
+typedef enum { DI_F32 = 0, DI_BF16 = 1 } di_dtype;
+
+enum {
+  DI_OK = 0,
+  DI_EINVAL = -1,   /* bad shape / null pointer / unsupported config */
+  DI_ERANGE = -2,   /* a chain exceeds NODE_COUNT_LIMIT (reference raises IndexError) */
+};
+
+/* A batch of residue graphs (one graph per chain, concatenated). Edges are destination-major:
+ * the in-edges of node v are edge ids in_ptr[v] .. in_ptr[v+1]-1. All ids are GLOBAL to the batch. */
+typedef struct {
+  int32_t num_nodes;        /* Nt */
+  int32_t num_edges;        /* Et */
+  const int32_t* src;       /* [Et] source node of each edge */
+  const int32_t* dst;       /* [Et] destination node of each edge */
+  const int32_t* nbr;       /* [Et,4] src_nbr_e_ids[0:2], dst_nbr_e_ids[0:2] */
+  const int32_t* node_pos;  /* [Nt] node index inside its chain (positional-embedding row) */
+  const int32_t* in_ptr;    /* [Nt+1] CSR row pointer of in-edges by destination */
+} di_graph;
+
+/* one complex of a pair-tensor launch (host-built array copied to the device) */
+typedef struct {
+  int64_t h1_row;   /* first node row of chain 1 in the node-feature matrix */
+  int64_t h2_row;   /* first node row of chain 2 */
+  int64_t out_off;  /* element offset of this complex's [2H, L1, L2] block in `out` */
+  int32_t l1, l2;
+} di_pair_desc;
+
+int di_abi_version(void);
+/* bytes of the packed weight blobs a kernel expects: kind = 0 embed, 1 init_edge,
+ * 2 edge_layer(non-final), 3 edge_layer(final), 4 node_layer(non-final), 5 node_layer(final).
+ * `vec` selects the fp32 vector blob (biases) instead of the matrix blob. */
+int64_t di_blob_bytes(int kind, di_dtype dtype, int vec);
+
+/* in_dim: width of node_f rows (113 for LitGINI's raw node features; 128 with an identity
+ * embedding when DGLGeometricTransformer is used standalone on already-embedded features) */
+int di_node_embed(const di_graph* g, di_dtype dt, int32_t in_dim, const float* node_f /*[Nt,in_dim]*/,
+                  const void* wmat, const float* wvec,
+                  void* h_out /*[Nt,128]*/, void* qkv_out /*[Nt,384]*/, void* stream);
+
+int di_init_edge(const di_graph* g, di_dtype dt, const float* edge_f /*[Et,28]*/,
+                 const void* wmat, const float* wvec,
+                 const float* pos_src_tab /*[2304,128]*/, const float* pos_dst_tab /*[2304,128]*/,
+                 void* f_out /*[Et,128]*/, void* fn_out /*[Et,128]*/, void* stream);
+
+int di_edge_layer(const di_graph* g, di_dtype dt, int final_layer, const float* edge_f,
+                  const void* f_in, const void* fn_in, const void* qkv,
+                  const void* wmat, const float* wvec,
+                  float* alpha_out /*[Et,4]*/, void* f_out, void* fn_out, void* stream);
+
+int di_node_layer(const di_graph* g, di_dtype dt, int final_layer, const float* alpha,
+                  const void* h_in, const void* qkv, const void* wmat, const float* wvec,
+                  void* h_out, void* qkv_out, void* stream);
+
+/* aligned16 != 0 promises every L1*L2 plane and out_off is a multiple of 16 bytes (vector stores) */
+int di_pair_tensor(di_dtype dt, const di_pair_desc* descs /*device [B]*/, int32_t num_complexes,
+                   int32_t max_l1, int32_t max_l2, int32_t hidden, int32_t aligned16, const void* h,
+                   void* out, void* stream);
+
+/* ---- graph builder ----------------------------------------------------------------------- */
+/* Cα kNN per chain: idx_out [Nt,k] chain-local neighbour ids (ascending squared distance,
+ * self first), d2_out [Nt,k] the expansion-formula squared distances. node_off [G+1] device. */
+int di_knn_topk(int32_t num_graphs, const int32_t* node_off, const float* ca /*[Nt,3]*/, int32_t k,
+                int32_t max_nodes, int32_t* idx_out, float* d2_out, void* stream);
+
+typedef struct {
+  int32_t num_graphs, k, max_nodes;
+  const int32_t* node_off;   /* [G+1] */
+  const float* backbone;     /* [Nt,4,3] N, CA, C, O */
+  const float* amide_norm;   /* [Nt,3] */
+  const float* dips;         /* [Nt,106] DIPS-Plus residue features */
+  const int32_t* knn_idx;    /* [Nt,k] chain-local (di_knn_topk) */
+  const float* knn_d2;       /* [Nt,k] */
+  float* node_f;             /* out [Nt,113] */
+  float* edge_f;             /* out [Nt*k,28] */
+  float* stats;              /* workspace [G,4] */
+} di_geo_args;
+int di_geo_feats(const di_geo_args* args, void* stream);
+
+/* neighbour-edge ids: 2 distinct in-edges of src(e) and of dst(e), uniform, counter-based RNG
+ * (seed, e); nbr_out [Et,4] global edge ids in the di_graph.nbr layout. */
+int di_build_nbr_ids(int32_t num_edges, const int32_t* src, const int32_t* dst, const int32_t* in_ptr,
+                     uint64_t seed, int32_t* nbr_out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DEEPINTERACT_AMD_H */

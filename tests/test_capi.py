@@ -1,0 +1,46 @@
+"""The C-ABI library builds for gfx950, loads, and exports every entry point that
+include/deepinteract_amd.h declares (no compute calls: there is no GPU here)."""
+import ctypes
+import os
+import re
+
+from deepinteract_amd import _lib, build, packing
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_symbols():
+    src = open(os.path.join(ROOT, "include", "deepinteract_amd.h")).read()
+    return sorted(set(re.findall(r"\b(di_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_builds_and_exports_all_declared_symbols():
+    path = build.build()
+    lib = ctypes.CDLL(path)
+    syms = declared_symbols()
+    assert len(syms) >= 10
+    for s in syms:
+        assert hasattr(lib, s), s
+
+
+def test_abi_version_and_blob_sizes():
+    lib = _lib.load()
+    assert lib.di_abi_version() == 1
+    for kind, (nblk, nvec) in packing.BLOB_SIZES.items():
+        assert lib.di_blob_bytes(kind, _lib.DI_F32, 0) == nblk * 512 * 4
+        assert lib.di_blob_bytes(kind, _lib.DI_BF16, 0) == nblk * 512 * 2
+        assert lib.di_blob_bytes(kind, _lib.DI_F32, 1) == nvec * 4
+    assert lib.di_blob_bytes(9, _lib.DI_F32, 0) == -1
+
+
+def test_invalid_arguments_rejected_without_gpu():
+    lib = _lib.load()
+    assert lib.di_node_embed(None, 0, 113, None, None, None, None, None, None) == -1
+    assert lib.di_pair_tensor(0, None, 0, 0, 0, 128, 1, None, None, None) == -1
+    assert lib.di_knn_topk(1, None, None, 20, 10, None, None, None) == -1
+
+
+def test_ctypes_struct_layouts():
+    assert ctypes.sizeof(_lib.DiGraph) == 8 + 5 * 8
+    assert ctypes.sizeof(_lib.DiPairDesc) == 32
+    assert ctypes.sizeof(_lib.DiGeoArgs) == 16 + 8 * 9

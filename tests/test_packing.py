@@ -1,0 +1,97 @@
+"""CPU checks of the MFMA fragment packing (csrc/common.h): emulate the gfx950 lane maps of
+v_mfma_f32_16x16x32_bf16 and v_mfma_f32_16x16x4_f32 exactly as the ISA defines them and check
+that a packed weight times an activation held in the row-on-lane layout equals W @ x."""
+import numpy as np
+import pytest
+import torch
+
+from deepinteract_amd import packing
+
+
+def act_from_rows(x):
+    """x [16 rows, F] -> act[lane][block][r] with feature 16*b + 4*(lane>>4) + r of row lane&15."""
+    F = x.shape[1]
+    act = np.zeros((64, F // 16, 4))
+    for lane in range(64):
+        for b in range(F // 16):
+            for r in range(4):
+                act[lane, b, r] = x[lane & 15, 16 * b + 4 * (lane >> 4) + r]
+    return act
+
+
+def rows_from_act(act):
+    F = act.shape[1] * 16
+    x = np.zeros((16, F))
+    for lane in range(64):
+        for b in range(act.shape[1]):
+            for r in range(4):
+                x[lane & 15, 16 * b + 4 * (lane >> 4) + r] = act[lane, b, r]
+    return x
+
+
+def emulate_bf16(packed, nbo, ns, act):
+    out = np.zeros((64, nbo, 4))
+    for s in range(ns):
+        bop = np.concatenate([act[:, 2 * s, :], act[:, 2 * s + 1, :]], axis=1)  # [64, 8]
+        B = np.zeros((32, 16))
+        for lane in range(64):
+            for j in range(8):
+                B[8 * (lane >> 4) + j, lane & 15] = bop[lane, j]
+        for bo in range(nbo):
+            blk = packed[(bo * ns + s) * 512:(bo * ns + s + 1) * 512].reshape(64, 8)
+            A = np.zeros((16, 32))
+            for lane in range(64):
+                for j in range(8):
+                    A[lane & 15, 8 * (lane >> 4) + j] = blk[lane, j]
+            D = A @ B
+            for lane in range(64):
+                for r in range(4):
+                    out[lane, bo, r] += D[4 * (lane >> 4) + r, lane & 15]
+    return out
+
+
+def emulate_f32(packed, nbo, ns, act):
+    out = np.zeros((64, nbo, 4))
+    for s in range(ns):
+        for sub in range(2):
+            b = 2 * s + sub
+            for r_k in range(4):
+                B = np.zeros((4, 16))
+                for lane in range(64):
+                    B[lane >> 4, lane & 15] = act[lane, b, r_k]
+                for bo in range(nbo):
+                    blk = packed[(bo * ns + s) * 512:(bo * ns + s + 1) * 512].reshape(2, 64, 4)
+                    A = np.zeros((16, 4))
+                    for lane in range(64):
+                        A[lane & 15, lane >> 4] = blk[sub, lane, r_k]
+                    D = A @ B
+                    for lane in range(64):
+                        for r in range(4):
+                            out[lane, bo, r] += D[4 * (lane >> 4) + r, lane & 15]
+    return out
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "f32"])
+@pytest.mark.parametrize("nout,kin", [(32, 64), (16, 32), (64, 128)])
+def test_packed_linear_matches_dense(dtype, nout, kin):
+    rng = np.random.default_rng(0)
+    W = rng.integers(-4, 5, size=(nout, kin)).astype(np.float64)   # exact in bf16
+    x = rng.integers(-4, 5, size=(16, kin)).astype(np.float64)
+    packed = packing.pack_matrix(W, dtype)
+    act = act_from_rows(x)
+    out = (emulate_bf16 if dtype == "bf16" else emulate_f32)(packed, nout // 16, kin // 32, act)
+    np.testing.assert_array_equal(rows_from_act(out), x @ W.T)
+
+
+def test_blob_sizes_match_layout():
+    from deepinteract_amd.weights import seeded_state_dict
+    sd = seeded_state_dict(0, with_head=False)
+    p = packing.PackedGeoT(sd, "f32")
+    sizes = packing.BLOB_SIZES
+    assert p.embed[0].numel() == sizes[0][0] * 512 and p.embed[1].numel() == sizes[0][1]
+    assert p.init[0].numel() == sizes[1][0] * 512
+    assert p.edge[0][0].numel() == sizes[2][0] * 512 and p.edge[1][0].numel() == sizes[3][0] * 512
+    assert p.node[0][0].numel() == sizes[4][0] * 512 and p.node[1][0].numel() == sizes[5][0] * 512
+    assert p.pos_src.shape == (2304, 128)
+    pb = packing.PackedGeoT(sd, "bf16")
+    assert pb.edge[0][0].dtype == torch.bfloat16
