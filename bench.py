@@ -142,7 +142,7 @@ def main():
     ap.add_argument("--knn", type=int, default=20)
     ap.add_argument("--pool", type=int, default=16, help="distinct synthetic complexes replicated in HBM")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
-    ap.add_argument("--cpu-sample", type=int, default=2)
+    ap.add_argument("--cpu-sample", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
     args = ap.parse_args()
 
