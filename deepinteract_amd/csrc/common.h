@@ -13,8 +13,9 @@
 // in fragment order) and the previous accumulator X^T directly as the B operand: no LDS round
 // trip and no lane shuffles between chained layers (cdna_hip_programming.md §3, "An accumulator
 // tile as the next MFMA's operand"). A 128-feature activation costs 32 VGPRs per lane.
-// 16x16 tiles read exactly as many LDS weight bytes per MAC as 32x32 tiles (1 KiB of A per
-// 16K MAC) at half the activation registers, which is what sets occupancy here.
+// 16x16 tiles need twice the LDS weight bytes per MAC of 32x32 tiles (1 KiB of A per 8K MAC
+// instead of 16K) but half the activation registers, which is what sets occupancy here; at full
+// MFMA rate on 4 SIMDs that is 256 B/clk/CU, the ds_read_b128 peak.
 //
 // The k-permutation implied by using an accumulator as B is baked into the host-side packing
 // (deepinteract_amd/packing.py). One packed block = 16 output rows x 32 input features =
@@ -83,8 +84,13 @@ __device__ __forceinline__ float expf_(float x) {
   if constexpr (FAST) return __expf(x);
   else return expf(x);
 }
+// SiLU. FAST (bf16 path): x * rcp(1 + exp(-x)) = 5 VALU ops (v_exp/v_rcp at ~1 ulp); the
+// exact path keeps the IEEE division (~10 ops) for fp32 parity.
 template <bool FAST>
-__device__ __forceinline__ float silu(float x) { return x / (1.0f + expf_<FAST>(-x)); }
+__device__ __forceinline__ float silu(float x) {
+  if constexpr (FAST) return x * __builtin_amdgcn_rcpf(1.0f + __expf(-x));
+  else return x / (1.0f + expf(-x));
+}
 
 // ------------------------------------------------------------------ activations
 template <int NB>  // NB blocks of 16 features
@@ -129,6 +135,40 @@ __device__ __forceinline__ void store_row(const Act<NB>& a, T* row, int g) {
 #pragma unroll
   for (int b = 0; b < NB; ++b) st4(row + 16 * b + 4 * g, a.v[b]);
 }
+
+// A 128-feature row held in its STORAGE format (bf16: 16 VGPRs instead of 32), for prefetching
+// gathered rows several MFMA chains ahead of their use.
+template <typename T>
+struct RawRow;
+template <>
+struct RawRow<u16> {
+  uint2 u[8];
+  __device__ __forceinline__ void load(const u16* row, int g) {
+#pragma unroll
+    for (int b = 0; b < 8; ++b) u[b] = *reinterpret_cast<const uint2*>(row + 16 * b + 4 * g);
+  }
+  __device__ __forceinline__ void to_act(Act<8>& a) const {
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      a.v[b][0] = __builtin_bit_cast(float, u[b].x << 16);
+      a.v[b][1] = __builtin_bit_cast(float, u[b].x & 0xffff0000u);
+      a.v[b][2] = __builtin_bit_cast(float, u[b].y << 16);
+      a.v[b][3] = __builtin_bit_cast(float, u[b].y & 0xffff0000u);
+    }
+  }
+};
+template <>
+struct RawRow<float> {
+  floatx4 v[8];
+  __device__ __forceinline__ void load(const float* row, int g) {
+#pragma unroll
+    for (int b = 0; b < 8; ++b) v[b] = ld4(row + 16 * b + 4 * g);
+  }
+  __device__ __forceinline__ void to_act(Act<8>& a) const {
+#pragma unroll
+    for (int b = 0; b < 8; ++b) a.v[b] = v[b];
+  }
+};
 
 // edge feature row G [28] (fp32, 112-B rows) as a 32-feature activation, features 28..31 = 0
 __device__ __forceinline__ void load_edge_geo(Act<2>& a, const float* row, int g) {
@@ -186,6 +226,23 @@ __device__ __forceinline__ void make_op(Op<F32T, NS>& o, const Act<2 * NS>& a) {
   for (int b = 0; b < 2 * NS; ++b) o.f[b] = a.v[b];
 }
 
+// inverse of make_op for bf16 (exact: bf16 -> fp32)
+template <int NS>
+__device__ __forceinline__ void unpack_op(Act<2 * NS>& a, const Op<BF16T, NS>& o) {
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    const uint4 u = __builtin_bit_cast(uint4, o.f[s]);
+    a.v[2 * s][0] = __builtin_bit_cast(float, u.x << 16);
+    a.v[2 * s][1] = __builtin_bit_cast(float, u.x & 0xffff0000u);
+    a.v[2 * s][2] = __builtin_bit_cast(float, u.y << 16);
+    a.v[2 * s][3] = __builtin_bit_cast(float, u.y & 0xffff0000u);
+    a.v[2 * s + 1][0] = __builtin_bit_cast(float, u.z << 16);
+    a.v[2 * s + 1][1] = __builtin_bit_cast(float, u.z & 0xffff0000u);
+    a.v[2 * s + 1][2] = __builtin_bit_cast(float, u.w << 16);
+    a.v[2 * s + 1][3] = __builtin_bit_cast(float, u.w & 0xffff0000u);
+  }
+}
+
 // out (NBO 16-row blocks) += W (NBO x NS packed blocks, in LDS) . op (NS 32-feature k-steps)
 template <int NBO, int NS>
 __device__ __forceinline__ void mma(Act<NBO>& out, const Op<BF16T, NS>& op, const u16* w, int lane) {
@@ -227,19 +284,60 @@ __device__ __forceinline__ void linear(Act<NBO>& out, const Act<2 * NS>& a, cons
 // ------------------------------------------------------------------ weight staging
 // Copy `nblk` packed blocks (512 elements each) from global memory to LDS with LDS-DMA
 // (global_load_lds_dwordx4: 1 KiB per wave-instruction, lane-linear destination = the packed
-// order). Called by all threads; the trailing barrier (s_waitcnt vmcnt(0) + s_barrier) waits
-// for the DMA.
-template <typename T>
-__device__ __forceinline__ void stage(T* lds, const T* g, int nblk) {
-  __syncthreads();  // previous readers of the buffer are done
+// order). Issued by all NW waves of the block; completion is awaited by the next barrier.
+template <int NW, typename T>
+__device__ __forceinline__ void dma_blocks(T* lds, const T* g, int nblk) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int nkib = nblk * BLK * (int)sizeof(T) / 1024;
-  for (int i = wave; i < nkib; i += WAVES) {
+  for (int i = wave; i < nkib; i += NW) {
     const char* src = reinterpret_cast<const char*>(g) + i * 1024 + lane * 16;
     __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                      (__attribute__((address_space(3))) void*)(reinterpret_cast<char*>(lds) + i * 1024),
                                      16, 0, 0);
   }
+}
+
+// Weight pipeline over one (DBUF=false) or two (DBUF=true) LDS buffers of CAP blocks.
+//   issue(W_next) starts the DMA of the NEXT layer's weights; next() waits for it (barrier,
+//   which also drains this wave's DMA: s_waitcnt vmcnt(0)) and returns the buffer to compute on.
+// With DBUF the DMA of layer i+1 runs under layer i's MFMAs; the buffer it overwrites was last
+// read in layer i-1, before the barrier inside next(). Call pattern per layer:
+//     w = pipe.next(); pipe.issue(next layer); compute(w);
+template <typename T, int NW, bool DBUF, int CAP>
+struct WPipe {
+  T* buf0;
+  T* buf1;
+  int cur;
+  const T* pend;
+  int pend_n;
+  __device__ explicit WPipe(T* lds) : buf0(lds), buf1(lds + (DBUF ? CAP * BLK : 0)), cur(0), pend(nullptr), pend_n(0) {}
+  __device__ __forceinline__ void issue(const T* g, int nblk) {
+    if constexpr (DBUF) {
+      dma_blocks<NW>(cur ? buf0 : buf1, g, nblk);
+    } else {
+      pend = g;
+      pend_n = nblk;
+    }
+  }
+  __device__ __forceinline__ const T* next() {
+    if constexpr (DBUF) {
+      __syncthreads();
+      cur ^= 1;
+      return cur ? buf1 : buf0;
+    } else {
+      __syncthreads();
+      dma_blocks<NW>(buf0, pend, pend_n);
+      __syncthreads();
+      return buf0;
+    }
+  }
+};
+
+// Single synchronous stage (kept for simple kernels).
+template <typename T>
+__device__ __forceinline__ void stage(T* lds, const T* g, int nblk) {
+  __syncthreads();
+  dma_blocks<WAVES>(lds, g, nblk);
   __syncthreads();
 }
 

@@ -62,6 +62,7 @@ struct EdgeArgs {
 
 struct NodeArgs {
   int Nt;
+  void* hT_out;  // optional [128, Nt] transposed copy of h_out (pair-tensor input)
   const int* src;
   const int* in_ptr;
   const float* alpha;
@@ -74,20 +75,66 @@ struct NodeArgs {
 };
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+template <int NW>
 __device__ __forceinline__ int row_id() {
-  return blockIdx.x * ROWS_PER_BLOCK + (threadIdx.x >> 6) * ROWS_PER_WAVE + (threadIdx.x & 15);
+  return blockIdx.x * (NW * ROWS_PER_WAVE) + (threadIdx.x >> 6) * ROWS_PER_WAVE + (threadIdx.x & 15);
 }
+
+// Launch geometry per storage dtype. bf16 (the benchmark path): 4-wave blocks, two per CU
+// (2 x 80 KiB of LDS, <=256 VGPRs), each double-buffering its weight stages so the LDS-DMA of
+// layer i+1 runs under layer i's MFMAs. Two independent blocks per CU matter: the waves of ONE
+// block meet at every stage barrier in lockstep, so only waves of the other block can fill a
+// SIMD's MFMA pipe while these run their SiLU VALU work (and vice versa).
+// fp32 (parity path; stages twice as large): same geometry, synchronous single-buffered stages.
+template <class DT>
+struct Geo {
+  static constexpr int NW = 4;
+  static constexpr bool DBUF = DT::kBF16;
+  static constexpr int CAP = 40;  // blocks per weight stage buffer
+  static constexpr int THREADS = 64 * NW;
+  static constexpr int ROWS = ROWS_PER_WAVE * NW;
+};
+
+// The edge's own input row F: bf16 path keeps it in registers as a packed MFMA operand (its
+// stored values are bf16, so unpacking is exact); fp32 path re-reads it (L2) where needed.
+template <class DT>
+struct FRow;
+template <>
+struct FRow<BF16T> {
+  Op<BF16T, 4> op;
+  __device__ void load(const u16* row, int g) {
+    Act<8> a;
+    load_row(a, row, g);
+    make_op(op, a);
+  }
+  __device__ void act(Act<8>& a, const u16*, int) const { unpack_op(a, op); }
+  __device__ const Op<BF16T, 4>& operand(const u16*, int) const { return op; }
+};
+template <>
+struct FRow<F32T> {
+  Op<F32T, 4> tmp;
+  __device__ void load(const float*, int) {}
+  __device__ void act(Act<8>& a, const float* row, int g) const { load_row(a, row, g); }
+  __device__ const Op<F32T, 4>& operand(const float* row, int g) {
+    Act<8> a;
+    load_row(a, row, g);
+    make_op(tmp, a);
+    return tmp;
+  }
+};
 
 // ================================================================ node embedding (+ Q/K/V of layer 0)
 template <class DT>
 __global__ __launch_bounds__(THREADS) void k_node_embed(EmbedArgs a) {
   using T = typename DT::T;
-  __shared__ __attribute__((aligned(16))) T wst[MAT128 * BLK];
+  __shared__ __attribute__((aligned(16))) T lds[2 * MAT128 * BLK];
   const int lane = lane_id(), g = lane >> 4;
-  const int r = row_id();
+  const int r = row_id<WAVES>();
   const bool valid = r < a.Nt;
   const int v = valid ? r : a.Nt - 1;
   const T* W = reinterpret_cast<const T*>(a.wmat);
+  WPipe<T, WAVES, true, MAT128> pipe(lds);
+  pipe.issue(W + EM_EMB * BLK, MAT128);
 
   Act<8> x;  // in_dim (113 raw DIPS-Plus + geometric features) input columns, zero padded to 128
   const float* row = a.node_f + (int64_t)v * a.in_dim;
@@ -98,33 +145,39 @@ __global__ __launch_bounds__(THREADS) void k_node_embed(EmbedArgs a) {
       const int f = 16 * b + 4 * g + q;
       x.v[b][q] = f < a.in_dim ? row[f] : 0.f;
     }
-  stage(wst, W + EM_EMB * BLK, MAT128);
+  const T* w = pipe.next();
+  pipe.issue(W + EM_Q * BLK, MAT128);
   Act<8> h;
   zero(h);
-  linear<DT, 8, 4>(h, x, wst, lane);
+  linear<DT, 8, 4>(h, x, w, lane);
   if (valid) store_row(h, reinterpret_cast<T*>(a.h_out) + (int64_t)v * HID, g);
   T* qkv = reinterpret_cast<T*>(a.qkv_out);
 #pragma unroll 1
   for (int q = 0; q < 3; ++q) {
-    stage(wst, W + (EM_Q + MAT128 * q) * BLK, MAT128);
+    w = pipe.next();
+    if (q < 2) pipe.issue(W + (EM_Q + MAT128 * (q + 1)) * BLK, MAT128);
     Act<8> t;
     init_vec(t, a.wvec + EMV_Q + 128 * q, g);
-    linear<DT, 8, 4>(t, h, wst, lane);
+    linear<DT, 8, 4>(t, h, w, lane);
     if (valid) store_row(t, qkv + (int64_t)v * 3 * HID + q * HID, g);
   }
 }
 
 // ================================================================ InitEdgeModule (+ layer-0 nbr_linear)
 template <class DT>
-__global__ __launch_bounds__(THREADS) void k_init_edge(InitArgs a) {
+__global__ __launch_bounds__(Geo<DT>::THREADS, 2) void k_init_edge(InitArgs a) {
   using T = typename DT::T;
+  using G = Geo<DT>;
   constexpr bool FAST = DT::kBF16;
-  __shared__ __attribute__((aligned(16))) T wst[40 * BLK];
+  constexpr int CAP = G::CAP;
+  __shared__ __attribute__((aligned(16))) T lds[(G::DBUF ? 2 : 1) * CAP * BLK];
   const int lane = lane_id(), g = lane >> 4;
-  const int r = row_id();
+  const int r = row_id<G::NW>();
   const bool valid = r < a.Et;
   const int e = valid ? r : a.Et - 1;
   const T* W = reinterpret_cast<const T*>(a.wmat);
+  WPipe<T, G::NW, G::DBUF, CAP> pipe(lds);
+  pipe.issue(W + IE_T0 * BLK, 40);
 
   Act<2> geo;
   load_edge_geo(geo, a.edge_f + (int64_t)e * NFEAT_E, g);
@@ -137,56 +190,99 @@ __global__ __launch_bounds__(THREADS) void k_init_edge(InitArgs a) {
   add_row(acc, a.pos_dst + (int64_t)a.node_pos[a.dst[e]] * HID, g);
 #pragma unroll 1
   for (int t = 0; t < 5; ++t) {
-    stage(wst, W + (IE_T0 + 40 * t) * BLK, 40);
+    const T* w = pipe.next();
+    if (t < 4) pipe.issue(W + (IE_T0 + 40 * (t + 1)) * BLK, 40);
+    else pipe.issue(W + IE_GEO1 * BLK, 40);
     Act<8> y;
     zero(y);
-    mma<8, 1>(y, gop, wst, lane);
+    mma<8, 1>(y, gop, w, lane);
     if (t > 0) silu_<8, FAST>(y);
-    linear<DT, 8, 4>(acc, y, wst + 8 * BLK, lane);
+    linear<DT, 8, 4>(acc, y, w + 8 * BLK, lane);
   }
   silu_<8, FAST>(acc);  // combined_edge_logits
   // gating: (em1 + silu(d1) + silu(r1) + silu(o1) + silu(a1)) * c
-  stage(wst, W + IE_GEO1 * BLK, 40);
-  Act<8> gs;
-  zero(gs);
+  {
+    const T* w = pipe.next();
+    pipe.issue(W + IE_C1 * BLK, 16);
+    Act<8> gs;
+    zero(gs);
 #pragma unroll 1
-  for (int t = 0; t < 5; ++t) {
-    Act<8> y;
-    zero(y);
-    mma<8, 1>(y, gop, wst + 8 * t * BLK, lane);
-    if (t > 0) silu_<8, FAST>(y);
-    add_(gs, y);
+    for (int t = 0; t < 5; ++t) {
+      Act<8> y;
+      zero(y);
+      mma<8, 1>(y, gop, w + 8 * t * BLK, lane);
+      if (t > 0) silu_<8, FAST>(y);
+      add_(gs, y);
+    }
+    mul_(acc, gs);
   }
-  mul_(acc, gs);
   // combined_linear_2(combined_linear_1(.)) : 128 -> 28 (padded 32) -> 128
-  stage(wst, W + IE_C1 * BLK, 16);
-  Act<2> z;
-  zero(z);
-  linear<DT, 2, 4>(z, acc, wst, lane);
   Act<8> f;
-  zero(f);
-  linear<DT, 8, 1>(f, z, wst + 8 * BLK, lane);
+  {
+    const T* w = pipe.next();
+    pipe.issue(W + IE_NBR * BLK, MAT128);
+    Act<2> z;
+    zero(z);
+    linear<DT, 2, 4>(z, acc, w, lane);
+    zero(f);
+    linear<DT, 8, 1>(f, z, w + 8 * BLK, lane);
+  }
   if (valid) store_row(f, reinterpret_cast<T*>(a.f_out) + (int64_t)e * HID, g);
-  // layer-0 nbr_linear, applied once per edge (gathered by the conformation module)
-  stage(wst, W + IE_NBR * BLK, MAT128);
-  Act<8> fn;
-  init_vec(fn, a.wvec + IEV_NBR, g);
-  linear<DT, 8, 4>(fn, f, wst, lane);
-  if (valid) store_row(fn, reinterpret_cast<T*>(a.fn_out) + (int64_t)e * HID, g);
+  // layer-0 silu(nbr_linear(F)), applied once per edge and gathered by the conformation module
+  // (silu(nbr_linear(F[ids])) == silu(nbr_linear(F))[ids], deepinteract_modules.py:386-390)
+  {
+    const T* w = pipe.next();
+    Act<8> fn;
+    init_vec(fn, a.wvec + IEV_NBR, g);
+    linear<DT, 8, 4>(fn, f, w, lane);
+    silu_<8, FAST>(fn);
+    if (valid) store_row(fn, reinterpret_cast<T*>(a.fn_out) + (int64_t)e * HID, g);
+  }
 }
 
 // ================================================================ fused edge layer
-template <class DT>
-__device__ __forceinline__ void res_block(Act<8>& x, const typename DT::T* W, const float* V, int idx,
-                                          typename DT::T* wst, int lane, int g) {
+// Weight stage order of the edge layer (block offsets and sizes, csrc/layout.h).
+__constant__ int EL_ORDER[24] = {
+    EL_S0, EL_UP, EL_OM,
+    EL_RES + 0 * MAT128, EL_RES + 1 * MAT128, EL_RES + 2 * MAT128,
+    EL_RES + 3 * MAT128, EL_RES + 4 * MAT128, EL_RES + 5 * MAT128,
+    EL_RC,
+    EL_RES + 6 * MAT128, EL_RES + 7 * MAT128, EL_RES + 8 * MAT128,
+    EL_RES + 9 * MAT128, EL_RES + 10 * MAT128, EL_RES + 11 * MAT128,
+    EL_F, EL_P,
+    EL_OE, EL_F1, EL_F2, EL_F1 + MAT128, EL_F2 + MAT128, EL_NN};
+__constant__ int EL_SIZE[24] = {36, 16, 32, 32, 32, 32, 32, 32, 32, 32, 32, 32,
+                                32, 32, 32, 32, 40, 32, 32, 32, 32, 32, 32, 32};
+constexpr int EL_NSTAGE_FINAL = 18, EL_NSTAGE = 24;
+
+template <class DT, bool FINAL>
+struct EdgeStages {
+  using T = typename DT::T;
+  using G = Geo<DT>;
+  WPipe<T, G::NW, G::DBUF, G::CAP>& pipe;
+  const T* W;
+  int i;
+  // wait for stage i (already issued), start stage i+1, return stage i's buffer
+  __device__ const T* next() {
+    const T* w = pipe.next();
+    const int n = FINAL ? EL_NSTAGE_FINAL : EL_NSTAGE;
+    if (i + 1 < n) pipe.issue(W + EL_ORDER[i + 1] * BLK, EL_SIZE[i + 1]);
+    ++i;
+    return w;
+  }
+};
+
+template <class DT, bool FINAL>
+__device__ __forceinline__ void res_block(Act<8>& x, EdgeStages<DT, FINAL>& st, const float* V, int idx, int lane,
+                                          int g) {
   constexpr bool FAST = DT::kBF16;
   Act<8> y = x;
 #pragma unroll 1
   for (int l = 0; l < 3; ++l) {
-    stage(wst, W + (EL_RES + MAT128 * (3 * idx + l)) * BLK, MAT128);
+    const typename DT::T* w = st.next();
     Act<8> t;
     init_vec(t, V + ELV_RES + 128 * (3 * idx + l), g);
-    linear<DT, 8, 4>(t, y, wst, lane);
+    linear<DT, 8, 4>(t, y, w, lane);
     silu_<8, FAST>(t);
     y = t;
   }
@@ -194,108 +290,117 @@ __device__ __forceinline__ void res_block(Act<8>& x, const typename DT::T* W, co
 }
 
 template <class DT, bool FINAL>
-__global__ __launch_bounds__(THREADS) void k_edge_layer(EdgeArgs a) {
+__global__ __launch_bounds__(Geo<DT>::THREADS, 2) void k_edge_layer(EdgeArgs a) {
   using T = typename DT::T;
+  using G = Geo<DT>;
   constexpr bool FAST = DT::kBF16;
-  __shared__ __attribute__((aligned(16))) T lds[60 * BLK];
-  T* wst = lds;                 // 32-block staging buffer
-  T* wg = lds + MAT128 * BLK;   // resident geometric projections (28 blocks)
+  __shared__ __attribute__((aligned(16))) T lds[(G::DBUF ? 2 : 1) * G::CAP * BLK];
   const int lane = lane_id(), g = lane >> 4;
-  const int r = row_id();
+  const int r = row_id<G::NW>();
   const bool valid = r < a.Et;
   const int e = valid ? r : a.Et - 1;
   const T* W = reinterpret_cast<const T*>(a.wmat);
   const float* V = a.wvec;
-  const T* f_in = reinterpret_cast<const T*>(a.f_in);
   const T* fn_in = reinterpret_cast<const T*>(a.fn_in);
   const T* qkv = reinterpret_cast<const T*>(a.qkv);
-  const T* f_row = f_in + (int64_t)e * HID;
+  const T* f_row = reinterpret_cast<const T*>(a.f_in) + (int64_t)e * HID;
 
-  stage(wg, W + EL_MG * BLK, 28);
+  WPipe<T, G::NW, G::DBUF, G::CAP> pipe(lds);
+  EdgeStages<DT, FINAL> st{pipe, W, 0};
+  pipe.issue(W + EL_S0 * BLK, 36);
+
+  const int4 nb = *reinterpret_cast<const int4*>(a.nbr + (int64_t)e * 4);
+  RawRow<T> xn;
+  xn.load(fn_in + (int64_t)nb.x * HID, g);  // first neighbour row in flight early
   Act<2> geo;
   load_edge_geo(geo, a.edge_f + (int64_t)e * NFEAT_E, g);
   Op<DT, 1> gop;
   make_op(gop, geo);
+  FRow<DT> fr;
+  fr.load(f_row, g);
 
   // ---- neighbour-edge messages (conformation_module_message_func :384-418)
-  Act<4> gate;  // dir . orient . amide embeddings (64)
+  const T* w = st.next();  // geometric gates + downward_proj
+  Act<4> gate;              // dir . orient . amide embeddings (64)
   {
     Act<4> t1;
     zero(gate);
-    mma<4, 1>(gate, gop, wg + 8 * BLK, lane);
+    mma<4, 1>(gate, gop, w + 8 * BLK, lane);
     zero(t1);
-    mma<4, 1>(t1, gop, wg + 12 * BLK, lane);
+    mma<4, 1>(t1, gop, w + 12 * BLK, lane);
     mul_(gate, t1);
     zero(t1);
-    mma<4, 1>(t1, gop, wg + 16 * BLK, lane);
+    mma<4, 1>(t1, gop, w + 16 * BLK, lane);
     mul_(gate, t1);
   }
-  stage(wst, W + EL_DOWN * BLK, 16);
+
   Act<4> s;
   zero(s);
-#pragma unroll 1
+#pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const int ne = a.nbr[(int64_t)e * 4 + j];
     Act<8> x;
-    load_row(x, fn_in + (int64_t)ne * HID, g);
+    xn.to_act(x);
+    if (j < 3) {  // prefetch the next neighbour row under this one's MFMAs
+      const int nx = j == 0 ? nb.y : (j == 1 ? nb.z : nb.w);
+      xn.load(fn_in + (int64_t)nx * HID, g);
+    }
+    // dist_linear_1(dist_linear_0(dist)), recomputed per neighbour (8 MFMAs) rather than held
+    // live across the loop: the memory clobber stops the compiler from hoisting it (32 VGPRs)
+    asm volatile("" ::: "memory");
     Act<8> dg;
     zero(dg);
-    mma<8, 1>(dg, gop, wg, lane);  // dist_linear_1(dist_linear_0(dist))
+    mma<8, 1>(dg, gop, w, lane);
 #pragma unroll
     for (int b = 0; b < 8; ++b)
 #pragma unroll
-      for (int q = 0; q < 4; ++q) x.v[b][q] = silu<FAST>(x.v[b][q]) * dg.v[b][q];
+      for (int q = 0; q < 4; ++q) x.v[b][q] *= dg.v[b][q];  // gathered rows are silu(nbr_linear(F))
     Act<4> y;
     zero(y);
-    linear<DT, 4, 4>(y, x, wst, lane);  // downward_proj
+    linear<DT, 4, 4>(y, x, w + 20 * BLK, lane);  // downward_proj
 #pragma unroll
     for (int b = 0; b < 4; ++b)
 #pragma unroll
       for (int q = 0; q < 4; ++q) s.v[b][q] += silu<FAST>(y.v[b][q]) * gate.v[b][q];
   }
-  stage(wst, W + EL_UP * BLK, 16);
   Act<8> x;
+  w = st.next();  // upward_proj
   zero(x);
-  linear<DT, 8, 2>(x, s, wst, lane);  // upward_proj
+  linear<DT, 8, 2>(x, s, w, lane);
   silu_<8, FAST>(x);
   add_vec(x, V + ELV_OM, g);
-  stage(wst, W + EL_OM * BLK, MAT128);
+  w = st.next();  // orig_msg_linear(res) + nbr
+  mma<8, 4>(x, fr.operand(f_row, g), w, lane);
+  res_block<DT, FINAL>(x, st, V, 0, lane, g);
+  res_block<DT, FINAL>(x, st, V, 1, lane, g);
   {
-    Act<8> f;
-    load_row(f, f_row, g);
-    linear<DT, 8, 4>(x, f, wst, lane);  // orig_msg_linear(res) + nbr
-  }
-  res_block<DT>(x, W, V, 0, wst, lane, g);
-  res_block<DT>(x, W, V, 1, wst, lane, g);
-  {
-    stage(wst, W + EL_RC * BLK, MAT128);
+    w = st.next();  // res_connect_linear
     Act<8> y;
     init_vec(y, V + ELV_RC, g);
-    linear<DT, 8, 4>(y, x, wst, lane);
+    linear<DT, 8, 4>(y, x, w, lane);
     silu_<8, FAST>(y);
-    load_row(x, f_row, g);
+    fr.act(x, f_row, g);
     add_(x, y);
   }
-  res_block<DT>(x, W, V, 2, wst, lane, g);
-  res_block<DT>(x, W, V, 3, wst, lane, g);
+  res_block<DT, FINAL>(x, st, V, 2, lane, g);
+  res_block<DT, FINAL>(x, st, V, 3, lane, g);
   {
+    w = st.next();  // final_linear + final geometric gate
     Act<8> fg;
     zero(fg);
-    mma<8, 1>(fg, gop, wg + 20 * BLK, lane);
+    mma<8, 1>(fg, gop, w + 32 * BLK, lane);
     mul_(x, fg);
-    stage(wst, W + EL_F * BLK, MAT128);
     Act<8> y;
     init_vec(y, V + ELV_F, g);
-    linear<DT, 8, 4>(y, x, wst, lane);
+    linear<DT, 8, 4>(y, x, w, lane);
     silu_<8, FAST>(y);
-    load_row(x, f_row, g);
+    fr.act(x, f_row, g);
     add_(x, y);  // conformation output
   }
   // ---- attention scores (propagate_attention :76-91)
-  stage(wst, W + EL_P * BLK, MAT128);
+  w = st.next();  // edge_feats_projection(BN1e(conf))
   Act<8> p;
   init_vec(p, V + ELV_P, g);
-  linear<DT, 8, 4>(p, x, wst, lane);  // edge_feats_projection(BN1e(conf))
+  linear<DT, 8, 4>(p, x, w, lane);
   {
     const int sn = a.src[e], dn = a.dst[e];
     Act<8> kq, qd;
@@ -306,7 +411,7 @@ __global__ __launch_bounds__(THREADS) void k_edge_layer(EdgeArgs a) {
     for (int b = 0; b < 8; ++b)
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        float sc = (kq.v[b][q] * qd.v[b][q]) / scale;
+        float sc = FAST ? (kq.v[b][q] * qd.v[b][q]) * (1.0f / scale) : (kq.v[b][q] * qd.v[b][q]) / scale;
         sc = fminf(fmaxf(sc, -5.f), 5.f);
         p.v[b][q] = sc * p.v[b][q];  // score = e_out
       }
@@ -318,46 +423,54 @@ __global__ __launch_bounds__(THREADS) void k_edge_layer(EdgeArgs a) {
 
   if constexpr (!FINAL) {
     // ---- edge output: e = in + O_e(e_out); e = e + FFN(BN2e(e)) (:697-724)
-    stage(wst, W + EL_OE * BLK, MAT128);
+    w = st.next();  // O_edge_feats
     Act<8> e1;
     init_vec(e1, V + ELV_OE, g);
-    linear<DT, 8, 4>(e1, p, wst, lane);
-    add_row(e1, f_row, g);
+    linear<DT, 8, 4>(e1, p, w, lane);
+    {
+      Act<8> fa;
+      fr.act(fa, f_row, g);
+      add_(e1, fa);
+    }
     Act<8> o;
     zero(o);
 #pragma unroll 1
     for (int half = 0; half < 2; ++half) {
-      stage(wst, W + (EL_F1 + MAT128 * half) * BLK, MAT128);
+      w = st.next();  // edge_feats_MLP.0 (BN2e folded), hidden half
       Act<8> t;
       init_vec(t, V + ELV_F1 + 128 * half, g);
-      linear<DT, 8, 4>(t, e1, wst, lane);
+      linear<DT, 8, 4>(t, e1, w, lane);
       silu_<8, FAST>(t);
-      stage(wst, W + (EL_F2 + MAT128 * half) * BLK, MAT128);
-      linear<DT, 8, 4>(o, t, wst, lane);
+      w = st.next();  // edge_feats_MLP.3, input half
+      linear<DT, 8, 4>(o, t, w, lane);
     }
     add_(e1, o);
     if (valid) store_row(e1, reinterpret_cast<T*>(a.f_out) + (int64_t)e * HID, g);
-    stage(wst, W + EL_NN * BLK, MAT128);
+    w = st.next();  // next layer's silu(nbr_linear(.))
     Act<8> fn;
     init_vec(fn, V + ELV_NN, g);
-    linear<DT, 8, 4>(fn, e1, wst, lane);
+    linear<DT, 8, 4>(fn, e1, w, lane);
+    silu_<8, FAST>(fn);
     if (valid) store_row(fn, reinterpret_cast<T*>(a.fn_out) + (int64_t)e * HID, g);
   }
 }
 
 // ================================================================ fused node layer
 template <class DT, bool FINAL>
-__global__ __launch_bounds__(THREADS) void k_node_layer(NodeArgs a) {
+__global__ __launch_bounds__(THREADS, 2) void k_node_layer(NodeArgs a) {
   using T = typename DT::T;
   constexpr bool FAST = DT::kBF16;
-  __shared__ __attribute__((aligned(16))) T wst[MAT128 * BLK];
+  constexpr bool DB = DT::kBF16;
+  __shared__ __attribute__((aligned(16))) T lds[(DB ? 2 : 1) * MAT128 * BLK];
   const int lane = lane_id(), g = lane >> 4;
-  const int r = row_id();
+  const int r = row_id<WAVES>();
   const bool valid = r < a.Nt;
   const int v = valid ? r : a.Nt - 1;
   const T* W = reinterpret_cast<const T*>(a.wmat);
   const float* V = a.wvec;
   const T* qkv = reinterpret_cast<const T*>(a.qkv);
+  WPipe<T, WAVES, DB, MAT128> pipe(lds);
+  pipe.issue(W + NL_ON * BLK, MAT128);
 
   // send_and_recv(u_mul_e('V_h','score'), sum) and (copy_e('score'), sum); h = wV / (z + 1e-6)
   Act<8> wv;
@@ -380,34 +493,50 @@ __global__ __launch_bounds__(THREADS) void k_node_layer(NodeArgs a) {
     for (int q = 0; q < 4; ++q) wv.v[b][q] = wv.v[b][q] / d;
   }
   // n = in1 + O_node(h)
-  stage(wst, W + NL_ON * BLK, MAT128);
+  const T* w = pipe.next();
+  pipe.issue(W + NL_F1 * BLK, MAT128);
   Act<8> n;
   init_vec(n, V + NLV_ON, g);
-  linear<DT, 8, 4>(n, wv, wst, lane);
+  linear<DT, 8, 4>(n, wv, w, lane);
   add_row(n, reinterpret_cast<const T*>(a.h_in) + (int64_t)v * HID, g);
   // n = n + W2 silu(W1 BN2(n))
   Act<8> o;
   zero(o);
 #pragma unroll 1
   for (int half = 0; half < 2; ++half) {
-    stage(wst, W + (NL_F1 + MAT128 * half) * BLK, MAT128);
+    w = pipe.next();
+    pipe.issue(W + (NL_F2 + MAT128 * half) * BLK, MAT128);
     Act<8> t;
     init_vec(t, V + NLV_F1 + 128 * half, g);
-    linear<DT, 8, 4>(t, n, wst, lane);
+    linear<DT, 8, 4>(t, n, w, lane);
     silu_<8, FAST>(t);
-    stage(wst, W + (NL_F2 + MAT128 * half) * BLK, MAT128);
-    linear<DT, 8, 4>(o, t, wst, lane);
+    w = pipe.next();
+    if (half == 0) pipe.issue(W + (NL_F1 + MAT128) * BLK, MAT128);
+    else if (!FINAL) pipe.issue(W + NL_Q * BLK, MAT128);
+    linear<DT, 8, 4>(o, t, w, lane);
   }
   add_(n, o);
   if (valid) store_row(n, reinterpret_cast<T*>(a.h_out) + (int64_t)v * HID, g);
+  if (a.hT_out != nullptr && valid) {  // 16 lanes (nodes) store 32 contiguous bytes per feature
+    T* hT = reinterpret_cast<T*>(a.hT_out);
+#pragma unroll
+    for (int b = 0; b < 8; ++b)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float x = n.v[b][q];
+        if constexpr (DT::kBF16) hT[(int64_t)(16 * b + 4 * g + q) * a.Nt + v] = (u16)(pack_bf16x2(x, 0.f) & 0xffffu);
+        else hT[(int64_t)(16 * b + 4 * g + q) * a.Nt + v] = x;
+      }
+  }
   if constexpr (!FINAL) {
     T* qo = reinterpret_cast<T*>(a.qkv_out);
 #pragma unroll 1
     for (int q = 0; q < 3; ++q) {
-      stage(wst, W + (NL_Q + MAT128 * q) * BLK, MAT128);
+      w = pipe.next();
+      if (q < 2) pipe.issue(W + (NL_Q + MAT128 * (q + 1)) * BLK, MAT128);
       Act<8> t;
       init_vec(t, V + NLV_Q + 128 * q, g);
-      linear<DT, 8, 4>(t, n, wst, lane);
+      linear<DT, 8, 4>(t, n, w, lane);
       if (valid) store_row(t, qo + (int64_t)v * 3 * HID + q * HID, g);
     }
   }
@@ -418,7 +547,7 @@ __global__ __launch_bounds__(THREADS) void k_node_layer(NodeArgs a) {
 // ================================================================ C ABI
 using namespace di;
 
-static inline int grid_rows(int n) { return (n + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK; }
+static inline int grid_rows(int n, int rows = ROWS_PER_BLOCK) { return (n + rows - 1) / rows; }
 
 static inline int launch_status() {
   hipError_t e = hipGetLastError();
@@ -465,9 +594,9 @@ extern "C" int di_init_edge(const di_graph* g, di_dtype dt, const float* edge_f,
              f_out, fn_out};
   hipStream_t s = (hipStream_t)stream;
   if (dt == DI_BF16)
-    hipLaunchKernelGGL(k_init_edge<BF16T>, dim3(grid_rows(a.Et)), dim3(THREADS), 0, s, a);
+    hipLaunchKernelGGL(k_init_edge<BF16T>, dim3(grid_rows(a.Et, Geo<BF16T>::ROWS)), dim3(Geo<BF16T>::THREADS), 0, s, a);
   else
-    hipLaunchKernelGGL(k_init_edge<F32T>, dim3(grid_rows(a.Et)), dim3(THREADS), 0, s, a);
+    hipLaunchKernelGGL(k_init_edge<F32T>, dim3(grid_rows(a.Et, Geo<F32T>::ROWS)), dim3(Geo<F32T>::THREADS), 0, s, a);
   return launch_status();
 }
 
@@ -481,11 +610,12 @@ extern "C" int di_edge_layer(const di_graph* g, di_dtype dt, int final_layer, co
   EdgeArgs a{g->num_edges, edge_f, g->src, g->dst, g->nbr, f_in, fn_in, qkv, wmat, wvec, alpha_out,
              f_out, fn_out};
   hipStream_t s = (hipStream_t)stream;
-  dim3 grid(grid_rows(a.Et)), block(THREADS);
   if (dt == DI_BF16) {
+    dim3 grid(grid_rows(a.Et, Geo<BF16T>::ROWS)), block(Geo<BF16T>::THREADS);
     if (final_layer) hipLaunchKernelGGL((k_edge_layer<BF16T, true>), grid, block, 0, s, a);
     else hipLaunchKernelGGL((k_edge_layer<BF16T, false>), grid, block, 0, s, a);
   } else {
+    dim3 grid(grid_rows(a.Et, Geo<F32T>::ROWS)), block(Geo<F32T>::THREADS);
     if (final_layer) hipLaunchKernelGGL((k_edge_layer<F32T, true>), grid, block, 0, s, a);
     else hipLaunchKernelGGL((k_edge_layer<F32T, false>), grid, block, 0, s, a);
   }
@@ -494,10 +624,10 @@ extern "C" int di_edge_layer(const di_graph* g, di_dtype dt, int final_layer, co
 
 extern "C" int di_node_layer(const di_graph* g, di_dtype dt, int final_layer, const float* alpha,
                              const void* h_in, const void* qkv, const void* wmat, const float* wvec,
-                             void* h_out, void* qkv_out, void* stream) {
+                             void* h_out, void* qkv_out, void* hT_out, void* stream) {
   if (!g || !alpha || !h_in || !qkv || !wmat || !wvec || !h_out || g->num_nodes <= 0) return DI_EINVAL;
   if (!final_layer && !qkv_out) return DI_EINVAL;
-  NodeArgs a{g->num_nodes, g->src, g->in_ptr, alpha, h_in, qkv, wmat, wvec, h_out, qkv_out};
+  NodeArgs a{g->num_nodes, hT_out, g->src, g->in_ptr, alpha, h_in, qkv, wmat, wvec, h_out, qkv_out};
   hipStream_t s = (hipStream_t)stream;
   dim3 grid(grid_rows(a.Nt)), block(THREADS);
   if (dt == DI_BF16) {

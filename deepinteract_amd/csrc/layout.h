@@ -23,13 +23,15 @@ constexpr int IE_NBLK = 288;
 constexpr int IEV_NBR = 0, IEV_N = 128;
 
 // ---- kind 2/3: edge layer (conformation + attention scores [+ edge output]) --------------
-constexpr int EL_MG = 0;      // [28 x 1]: dist gate 0-7, dir 8-11, orient 12-15, amide 16-19, final gate 20-27
-constexpr int EL_DOWN = 28;   // [4 x 4]
-constexpr int EL_UP = 44;     // [8 x 2]
-constexpr int EL_OM = 60;     // orig_msg_linear
-constexpr int EL_RES = 92;    // 12 x [8x4]: pre0 l0..l2, pre1, post0, post1
-constexpr int EL_RC = 476;
-constexpr int EL_F = 508;
+// stage 0 = geometric gates + downward_proj (one 36-block stage), final gate rides with final_linear
+constexpr int EL_S0 = 0;      // dist gate [8x1] 0-7, dir 8-11, orient 12-15, amide 16-19, then DOWN
+constexpr int EL_DOWN = 20;   // [4 x 4]
+constexpr int EL_UP = 36;     // [8 x 2]
+constexpr int EL_OM = 52;     // orig_msg_linear
+constexpr int EL_RES = 84;    // 12 x [8x4]: pre0 l0..l2, pre1, post0, post1
+constexpr int EL_RC = 468;
+constexpr int EL_F = 500;     // final_linear [8x4]
+constexpr int EL_FG = 532;    // final gate (sum of the 4 final_* geometric linears) [8x1]
 constexpr int EL_P = 540;     // edge_feats_projection . BN1e
 constexpr int EL_NBLK_FINAL = 572;
 constexpr int EL_OE = 572;

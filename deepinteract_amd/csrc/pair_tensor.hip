@@ -3,11 +3,14 @@
 //     T[c, i, j] = h1[i, c]          for c <  H
 //     T[c, i, j] = h2[j, c - H]      for c >= H          (NCHW, [2H, L1, L2] per complex)
 // The reference materialises it with two repeat_interleave tensors plus a cat (3x the output
-// bytes); here every output byte is written exactly once and nothing else is written or
-// re-read: the kernel is a pure HBM store stream (512 MB per 2x1000-residue complex in bf16).
+// bytes); here every output byte is written exactly once: a pure HBM store stream (512 MB per
+// 2x1000-residue complex in bf16), with non-temporal 16-B stores (write-once data, kept out of
+// the caches the concurrently running GeoT kernels use).
 //
-// Grid: x = 64K-element chunk of a [L1*L2] channel plane, y = channel (2H), z = complex.
-// Channel planes of chain 2 are served from a copy of column h2[:, c-H] staged in LDS.
+// Persistent grid: a few blocks per CU walk work items (complex, channel, 64K-element chunk);
+// no LDS, so the kernel co-resides with the GeoT kernels on the other stream (which hold the
+// LDS) instead of starving them of CU slots. Chain-2 planes read the transposed features hT
+// [H, Nt] (written by the final node layer), so each 16-B store is fed by one 16-B load.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include "common.h"
@@ -16,8 +19,8 @@
 namespace di {
 
 constexpr int PAIR_THREADS = 256;
-constexpr int PAIR_CHUNK = 65536;   // elements per block
-constexpr int PAIR_MAX_L = 8192;    // longest chain the LDS column buffer holds
+constexpr int PAIR_CHUNK = 65536;  // elements per work item
+constexpr int PAIR_MAX_BLOCKS = 512;
 
 template <typename T>
 struct Vec16;
@@ -26,56 +29,59 @@ struct Vec16<float> {
   using V = floatx4;
   static constexpr int N = 4;
 };
+typedef unsigned int uintx4 __attribute__((ext_vector_type(4)));
 template <>
 struct Vec16<u16> {
-  using V = uint4;
+  using V = uintx4;
   static constexpr int N = 8;
 };
 
 template <typename T, bool ALIGNED>
 __global__ __launch_bounds__(PAIR_THREADS) void k_pair_tensor(const di_pair_desc* __restrict__ descs, int hidden,
-                                                            const T* __restrict__ h, T* __restrict__ out) {
-  __shared__ __attribute__((aligned(16))) T col[PAIR_MAX_L];
+                                                            const T* __restrict__ h, const T* __restrict__ hT,
+                                                            int nrows, int chunks, int64_t items,
+                                                            T* __restrict__ out) {
+  using V = typename Vec16<T>::V;
   constexpr int VEC = Vec16<T>::N;
-  const di_pair_desc d = descs[blockIdx.z];
-  const int c = blockIdx.y;
-  const int64_t plane = (int64_t)d.l1 * d.l2;
-  const int64_t q_begin = (int64_t)blockIdx.x * PAIR_CHUNK;
-  if (q_begin >= plane) return;  // uniform per block
-  const int64_t q_end = q_begin + PAIR_CHUNK < plane ? q_begin + PAIR_CHUNK : plane;
-  T* o = out + d.out_off + (int64_t)c * plane;
-  const bool second = c >= hidden;
-  if (second) {
-    for (int j = threadIdx.x; j < d.l2; j += PAIR_THREADS) col[j] = h[(d.h2_row + j) * hidden + (c - hidden)];
-    __syncthreads();
-  }
-  const T* h1c = h + d.h1_row * hidden + c;
-  for (int64_t q = q_begin + (int64_t)threadIdx.x * VEC; q < q_end; q += (int64_t)PAIR_THREADS * VEC) {
-    T vals[VEC];
-    if (ALIGNED && d.l2 >= VEC) {
+  for (int64_t item = blockIdx.x; item < items; item += gridDim.x) {
+    const int chunk = (int)(item % chunks);
+    const int64_t rest = item / chunks;
+    const int c = (int)(rest % (2 * hidden));
+    const int cpx = (int)(rest / (2 * hidden));
+    const di_pair_desc d = descs[cpx];
+    const int64_t plane = (int64_t)d.l1 * d.l2;
+    const int64_t q_begin = (int64_t)chunk * PAIR_CHUNK;
+    if (q_begin >= plane) continue;  // uniform per block
+    const int64_t q_end = q_begin + PAIR_CHUNK < plane ? q_begin + PAIR_CHUNK : plane;
+    T* o = out + d.out_off + (int64_t)c * plane;
+    const bool second = c >= hidden;
+    const T* h1c = h + d.h1_row * hidden + c;                                      // column c of chain 1
+    const T* h2t = hT ? hT + (int64_t)(c - hidden) * nrows + d.h2_row : nullptr;  // row c-H of hT
+    const T* h2c = h + d.h2_row * hidden + (c - hidden);                           // strided fallback
+    for (int64_t q = q_begin + (int64_t)threadIdx.x * VEC; q < q_end; q += (int64_t)PAIR_THREADS * VEC) {
       const int i = (int)(q / d.l2);
       const int j = (int)(q - (int64_t)i * d.l2);
-      if (second) {
+      if (ALIGNED) {
+        V vals;
+        if (second) {
+          vals = *reinterpret_cast<const V*>(h2t + j);  // j % VEC == 0 and L2 % VEC == 0: no row wrap
+        } else {
+          const T v0 = h1c[(int64_t)i * hidden];
+          T tmp[VEC];
+#pragma unroll
+          for (int t = 0; t < VEC; ++t) tmp[t] = v0;
+          vals = *reinterpret_cast<const V*>(tmp);
+        }
+        __builtin_nontemporal_store(vals, reinterpret_cast<V*>(o + q));
+      } else {
 #pragma unroll
         for (int t = 0; t < VEC; ++t) {
-          const int jj = j + t < d.l2 ? j + t : j + t - d.l2;
-          vals[t] = col[jj];
-        }
-      } else {
-        const T v0 = h1c[(int64_t)i * hidden];
-        const T v1 = i + 1 < d.l1 ? h1c[(int64_t)(i + 1) * hidden] : v0;
-#pragma unroll
-        for (int t = 0; t < VEC; ++t) vals[t] = j + t < d.l2 ? v0 : v1;
-      }
-      *reinterpret_cast<typename Vec16<T>::V*>(o + q) = *reinterpret_cast<const typename Vec16<T>::V*>(vals);
-    } else {
-#pragma unroll
-      for (int t = 0; t < VEC; ++t) {
-        const int64_t qq = q + t;
-        if (qq < q_end) {
-          const int i = (int)(qq / d.l2);
-          const int j = (int)(qq - (int64_t)i * d.l2);
-          o[qq] = second ? col[j] : h1c[(int64_t)i * hidden];
+          const int64_t qq = q + t;
+          if (qq < q_end) {
+            const int ii = (int)(qq / d.l2);
+            const int jj = (int)(qq - (int64_t)ii * d.l2);
+            o[qq] = second ? (h2t ? h2t[jj] : h2c[(int64_t)jj * hidden]) : h1c[(int64_t)ii * hidden];
+          }
         }
       }
     }
@@ -87,25 +93,31 @@ __global__ __launch_bounds__(PAIR_THREADS) void k_pair_tensor(const di_pair_desc
 using namespace di;
 
 extern "C" int di_pair_tensor(di_dtype dt, const di_pair_desc* descs, int32_t num_complexes, int32_t max_l1,
-                              int32_t max_l2, int32_t hidden, int32_t aligned16, const void* h, void* out,
-                              void* stream) {
+                              int32_t max_l2, int32_t hidden, int32_t aligned16, const void* h, const void* hT,
+                              int32_t num_rows, void* out, void* stream) {
   if (!descs || !h || !out || num_complexes <= 0 || max_l1 <= 0 || max_l2 <= 0 || hidden <= 0) return DI_EINVAL;
-  if (max_l2 > PAIR_MAX_L || num_complexes > 65535) return DI_EINVAL;
+  if (aligned16 && !hT) return DI_EINVAL;
   const int64_t plane = (int64_t)max_l1 * max_l2;
-  dim3 grid((unsigned)((plane + PAIR_CHUNK - 1) / PAIR_CHUNK), (unsigned)(2 * hidden), (unsigned)num_complexes);
+  const int chunks = (int)((plane + PAIR_CHUNK - 1) / PAIR_CHUNK);
+  const int64_t items = (int64_t)num_complexes * 2 * hidden * chunks;
+  const unsigned grid = (unsigned)(items < PAIR_MAX_BLOCKS ? items : PAIR_MAX_BLOCKS);
   hipStream_t s = (hipStream_t)stream;
-  // aligned16: the caller guarantees every channel plane (L1*L2) and every out_off is a multiple
-  // of 16 bytes, which enables the 16-B vector store path.
+  // aligned16: every channel plane (L1*L2), out_off, L2 and h2_row is a multiple of 16 bytes of
+  // elements: 16-B vector loads and non-temporal 16-B stores.
   if (dt == DI_BF16) {
     if (aligned16)
-      hipLaunchKernelGGL((k_pair_tensor<u16, true>), grid, dim3(PAIR_THREADS), 0, s, descs, hidden, (const u16*)h, (u16*)out);
+      hipLaunchKernelGGL((k_pair_tensor<u16, true>), dim3(grid), dim3(PAIR_THREADS), 0, s, descs, hidden,
+                         (const u16*)h, (const u16*)hT, num_rows, chunks, items, (u16*)out);
     else
-      hipLaunchKernelGGL((k_pair_tensor<u16, false>), grid, dim3(PAIR_THREADS), 0, s, descs, hidden, (const u16*)h, (u16*)out);
+      hipLaunchKernelGGL((k_pair_tensor<u16, false>), dim3(grid), dim3(PAIR_THREADS), 0, s, descs, hidden,
+                         (const u16*)h, (const u16*)hT, num_rows, chunks, items, (u16*)out);
   } else {
     if (aligned16)
-      hipLaunchKernelGGL((k_pair_tensor<float, true>), grid, dim3(PAIR_THREADS), 0, s, descs, hidden, (const float*)h, (float*)out);
+      hipLaunchKernelGGL((k_pair_tensor<float, true>), dim3(grid), dim3(PAIR_THREADS), 0, s, descs, hidden,
+                         (const float*)h, (const float*)hT, num_rows, chunks, items, (float*)out);
     else
-      hipLaunchKernelGGL((k_pair_tensor<float, false>), grid, dim3(PAIR_THREADS), 0, s, descs, hidden, (const float*)h, (float*)out);
+      hipLaunchKernelGGL((k_pair_tensor<float, false>), dim3(grid), dim3(PAIR_THREADS), 0, s, descs, hidden,
+                         (const float*)h, (const float*)hT, num_rows, chunks, items, (float*)out);
   }
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? DI_OK : (int)e;

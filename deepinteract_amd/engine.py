@@ -63,8 +63,7 @@ class GeoTEngine:
         self.device = torch.device(device)
         self.packed = PackedGeoT(state_dict, dtype, cfg, self.device)
         self._check_blob_sizes()
-        self._ws = None
-        self._ws_key = None
+        self._ws = {}
 
     def _check_blob_sizes(self):
         p, dt = self.packed, _DI_DT[self.dtype]
@@ -80,27 +79,29 @@ class GeoTEngine:
             if want_m != got_m or want_v != got_v:
                 raise RuntimeError(f"weight blob {kind} size mismatch: {got_m}/{got_v} vs {want_m}/{want_v}")
 
-    def workspace(self, num_nodes: int, num_edges: int):
+    def workspace(self, num_nodes: int, num_edges: int, slot: int = 0):
+        """Per-slot activation buffers (two slots let a consumer of slot s's outputs, e.g. the
+        pair-tensor kernel on another stream, run while the next batch computes in slot 1-s)."""
         key = (num_nodes, num_edges)
-        if self._ws_key != key:
+        if slot not in self._ws or self._ws[slot][0] != key:
             dt, dev, H = _TORCH_DT[self.dtype], self.device, self.cfg.num_gnn_hidden_channels
-            self._ws = {
+            self._ws[slot] = (key, {
                 "h": [torch.empty(num_nodes, H, dtype=dt, device=dev) for _ in range(2)],
                 "qkv": [torch.empty(num_nodes, 3 * H, dtype=dt, device=dev) for _ in range(2)],
                 "f": [torch.empty(num_edges, H, dtype=dt, device=dev) for _ in range(2)],
                 "fn": [torch.empty(num_edges, H, dtype=dt, device=dev) for _ in range(2)],
                 "alpha": torch.empty(num_edges, 4, dtype=torch.float32, device=dev),
-            }
-            self._ws_key = key
-        return self._ws
+                "hT": torch.empty(H, num_nodes, dtype=dt, device=dev),
+            })
+        return self._ws[slot][1]
 
-    def forward(self, gb: GraphBatch, clone: bool = True, events=None):
+    def forward(self, gb: GraphBatch, clone: bool = True, events=None, slot: int = 0):
         """-> (node feats [Nt,128], edge feats [Et,128]) in the engine dtype.
 
         events: optional dict kernel-name -> list; (start, end) torch.cuda.Event pairs are recorded
         around every launch on the launch stream (for per-kernel timing in bench.py)."""
         lib, p, dt = self.lib, self.packed, _DI_DT[self.dtype]
-        ws = self.workspace(gb.num_nodes, gb.num_edges)
+        ws = self.workspace(gb.num_nodes, gb.num_edges, slot)
         g = ctypes.byref(gb.c_graph)
         st = _stream()
         h, qkv, f, fn, alpha = ws["h"], ws["qkv"], ws["f"], ws["fn"], ws["alpha"]
@@ -127,12 +128,13 @@ class GeoTEngine:
             tick("node_layer_final" if final else "node_layer")
             _lib.check(lib.di_node_layer(g, dt, int(final), _ptr(alpha), _ptr(h[cur]), _ptr(qkv[cur]),
                                          _ptr(nm), _ptr(nv), _ptr(h[nxt]), _ptr(None if final else qkv[nxt]),
-                                         st), "di_node_layer")
+                                         _ptr(ws["hT"] if final else None), st), "di_node_layer")
             if not final:
                 f_out = nxt
             cur = nxt
         tick(None)
         node_out = h[cur]
+        self.last_hT = ws["hT"]  # [128, Nt] transposed final node features (pair-tensor input)
         edge_out = f[f_out] if L > 1 else f[0]
         if clone:
             return node_out.clone(), edge_out.clone()
@@ -161,7 +163,7 @@ class PairTensorOp:
             self._desc_cache[key] = (t, offs, off)
         return self._desc_cache[key]
 
-    def __call__(self, h, h1_rows, h2_rows, l1s, l2s, out=None, events=None):
+    def __call__(self, h, h1_rows, h2_rows, l1s, l2s, out=None, events=None, hT=None):
         """h: [rows, H] node features (both chains of every complex). Returns a flat buffer and
         the per-complex [1, 2H, L1, L2] views."""
         hidden = h.shape[1]
@@ -174,12 +176,16 @@ class PairTensorOp:
         elif out.numel() < total:
             raise ValueError("pair-tensor output buffer too small")
         vec = 16 // h.element_size()
-        aligned = all((l1 * l2) % vec == 0 for l1, l2 in zip(l1s, l2s)) and all(o % vec == 0 for o in offs) \
-            and out.data_ptr() % 16 == 0
+        if hT is not None and (hT.shape != (hidden, h.shape[0]) or hT.dtype != h.dtype):
+            raise ValueError("hT must be h transposed")
+        aligned = hT is not None and h.shape[0] % vec == 0 and out.data_ptr() % 16 == 0 \
+            and all(l2 % vec == 0 for l2 in l2s) and all(o % vec == 0 for o in offs) \
+            and all(r % vec == 0 for r in h2_rows)
         tick = _Ticker(events)
         tick("pair_tensor")
         _lib.check(self.lib.di_pair_tensor(dt, _ptr(d), len(l1s), max(l1s), max(l2s), hidden, int(aligned),
-                                           _ptr(h.contiguous()), _ptr(out), _stream()), "di_pair_tensor")
+                                           _ptr(h.contiguous()), _ptr(hT), h.shape[0], _ptr(out), _stream()),
+                   "di_pair_tensor")
         tick(None)
         views = [out[o:o + 2 * hidden * l1 * l2].view(1, 2 * hidden, l1, l2)
                  for o, l1, l2 in zip(offs, l1s, l2s)]

@@ -147,7 +147,7 @@ class LitGINI(nn.Module):
         h2r = [off[b] for _, b in pairs]
         l1 = [gb.nodes_per_graph[a] for a, _ in pairs]
         l2 = [gb.nodes_per_graph[b] for _, b in pairs]
-        _, views = self.pair_op(h, h1r, h2r, l1, l2)
+        _, views = self.pair_op(h, h1r, h2r, l1, l2, hT=self.engine.last_hT)
         logits = [self.interact_forward(v) for v in views]
         return logits, h, e
 

@@ -172,19 +172,20 @@ def edge_blob(sd, li, final, dtype, cfg: GeoTConfig):
     c = f"{p}.conformation_module"
     bb = BlobBuilder(dtype, EL_NBLK_FINAL if final else EL_NBLK, ELV_N_FINAL if final else ELV_N)
     two = lambda a, b: _np(sd[f"{c}.{a}.weight"]) @ _np(sd[f"{c}.{b}.weight"])  # noqa: E731
-    mg = np.zeros((448, 32))
+    mg = np.zeros((320, 32))
     mg[0:128] = _geo_rows(two("dist_linear_1", "dist_linear_0"), "dist")
     mg[128:192] = _geo_rows(two("dir_linear_1", "dir_linear_0"), "dir")
     mg[192:256] = _geo_rows(two("orient_linear_1", "orient_linear_0"), "orient")
     mg[256:320] = _geo_rows(two("amide_linear_1", "amide_linear_0"), "amide")
+    fg = np.zeros((128, 32))
     for kind, name in (("dist", "final_dist_linear"), ("dir", "final_dir_linear"),
                        ("orient", "final_orient_linear"), ("amide", "final_amide_linear")):
-        mg[320:448] += _geo_rows(_np(sd[f"{c}.{name}.weight"]), kind)
+        fg += _geo_rows(_np(sd[f"{c}.{name}.weight"]), kind)
     bb.put(0, mg)
-    bb.put(28, _np(sd[f"{c}.downward_proj.weight"]))
-    bb.put(44, _np(sd[f"{c}.upward_proj.weight"]))
+    bb.put(20, _np(sd[f"{c}.downward_proj.weight"]))
+    bb.put(36, _np(sd[f"{c}.upward_proj.weight"]))
     w, b = lin(sd, f"{c}.orig_msg_linear")
-    bb.put(60, w)
+    bb.put(52, w)
     bb.putv(0, b)
     i = 0
     for kind in ("pre_res_blocks", "post_res_blocks"):
@@ -194,15 +195,16 @@ def edge_blob(sd, li, final, dtype, cfg: GeoTConfig):
             for l in (0, 3, 6):
                 w, b = lin(sd, f"{r}.{l}")
                 w, b = fold_bn_after(w, b, s, t)
-                bb.put(92 + 32 * i, w)
+                bb.put(84 + 32 * i, w)
                 bb.putv(128 + 128 * i, b)
                 i += 1
     w, b = lin(sd, f"{c}.res_connect_linear")
-    bb.put(476, w)
+    bb.put(468, w)
     bb.putv(1664, b)
     w, b = lin(sd, f"{c}.final_linear")
-    bb.put(508, w)
+    bb.put(500, w)
     bb.putv(1792, b)
+    bb.put(532, fg)
     s, t = bn_affine(sd, f"{p}.batch_norm1_edge_feats")
     w, b = fold_bn_before(*lin(sd, f"{p}.mha_module.edge_feats_projection"), s, t)
     bb.put(540, w)

@@ -84,14 +84,18 @@ int di_edge_layer(const di_graph* g, di_dtype dt, int final_layer, const float* 
                   const void* wmat, const float* wvec,
                   float* alpha_out /*[Et,4]*/, void* f_out, void* fn_out, void* stream);
 
+/* hT_out (optional, may be NULL): also write h_out transposed, [128, Nt] (pair-tensor input) */
 int di_node_layer(const di_graph* g, di_dtype dt, int final_layer, const float* alpha,
                   const void* h_in, const void* qkv, const void* wmat, const float* wvec,
-                  void* h_out, void* qkv_out, void* stream);
+                  void* h_out, void* qkv_out, void* hT_out, void* stream);
 
-/* aligned16 != 0 promises every L1*L2 plane and out_off is a multiple of 16 bytes (vector stores) */
+/* h [Nt, hidden] node features; hT (optional, may be NULL) the same transposed [hidden, Nt]
+ * (di_node_layer's hT_out), which turns chain-2 column reads into 16-B vector loads.
+ * aligned16 != 0 promises every L1*L2 plane, out_off, L2 and h2_row are multiples of 16 bytes
+ * worth of elements (vector loads/stores). Output stores are non-temporal (write-once stream). */
 int di_pair_tensor(di_dtype dt, const di_pair_desc* descs /*device [B]*/, int32_t num_complexes,
                    int32_t max_l1, int32_t max_l2, int32_t hidden, int32_t aligned16, const void* h,
-                   void* out, void* stream);
+                   const void* hT, int32_t num_rows, void* out, void* stream);
 
 /* ---- graph builder ----------------------------------------------------------------------- */
 /* Cα kNN per chain: idx_out [Nt,k] chain-local neighbour ids (ascending squared distance,

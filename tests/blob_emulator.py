@@ -63,32 +63,33 @@ class Emu:
         c = c * gs
         z = c @ self.M(ib, 240, 32, 128).T
         F = z @ self.M(ib, 248, 128, 32).T
-        Fn = F @ self.M(ib, 256, 128, 128).T + ib[1].numpy()[:128]
+        Fn = silu(F @ self.M(ib, 256, 128, 128).T + ib[1].numpy()[:128])  # stored post-activation
         L = p.num_layers
         F_last = F
         for li in range(L):
             final = li == L - 1
             eb = p.edge[li]
             V = eb[1].numpy()
-            mg = self.M(eb, 0, 448, 32)
+            mg = self.M(eb, 0, 320, 32)
+            fgm = self.M(eb, 532, 128, 32)
             gate = (G @ mg[128:192].T) * (G @ mg[192:256].T) * (G @ mg[256:320].T)
             dg = G @ mg[0:128].T
-            Wd = self.M(eb, 28, 64, 128)
+            Wd = self.M(eb, 20, 64, 128)
             s = 0
             for j in range(4):
-                x = silu(Fn[nbr[:, j]]) * dg
+                x = Fn[nbr[:, j]] * dg
                 s = s + silu(x @ Wd.T) * gate
-            x = silu(s @ self.M(eb, 44, 128, 64).T) + V[0:128] + F @ self.M(eb, 60, 128, 128).T
+            x = silu(s @ self.M(eb, 36, 128, 64).T) + V[0:128] + F @ self.M(eb, 52, 128, 128).T
             for rb in range(4):
                 if rb == 2:
-                    x = F + silu(x @ self.M(eb, 476, 128, 128).T + V[1664:1792])
+                    x = F + silu(x @ self.M(eb, 468, 128, 128).T + V[1664:1792])
                 y = x
                 for l in range(3):
                     i = 3 * rb + l
-                    y = silu(y @ self.M(eb, 92 + 32 * i, 128, 128).T + V[128 + 128 * i:256 + 128 * i])
+                    y = silu(y @ self.M(eb, 84 + 32 * i, 128, 128).T + V[128 + 128 * i:256 + 128 * i])
                 x = x + y
-            x = x * (G @ mg[320:448].T)
-            conf = F + silu(x @ self.M(eb, 508, 128, 128).T + V[1792:1920])
+            x = x * (G @ fgm.T)
+            conf = F + silu(x @ self.M(eb, 500, 128, 128).T + V[1792:1920])
             P = conf @ self.M(eb, 540, 128, 128).T + V[1920:2048]
             sc = np.clip(qkv[src, 128:256] * qkv[dst, 0:128] / np.sqrt(32), -5, 5) * P
             alpha = np.exp(np.clip(sc.reshape(E, 4, 32).sum(-1), -5, 5))
@@ -99,7 +100,7 @@ class Emu:
                     t_ = silu(e1 @ self.M(eb, 604 + 32 * half, 128, 128).T + V[2176 + 128 * half:2304 + 128 * half])
                     o = o + t_ @ self.M(eb, 668 + 32 * half, 128, 128).T
                 F_next = e1 + o
-                Fn = F_next @ self.M(eb, 732, 128, 128).T + V[2432:2560]
+                Fn = silu(F_next @ self.M(eb, 732, 128, 128).T + V[2432:2560])
             # node layer
             nb = p.node[li]
             NV = nb[1].numpy()

@@ -36,7 +36,7 @@ def test_abi_version_and_blob_sizes():
 def test_invalid_arguments_rejected_without_gpu():
     lib = _lib.load()
     assert lib.di_node_embed(None, 0, 113, None, None, None, None, None, None) == -1
-    assert lib.di_pair_tensor(0, None, 0, 0, 0, 128, 1, None, None, None) == -1
+    assert lib.di_pair_tensor(0, None, 0, 0, 0, 128, 1, None, None, 0, None, None) == -1
     assert lib.di_knn_topk(1, None, None, 20, 10, None, None, None) == -1
 
 

@@ -70,7 +70,8 @@ def test_pair_tensor_exact(engines, case):
     h, _ = engines["f32"].forward(gb)
     n1, n2 = gb.nodes_per_graph
     op = PairTensorOp()
-    _, views = op(h, [0], [n1], [n1], [n2])
+    _, views = op(h, [0], [n1], [n1], [n2], hT=engines["f32"].last_hT)
+    assert torch.equal(engines["f32"].last_hT, h.t())
     torch.cuda.synchronize()
     t = views[0]
     ref = torch.cat((h[:n1].t().unsqueeze(0).unsqueeze(3).expand(1, 128, n1, n2),
