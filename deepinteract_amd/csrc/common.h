@@ -111,6 +111,14 @@ __device__ __forceinline__ void init_vec(Act<NB>& a, const float* vec, int g) {
   for (int b = 0; b < NB; ++b) a.v[b] = ld4(vec + (b * 4 + g) * 4);
 }
 
+// the same from LDS (vector staged with the layer's weights)
+template <int NB>
+__device__ __forceinline__ void init_vec_lds(Act<NB>& a, const float* vec, int g) {
+  const __attribute__((address_space(3))) floatx4* p = (const __attribute__((address_space(3))) floatx4*)vec;
+#pragma unroll
+  for (int b = 0; b < NB; ++b) a.v[b] = p[b * 4 + g];
+}
+
 template <int NB>
 __device__ __forceinline__ void add_vec(Act<NB>& a, const float* vec, int g) {
 #pragma unroll
@@ -297,40 +305,68 @@ __device__ __forceinline__ void dma_blocks(T* lds, const T* g, int nblk) {
   }
 }
 
-// Weight pipeline over one (DBUF=false) or two (DBUF=true) LDS buffers of CAP blocks.
-//   issue(W_next) starts the DMA of the NEXT layer's weights; next() waits for it (barrier,
-//   which also drains this wave's DMA: s_waitcnt vmcnt(0)) and returns the buffer to compute on.
-// With DBUF the DMA of layer i+1 runs under layer i's MFMAs; the buffer it overwrites was last
-// read in layer i-1, before the barrier inside next(). Call pattern per layer:
-//     w = pipe.next(); pipe.issue(next layer); compute(w);
-template <typename T, int NW, bool DBUF, int CAP>
+// Copy `n512` 512-byte fp32 vector chunks (biases) to LDS: half-wave LDS-DMA pieces.
+template <int NW>
+__device__ __forceinline__ void dma_vec(float* lds, const float* g, int n512) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (int i = wave; i < n512; i += NW) {
+    if (lane < 32) {
+      const char* src = reinterpret_cast<const char*>(g) + i * 512 + lane * 16;
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                       (__attribute__((address_space(3))) void*)(reinterpret_cast<char*>(lds) + i * 512),
+                                       16, 0, 0);
+    }
+  }
+}
+
+// Weight pipeline over one (DBUF=false) or two (DBUF=true) LDS slots, each holding CAP packed
+// weight blocks plus VCAP fp32 vector elements (the stage's biases).
+//   issue(W_next, n, V_next, nv) starts the DMA of the NEXT layer's weights and biases; next()
+//   waits for it (barrier, which also drains this wave's DMA: s_waitcnt vmcnt(0)) and makes it
+//   the current slot (w(), v()).
+// With DBUF the DMA of layer i+1 runs under layer i's MFMAs; the slot it overwrites was last read
+// in layer i-1, before the barrier inside next(). Call pattern per layer:
+//     pipe.next(); pipe.issue(next layer); compute(pipe.w(), pipe.v());
+template <typename T, int NW, bool DBUF, int CAP, int VCAP = 0>
 struct WPipe {
-  T* buf0;
-  T* buf1;
+  static constexpr int SLOT_BYTES = CAP * BLK * (int)sizeof(T) + VCAP * 4;
+  char* base;
   int cur;
   const T* pend;
   int pend_n;
-  __device__ explicit WPipe(T* lds) : buf0(lds), buf1(lds + (DBUF ? CAP * BLK : 0)), cur(0), pend(nullptr), pend_n(0) {}
-  __device__ __forceinline__ void issue(const T* g, int nblk) {
+  const float* pendv;
+  int pendv_n;
+  __device__ explicit WPipe(void* lds)
+      : base(reinterpret_cast<char*>(lds)), cur(0), pend(nullptr), pend_n(0), pendv(nullptr), pendv_n(0) {}
+  __device__ __forceinline__ T* slot_w(int s) const { return reinterpret_cast<T*>(base + (DBUF ? s : 0) * SLOT_BYTES); }
+  __device__ __forceinline__ float* slot_v(int s) const {
+    return reinterpret_cast<float*>(base + (DBUF ? s : 0) * SLOT_BYTES + CAP * BLK * (int)sizeof(T));
+  }
+  __device__ __forceinline__ void issue(const T* g, int nblk, const float* gv = nullptr, int nvec = 0) {
     if constexpr (DBUF) {
-      dma_blocks<NW>(cur ? buf0 : buf1, g, nblk);
+      dma_blocks<NW>(slot_w(cur ^ 1), g, nblk);
+      if (gv) dma_vec<NW>(slot_v(cur ^ 1), gv, nvec / 128);
     } else {
       pend = g;
       pend_n = nblk;
+      pendv = gv;
+      pendv_n = nvec;
     }
   }
   __device__ __forceinline__ const T* next() {
     if constexpr (DBUF) {
       __syncthreads();
       cur ^= 1;
-      return cur ? buf1 : buf0;
     } else {
       __syncthreads();
-      dma_blocks<NW>(buf0, pend, pend_n);
+      dma_blocks<NW>(slot_w(0), pend, pend_n);
+      if (pendv) dma_vec<NW>(slot_v(0), pendv, pendv_n / 128);
       __syncthreads();
-      return buf0;
     }
+    return slot_w(cur);
   }
+  __device__ __forceinline__ const T* w() const { return slot_w(cur); }
+  __device__ __forceinline__ const float* v() const { return slot_v(cur); }
 };
 
 // Single synchronous stage (kept for simple kernels).

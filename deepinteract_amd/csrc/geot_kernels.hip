@@ -241,47 +241,62 @@ __global__ __launch_bounds__(Geo<DT>::THREADS, 2) void k_init_edge(InitArgs a) {
 }
 
 // ================================================================ fused edge layer
-// Weight stage order of the edge layer (block offsets and sizes, csrc/layout.h).
-__constant__ int EL_ORDER[24] = {
+// Weight stage order of the edge layer: block offsets / sizes (csrc/layout.h) and the fp32
+// vector (bias) staged with each layer (-1: none).
+__constant__ int EL_ORDER[25] = {
     EL_S0, EL_UP, EL_OM,
     EL_RES + 0 * MAT128, EL_RES + 1 * MAT128, EL_RES + 2 * MAT128,
     EL_RES + 3 * MAT128, EL_RES + 4 * MAT128, EL_RES + 5 * MAT128,
     EL_RC,
     EL_RES + 6 * MAT128, EL_RES + 7 * MAT128, EL_RES + 8 * MAT128,
     EL_RES + 9 * MAT128, EL_RES + 10 * MAT128, EL_RES + 11 * MAT128,
-    EL_F, EL_P,
+    EL_FG, EL_F, EL_P,
     EL_OE, EL_F1, EL_F2, EL_F1 + MAT128, EL_F2 + MAT128, EL_NN};
-__constant__ int EL_SIZE[24] = {36, 16, 32, 32, 32, 32, 32, 32, 32, 32, 32, 32,
-                                32, 32, 32, 32, 40, 32, 32, 32, 32, 32, 32, 32};
-constexpr int EL_NSTAGE_FINAL = 18, EL_NSTAGE = 24;
+__constant__ int EL_SIZE[25] = {36, 16, 32, 32, 32, 32, 32, 32, 32, 32, 32, 32, 32,
+                                32, 32, 32, 8, 32, 32, 32, 32, 32, 32, 32, 32};
+__constant__ int EL_VEC[25] = {-1, ELV_OM, -1,
+                               ELV_RES + 0 * 128, ELV_RES + 1 * 128, ELV_RES + 2 * 128,
+                               ELV_RES + 3 * 128, ELV_RES + 4 * 128, ELV_RES + 5 * 128,
+                               ELV_RC,
+                               ELV_RES + 6 * 128, ELV_RES + 7 * 128, ELV_RES + 8 * 128,
+                               ELV_RES + 9 * 128, ELV_RES + 10 * 128, ELV_RES + 11 * 128,
+                               -1, ELV_F, ELV_P,
+                               ELV_OE, ELV_F1, -1, ELV_F1 + 128, -1, ELV_NN};
+constexpr int EL_NSTAGE_FINAL = 19, EL_NSTAGE = 25;
+constexpr int EL_CAP = 36;
+
+template <class DT>
+using EdgePipe = WPipe<typename DT::T, Geo<DT>::NW, Geo<DT>::DBUF, EL_CAP, 128>;
 
 template <class DT, bool FINAL>
 struct EdgeStages {
   using T = typename DT::T;
-  using G = Geo<DT>;
-  WPipe<T, G::NW, G::DBUF, G::CAP>& pipe;
+  EdgePipe<DT>& pipe;
   const T* W;
+  const float* V;
   int i;
-  // wait for stage i (already issued), start stage i+1, return stage i's buffer
+  // wait for stage i (already issued), start stage i+1; pipe.w()/pipe.v() = stage i
   __device__ const T* next() {
     const T* w = pipe.next();
     const int n = FINAL ? EL_NSTAGE_FINAL : EL_NSTAGE;
-    if (i + 1 < n) pipe.issue(W + EL_ORDER[i + 1] * BLK, EL_SIZE[i + 1]);
+    if (i + 1 < n) {
+      const int vo = EL_VEC[i + 1];
+      pipe.issue(W + EL_ORDER[i + 1] * BLK, EL_SIZE[i + 1], vo >= 0 ? V + vo : nullptr, 128);
+    }
     ++i;
     return w;
   }
 };
 
 template <class DT, bool FINAL>
-__device__ __forceinline__ void res_block(Act<8>& x, EdgeStages<DT, FINAL>& st, const float* V, int idx, int lane,
-                                          int g) {
+__device__ __forceinline__ void res_block(Act<8>& x, EdgeStages<DT, FINAL>& st, int lane, int g) {
   constexpr bool FAST = DT::kBF16;
   Act<8> y = x;
 #pragma unroll 1
   for (int l = 0; l < 3; ++l) {
     const typename DT::T* w = st.next();
     Act<8> t;
-    init_vec(t, V + ELV_RES + 128 * (3 * idx + l), g);
+    init_vec_lds(t, st.pipe.v(), g);
     linear<DT, 8, 4>(t, y, w, lane);
     silu_<8, FAST>(t);
     y = t;
@@ -289,24 +304,27 @@ __device__ __forceinline__ void res_block(Act<8>& x, EdgeStages<DT, FINAL>& st, 
   add_(x, y);
 }
 
+// Two 4-wave blocks per CU, each wave capped at 240 VGPRs (amdgpu_num_vgpr counts the unified
+// VGPR+AGPR file in pairs on gfx950): 2 x 240 + 32 = 512 leaves one pair-tensor wave per SIMD
+// co-resident, so the HBM-bound pair stores run under the MFMA/VALU-bound edge layers.
 template <class DT, bool FINAL>
-__global__ __launch_bounds__(Geo<DT>::THREADS, 2) void k_edge_layer(EdgeArgs a) {
+__global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_eu(2, 2), amdgpu_num_vgpr(120)))
+void k_edge_layer(EdgeArgs a) {
   using T = typename DT::T;
   using G = Geo<DT>;
   constexpr bool FAST = DT::kBF16;
-  __shared__ __attribute__((aligned(16))) T lds[(G::DBUF ? 2 : 1) * G::CAP * BLK];
+  __shared__ __attribute__((aligned(16))) char lds[(G::DBUF ? 2 : 1) * EdgePipe<DT>::SLOT_BYTES];
   const int lane = lane_id(), g = lane >> 4;
   const int r = row_id<G::NW>();
   const bool valid = r < a.Et;
   const int e = valid ? r : a.Et - 1;
   const T* W = reinterpret_cast<const T*>(a.wmat);
-  const float* V = a.wvec;
   const T* fn_in = reinterpret_cast<const T*>(a.fn_in);
   const T* qkv = reinterpret_cast<const T*>(a.qkv);
   const T* f_row = reinterpret_cast<const T*>(a.f_in) + (int64_t)e * HID;
 
-  WPipe<T, G::NW, G::DBUF, G::CAP> pipe(lds);
-  EdgeStages<DT, FINAL> st{pipe, W, 0};
+  EdgePipe<DT> pipe(lds);
+  EdgeStages<DT, FINAL> st{pipe, W, a.wvec, 0};
   pipe.issue(W + EL_S0 * BLK, 36);
 
   const int4 nb = *reinterpret_cast<const int4*>(a.nbr + (int64_t)e * 4);
@@ -320,7 +338,7 @@ __global__ __launch_bounds__(Geo<DT>::THREADS, 2) void k_edge_layer(EdgeArgs a) 
   fr.load(f_row, g);
 
   // ---- neighbour-edge messages (conformation_module_message_func :384-418)
-  const T* w = st.next();  // geometric gates + downward_proj
+  const T* w = st.next();  // stage 0: geometric gates + downward_proj
   Act<4> gate;              // dir . orient . amide embeddings (64)
   {
     Act<4> t1;
@@ -333,7 +351,6 @@ __global__ __launch_bounds__(Geo<DT>::THREADS, 2) void k_edge_layer(EdgeArgs a) 
     mma<4, 1>(t1, gop, w + 16 * BLK, lane);
     mul_(gate, t1);
   }
-
   Act<4> s;
   zero(s);
 #pragma unroll
@@ -363,49 +380,57 @@ __global__ __launch_bounds__(Geo<DT>::THREADS, 2) void k_edge_layer(EdgeArgs a) 
       for (int q = 0; q < 4; ++q) s.v[b][q] += silu<FAST>(y.v[b][q]) * gate.v[b][q];
   }
   Act<8> x;
-  w = st.next();  // upward_proj
+  w = st.next();  // stage 1: upward_proj (+ orig_msg_linear bias)
   zero(x);
   linear<DT, 8, 2>(x, s, w, lane);
   silu_<8, FAST>(x);
-  add_vec(x, V + ELV_OM, g);
-  w = st.next();  // orig_msg_linear(res) + nbr
+  {
+    Act<8> bo;
+    init_vec_lds(bo, pipe.v(), g);
+    add_(x, bo);
+  }
+  w = st.next();  // stage 2: orig_msg_linear(res) + nbr
   mma<8, 4>(x, fr.operand(f_row, g), w, lane);
-  res_block<DT, FINAL>(x, st, V, 0, lane, g);
-  res_block<DT, FINAL>(x, st, V, 1, lane, g);
+  res_block<DT, FINAL>(x, st, lane, g);
+  res_block<DT, FINAL>(x, st, lane, g);
   {
     w = st.next();  // res_connect_linear
     Act<8> y;
-    init_vec(y, V + ELV_RC, g);
+    init_vec_lds(y, pipe.v(), g);
     linear<DT, 8, 4>(y, x, w, lane);
     silu_<8, FAST>(y);
     fr.act(x, f_row, g);
     add_(x, y);
   }
-  res_block<DT, FINAL>(x, st, V, 2, lane, g);
-  res_block<DT, FINAL>(x, st, V, 3, lane, g);
+  res_block<DT, FINAL>(x, st, lane, g);
+  res_block<DT, FINAL>(x, st, lane, g);
   {
-    w = st.next();  // final_linear + final geometric gate
+    w = st.next();  // final geometric gate
     Act<8> fg;
     zero(fg);
-    mma<8, 1>(fg, gop, w + 32 * BLK, lane);
+    mma<8, 1>(fg, gop, w, lane);
     mul_(x, fg);
+    w = st.next();  // final_linear
     Act<8> y;
-    init_vec(y, V + ELV_F, g);
+    init_vec_lds(y, pipe.v(), g);
     linear<DT, 8, 4>(y, x, w, lane);
     silu_<8, FAST>(y);
     fr.act(x, f_row, g);
     add_(x, y);  // conformation output
   }
   // ---- attention scores (propagate_attention :76-91)
+  const int sn = a.src[e], dn = a.dst[e];
+  RawRow<T> kr, qr;  // K[src], Q[dst] in flight under the projection's MFMAs
+  kr.load(qkv + (int64_t)sn * 3 * HID + HID, g);
+  qr.load(qkv + (int64_t)dn * 3 * HID, g);
   w = st.next();  // edge_feats_projection(BN1e(conf))
   Act<8> p;
-  init_vec(p, V + ELV_P, g);
+  init_vec_lds(p, pipe.v(), g);
   linear<DT, 8, 4>(p, x, w, lane);
   {
-    const int sn = a.src[e], dn = a.dst[e];
     Act<8> kq, qd;
-    load_row(kq, qkv + (int64_t)sn * 3 * HID + HID, g);
-    load_row(qd, qkv + (int64_t)dn * 3 * HID, g);
+    kr.to_act(kq);
+    qr.to_act(qd);
     const float scale = 5.656854249492381f;  // np.sqrt(32)
 #pragma unroll
     for (int b = 0; b < 8; ++b)
@@ -425,7 +450,7 @@ __global__ __launch_bounds__(Geo<DT>::THREADS, 2) void k_edge_layer(EdgeArgs a) 
     // ---- edge output: e = in + O_e(e_out); e = e + FFN(BN2e(e)) (:697-724)
     w = st.next();  // O_edge_feats
     Act<8> e1;
-    init_vec(e1, V + ELV_OE, g);
+    init_vec_lds(e1, pipe.v(), g);
     linear<DT, 8, 4>(e1, p, w, lane);
     {
       Act<8> fa;
@@ -438,7 +463,7 @@ __global__ __launch_bounds__(Geo<DT>::THREADS, 2) void k_edge_layer(EdgeArgs a) 
     for (int half = 0; half < 2; ++half) {
       w = st.next();  // edge_feats_MLP.0 (BN2e folded), hidden half
       Act<8> t;
-      init_vec(t, V + ELV_F1 + 128 * half, g);
+      init_vec_lds(t, pipe.v(), g);
       linear<DT, 8, 4>(t, e1, w, lane);
       silu_<8, FAST>(t);
       w = st.next();  // edge_feats_MLP.3, input half
@@ -448,7 +473,7 @@ __global__ __launch_bounds__(Geo<DT>::THREADS, 2) void k_edge_layer(EdgeArgs a) 
     if (valid) store_row(e1, reinterpret_cast<T*>(a.f_out) + (int64_t)e * HID, g);
     w = st.next();  // next layer's silu(nbr_linear(.))
     Act<8> fn;
-    init_vec(fn, V + ELV_NN, g);
+    init_vec_lds(fn, pipe.v(), g);
     linear<DT, 8, 4>(fn, e1, w, lane);
     silu_<8, FAST>(fn);
     if (valid) store_row(fn, reinterpret_cast<T*>(a.fn_out) + (int64_t)e * HID, g);
