@@ -61,11 +61,15 @@ def load(build_if_missing: bool = True):
     # torch ships its own libamdhip64.so.7: load it first so this library binds to the SAME HIP
     # runtime (same SONAME) instead of pulling /opt/rocm's copy into the process.
     import torch  # noqa: F401
-    if not os.path.exists(_build.LIB) or (build_if_missing and not _build.up_to_date()):
+    path = os.environ.get("DI_LIB")  # a tuning variant built by build.build_variant()
+    if path:
+        if not os.path.exists(path):
+            raise RuntimeError(f"DI_LIB={path} does not exist")
+    elif not os.path.exists(_build.LIB) or (build_if_missing and not _build.up_to_date()):
         if not build_if_missing:
             raise RuntimeError(f"deepinteract_amd HIP library missing: {_build.LIB}")
         _build.build()
-    lib = ctypes.CDLL(_build.LIB)
+    lib = ctypes.CDLL(path or _build.LIB)
     for name, (argtypes, restype) in _SIGS.items():
         fn = getattr(lib, name)
         fn.argtypes = argtypes

@@ -38,15 +38,19 @@ def up_to_date() -> bool:
     return all(os.path.getmtime(p) <= t for p in _deps())
 
 
-def build(force: bool = False, verbose: bool = True) -> str:
-    if not force and up_to_date():
+def build(force: bool = False, verbose: bool = True, defines=(), out: str | None = None) -> str:
+    """Build the library. ``defines``/``out`` build a tuning variant (extra -D flags) into its
+    own directory, loaded with DI_LIB=<path> (kernel experiments compared in one GPU session)."""
+    lib_path = out or LIB
+    if not force and not defines and out is None and up_to_date():
         return LIB
-    os.makedirs(os.path.join(LIBDIR, "obj"), exist_ok=True)
+    objdir = os.path.join(os.path.dirname(lib_path), "obj")
+    os.makedirs(objdir, exist_ok=True)
     objs = []
 
     def compile_one(src):
-        obj = os.path.join(LIBDIR, "obj", os.path.basename(src).replace(".hip", ".o"))
-        cmd = [HIPCC, *CFLAGS, "-c", src, "-o", obj]
+        obj = os.path.join(objdir, os.path.basename(src).replace(".hip", ".o"))
+        cmd = [HIPCC, *CFLAGS, *[f"-D{d}" for d in defines], "-c", src, "-o", obj]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr}")
@@ -54,13 +58,17 @@ def build(force: bool = False, verbose: bool = True) -> str:
 
     with cf.ThreadPoolExecutor(max_workers=min(8, len(_sources()))) as ex:
         objs = list(ex.map(compile_one, _sources()))
-    cmd = [HIPCC, "-shared", f"--offload-arch={ARCH}", "-o", LIB, *objs]
+    cmd = [HIPCC, "-shared", f"--offload-arch={ARCH}", "-o", lib_path, *objs]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed:\n{r.stderr}")
     if verbose:
-        print(f"built {LIB}", file=sys.stderr)
-    return LIB
+        print(f"built {lib_path}", file=sys.stderr)
+    return lib_path
+
+
+def build_variant(name: str, defines) -> str:
+    return build(defines=defines, out=os.path.join(LIBDIR, "variants", name, "libdeepinteract_amd.so"))
 
 
 if __name__ == "__main__":

@@ -88,6 +88,11 @@ __device__ __forceinline__ float expf_(float x) {
 // exact path keeps the IEEE division (~10 ops) for fp32 parity.
 template <bool FAST>
 __device__ __forceinline__ float silu(float x) {
+#if defined(DI_X_NOSILU)  // timing experiment only
+  if constexpr (FAST) return x;
+#elif defined(DI_X_HALFSILU)  // timing experiment only: one transcendental
+  if constexpr (FAST) return x * __expf(-x);
+#endif
   if constexpr (FAST) return x * __builtin_amdgcn_rcpf(1.0f + __expf(-x));
   else return x / (1.0f + expf(-x));
 }
@@ -252,16 +257,39 @@ __device__ __forceinline__ void unpack_op(Act<2 * NS>& a, const Op<BF16T, NS>& o
 }
 
 // out (NBO 16-row blocks) += W (NBO x NS packed blocks, in LDS) . op (NS 32-feature k-steps)
+#ifndef DI_MMA_ORDER
+#define DI_MMA_ORDER 3
+#endif
 template <int NBO, int NS>
 __device__ __forceinline__ void mma(Act<NBO>& out, const Op<BF16T, NS>& op, const u16* w, int lane) {
+  if constexpr (DI_MMA_ORDER == 0 || DI_MMA_ORDER == 2) {  // k-step major
 #pragma unroll
-  for (int s = 0; s < NS; ++s) {
+    for (int s = 0; s < NS; ++s) {
 #pragma unroll
-    for (int bo = 0; bo < NBO; ++bo) {
-      const bf16x8 af = *reinterpret_cast<const bf16x8*>(w + (bo * NS + s) * BLK + lane * 8);
-      out.v[bo] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, op.f[s], out.v[bo], 0, 0, 0);
+      for (int bo = 0; bo < NBO; ++bo) {
+#ifdef DI_X_NOLDSA  // timing experiment only: no LDS operand reads
+        const bf16x8 af = op.f[(s + bo) % NS];
+#else
+        const bf16x8 af = *reinterpret_cast<const bf16x8*>(w + (bo * NS + s) * BLK + lane * 8);
+#endif
+        out.v[bo] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, op.f[s], out.v[bo], 0, 0, 0);
+      }
+      if constexpr (DI_MMA_ORDER == 0)
+        __builtin_amdgcn_sched_barrier(0);  // bound the LDS fragments in flight (register pressure)
     }
-    __builtin_amdgcn_sched_barrier(0);  // bound the LDS fragments in flight (register pressure)
+  } else {  // output-block-pair major: blocks complete early (their epilogue can overlap)
+    constexpr int G = NBO < 2 ? NBO : 2;
+#pragma unroll
+    for (int b0 = 0; b0 < NBO; b0 += G) {
+#pragma unroll
+      for (int s = 0; s < NS; ++s)
+#pragma unroll
+        for (int bo = b0; bo < b0 + G; ++bo) {
+          const bf16x8 af = *reinterpret_cast<const bf16x8*>(w + (bo * NS + s) * BLK + lane * 8);
+          out.v[bo] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, op.f[s], out.v[bo], 0, 0, 0);
+        }
+      if constexpr (DI_MMA_ORDER == 1) __builtin_amdgcn_sched_barrier(0);
+    }
   }
 }
 template <int NBO, int NS>
@@ -293,30 +321,39 @@ __device__ __forceinline__ void linear(Act<NBO>& out, const Act<2 * NS>& a, cons
 // Copy `nblk` packed blocks (512 elements each) from global memory to LDS with LDS-DMA
 // (global_load_lds_dwordx4: 1 KiB per wave-instruction, lane-linear destination = the packed
 // order). Issued by all NW waves of the block; completion is awaited by the next barrier.
+// Issued as buffer_load_dwordx4 ... lds with an SGPR buffer resource and SGPR offset, and the
+// wave index made wave-uniform (readfirstlane): per 1 KiB piece the loop is scalar except the
+// load itself (s_mov m0, s_add, buffer_load; the lane offset is a loop-invariant VGPR).
+constexpr int BUF_RSRC_W3 = 0x00020000;  // gfx9 raw buffer: DATA_FORMAT 32, no swizzle / stride
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* g) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(g), 0, 0x7fffffff, BUF_RSRC_W3);
+}
+
 template <int NW, typename T>
 __device__ __forceinline__ void dma_blocks(T* lds, const T* g, int nblk) {
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int loff = (threadIdx.x & 63) * 16;
   const int nkib = nblk * BLK * (int)sizeof(T) / 1024;
-  for (int i = wave; i < nkib; i += NW) {
-    const char* src = reinterpret_cast<const char*>(g) + i * 1024 + lane * 16;
-    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                     (__attribute__((address_space(3))) void*)(reinterpret_cast<char*>(lds) + i * 1024),
-                                     16, 0, 0);
-  }
+#ifdef DI_X_NODMA  // timing experiment only: weights are never loaded
+  if (nkib > 0) return;
+#endif
+  const __amdgpu_buffer_rsrc_t r = buf_rsrc(g);
+  for (int i = wave; i < nkib; i += NW)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(
+        r, (__attribute__((address_space(3))) void*)(reinterpret_cast<char*>(lds) + i * 1024), 16, loff, i * 1024, 0, 0);
 }
 
 // Copy `n512` 512-byte fp32 vector chunks (biases) to LDS: half-wave LDS-DMA pieces.
 template <int NW>
 __device__ __forceinline__ void dma_vec(float* lds, const float* g, int n512) {
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  for (int i = wave; i < n512; i += NW) {
-    if (lane < 32) {
-      const char* src = reinterpret_cast<const char*>(g) + i * 512 + lane * 16;
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                       (__attribute__((address_space(3))) void*)(reinterpret_cast<char*>(lds) + i * 512),
-                                       16, 0, 0);
-    }
-  }
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const __amdgpu_buffer_rsrc_t r = buf_rsrc(g);
+  if (lane < 32)
+    for (int i = wave; i < n512; i += NW)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          r, (__attribute__((address_space(3))) void*)(reinterpret_cast<char*>(lds) + i * 512), 16, lane * 16, i * 512, 0, 0);
 }
 
 // Weight pipeline over one (DBUF=false) or two (DBUF=true) LDS slots, each holding CAP packed
@@ -355,7 +392,9 @@ struct WPipe {
   }
   __device__ __forceinline__ const T* next() {
     if constexpr (DBUF) {
+#ifndef DI_X_NOBAR  // timing experiment only: results are wrong without the barrier
       __syncthreads();
+#endif
       cur ^= 1;
     } else {
       __syncthreads();

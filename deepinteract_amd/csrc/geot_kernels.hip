@@ -87,8 +87,11 @@ __device__ __forceinline__ int row_id() {
 // SIMD's MFMA pipe while these run their SiLU VALU work (and vice versa).
 // fp32 (parity path; stages twice as large): same geometry, synchronous single-buffered stages.
 template <class DT>
+#ifndef DI_GEO_NW
+#define DI_GEO_NW 4
+#endif
 struct Geo {
-  static constexpr int NW = 4;
+  static constexpr int NW = DI_GEO_NW;  // waves per block (2 waves per SIMD either way)
   static constexpr bool DBUF = DT::kBF16;
   static constexpr int CAP = 40;  // blocks per weight stage buffer
   static constexpr int THREADS = 64 * NW;
@@ -165,7 +168,8 @@ __global__ __launch_bounds__(THREADS) void k_node_embed(EmbedArgs a) {
 
 // ================================================================ InitEdgeModule (+ layer-0 nbr_linear)
 template <class DT>
-__global__ __launch_bounds__(Geo<DT>::THREADS, 2) void k_init_edge(InitArgs a) {
+__global__ __attribute__((amdgpu_flat_work_group_size(1, 64 * DI_GEO_NW), amdgpu_waves_per_eu(2, 2)))
+void k_init_edge(InitArgs a) {
   using T = typename DT::T;
   using G = Geo<DT>;
   constexpr bool FAST = DT::kBF16;
@@ -308,7 +312,8 @@ __device__ __forceinline__ void res_block(Act<8>& x, EdgeStages<DT, FINAL>& st, 
 // VGPR+AGPR file in pairs on gfx950): 2 x 240 + 32 = 512 leaves one pair-tensor wave per SIMD
 // co-resident, so the HBM-bound pair stores run under the MFMA/VALU-bound edge layers.
 template <class DT, bool FINAL>
-__global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_eu(2, 2), amdgpu_num_vgpr(120)))
+__global__ __attribute__((amdgpu_flat_work_group_size(1, 64 * DI_GEO_NW), amdgpu_waves_per_eu(2, 2),
+                          amdgpu_num_vgpr(120)))
 void k_edge_layer(EdgeArgs a) {
   using T = typename DT::T;
   using G = Geo<DT>;

@@ -1,0 +1,33 @@
+"""Build kernel-tuning variants of the library (lib/variants/<name>/), compared on the GPU in
+one session with DI_LIB=<path> (tools/variants.sh)."""
+import concurrent.futures as cf
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from deepinteract_amd import build
+
+VARIANTS = {
+    "base": [],
+    "order1": ["DI_MMA_ORDER=1"],
+    "order2": ["DI_MMA_ORDER=2"],
+    "order3": ["DI_MMA_ORDER=3"],
+    "nobar": ["DI_X_NOBAR"],
+    "nosilu": ["DI_X_NOSILU"],
+    "halfsilu": ["DI_X_HALFSILU"],
+    "nodma": ["DI_X_NODMA"],
+    "nodma_nobar": ["DI_X_NODMA", "DI_X_NOBAR"],
+    "nodma_nosilu": ["DI_X_NODMA", "DI_X_NOSILU"],
+    "nodma_nobar_nosilu": ["DI_X_NODMA", "DI_X_NOBAR", "DI_X_NOSILU"],
+    "strip_noldsa": ["DI_X_NODMA", "DI_X_NOBAR", "DI_X_NOSILU", "DI_X_NOLDSA"],
+    "noldsa": ["DI_X_NOLDSA"],
+    "nw8": ["DI_GEO_NW=8"],
+    "nw8_order3": ["DI_GEO_NW=8", "DI_MMA_ORDER=3"],
+}
+
+if __name__ == "__main__":
+    names = sys.argv[1:] or list(VARIANTS)
+    with cf.ThreadPoolExecutor(2) as ex:
+        for p in ex.map(lambda n: build.build_variant(n, VARIANTS[n]), names):
+            print(p)
