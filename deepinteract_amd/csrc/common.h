@@ -404,6 +404,54 @@ struct WPipe {
     }
     return slot_w(cur);
   }
+  __device__ __forceinline__ void mid() const {}
+  __device__ __forceinline__ const T* w() const { return slot_w(cur); }
+  __device__ __forceinline__ const float* v() const { return slot_v(cur); }
+};
+
+// Ping-pong ring for 8-wave blocks: waves 0-3 (group 0) and 4-7 (group 1) run the same layer
+// sequence half a stage apart, so on every SIMD one wave is in a layer's MFMA half while its
+// partner is in the previous layer's SiLU/VALU half (the two waves of a SIMD come from the two
+// groups). Every wave calls next() (stage barrier, full wait) and mid() (bare s_barrier) once per
+// stage; group 1 starts and group 0 ends with one extra mid(), so their barrier counts match and
+// group 1's stage boundaries fall on group 0's mid-points. Only group 0 issues the LDS-DMA, at its
+// stage start, into the slot of stage i-2 (NSLOT = 3): group 1 finished that stage one barrier
+// earlier, and the DMA lands before group 0's next stage barrier (its own vmcnt(0) there).
+template <typename T, int CAP, int VCAP>
+struct RingPipe {
+  static constexpr int NSLOT = 3;
+  static constexpr int SLOT_BYTES = CAP * BLK * (int)sizeof(T) + VCAP * 4;
+  char* base;
+  int cur;
+  bool loader;
+  __device__ explicit RingPipe(void* lds) : base(reinterpret_cast<char*>(lds)), cur(NSLOT - 1) {
+    loader = __builtin_amdgcn_readfirstlane(threadIdx.x >> 8) == 0;
+  }
+  __device__ __forceinline__ T* slot_w(int s) const { return reinterpret_cast<T*>(base + s * SLOT_BYTES); }
+  __device__ __forceinline__ float* slot_v(int s) const {
+    return reinterpret_cast<float*>(base + s * SLOT_BYTES + CAP * BLK * (int)sizeof(T));
+  }
+  __device__ __forceinline__ int nxt(int s) const { return s == NSLOT - 1 ? 0 : s + 1; }
+  // DMA of the stage AFTER the current one (group 0 only)
+  __device__ __forceinline__ void issue(const T* g, int nblk, const float* gv = nullptr, int nvec = 0) {
+    if (loader) {
+      const int s = nxt(cur);
+      dma_blocks<4>(slot_w(s), g, nblk);
+      if (gv) dma_vec<4>(slot_v(s), gv, nvec / 128);
+    }
+  }
+  __device__ __forceinline__ const T* next() {
+    __syncthreads();
+    cur = nxt(cur);
+    return slot_w(cur);
+  }
+  __device__ __forceinline__ void mid() const {
+#ifndef DI_X_NOMID
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+#endif
+  }
   __device__ __forceinline__ const T* w() const { return slot_w(cur); }
   __device__ __forceinline__ const float* v() const { return slot_v(cur); }
 };

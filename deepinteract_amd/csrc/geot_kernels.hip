@@ -14,6 +14,7 @@
 //   * two-stage geometric embeddings (W1 . W0 . g) pre-multiplied on the host;
 //   * InitEdge's emb[src]/emb[dst] slots of combined_linear_0 precomputed per node position
 //     (pos tables [2304,128]); the 4 final gates summed before multiplying (a*x+b*x = (a+b)*x).
+#include <type_traits>
 #include "common.h"
 #include "layout.h"
 #include "../../include/deepinteract_amd.h"
@@ -109,6 +110,12 @@ struct FRow<BF16T> {
     Act<8> a;
     load_row(a, row, g);
     make_op(op, a);
+  }
+  // the raw row IS the packed operand: op.f[s] = {u[2s].x, u[2s].y, u[2s+1].x, u[2s+1].y}
+  __device__ void set_raw(const RawRow<u16>& r) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      op.f[k] = __builtin_bit_cast(bf16x8, (uint4){r.u[2 * k].x, r.u[2 * k].y, r.u[2 * k + 1].x, r.u[2 * k + 1].y});
   }
   __device__ void act(Act<8>& a, const u16*, int) const { unpack_op(a, op); }
   __device__ const Op<BF16T, 4>& operand(const u16*, int) const { return op; }
@@ -269,8 +276,25 @@ __constant__ int EL_VEC[25] = {-1, ELV_OM, -1,
 constexpr int EL_NSTAGE_FINAL = 19, EL_NSTAGE = 25;
 constexpr int EL_CAP = 36;
 
+// bf16: 8-wave ping-pong blocks (RingPipe, one block per CU, 128 rows per weight pass);
+// fp32 parity path: 4-wave blocks with synchronous stages (WPipe).
+#ifndef DI_EDGE_PP
+#define DI_EDGE_PP 0  // measured: 8-wave ping-pong 631 us vs 498 us for two 4-wave blocks per CU (C3 edge layer)
+#endif
 template <class DT>
-using EdgePipe = WPipe<typename DT::T, Geo<DT>::NW, Geo<DT>::DBUF, EL_CAP, 128>;
+struct EdgeGeo {
+  static constexpr bool PP = DT::kBF16 && DI_EDGE_PP;
+  static constexpr int NW = PP ? 8 : Geo<DT>::NW;
+  static constexpr int THREADS = 64 * NW;
+  static constexpr int ROWS = ROWS_PER_WAVE * NW;
+};
+template <class DT>
+using EdgePipe = std::conditional_t<EdgeGeo<DT>::PP, RingPipe<typename DT::T, EL_CAP, 128>,
+                                    WPipe<typename DT::T, Geo<DT>::NW, Geo<DT>::DBUF, EL_CAP, 128>>;
+template <class DT>
+constexpr int edge_lds_bytes() {
+  return (EdgeGeo<DT>::PP ? 3 : (Geo<DT>::DBUF ? 2 : 1)) * EdgePipe<DT>::SLOT_BYTES;
+}
 
 template <class DT, bool FINAL>
 struct EdgeStages {
@@ -278,14 +302,16 @@ struct EdgeStages {
   EdgePipe<DT>& pipe;
   const T* W;
   const float* V;
-  int i;
+  int i;      // stage whose DMA is pending / current
+  bool more;  // another tile follows: the last stage wraps to stage 0 of the next tile
   // wait for stage i (already issued), start stage i+1; pipe.w()/pipe.v() = stage i
   __device__ const T* next() {
     const T* w = pipe.next();
     const int n = FINAL ? EL_NSTAGE_FINAL : EL_NSTAGE;
-    if (i + 1 < n) {
-      const int vo = EL_VEC[i + 1];
-      pipe.issue(W + EL_ORDER[i + 1] * BLK, EL_SIZE[i + 1], vo >= 0 ? V + vo : nullptr, 128);
+    const int ni = i + 1 < n ? i + 1 : (more ? 0 : -1);
+    if (ni >= 0) {
+      const int vo = EL_VEC[ni];
+      pipe.issue(W + EL_ORDER[ni] * BLK, EL_SIZE[ni], vo >= 0 ? V + vo : nullptr, 128);
     }
     ++i;
     return w;
@@ -302,187 +328,253 @@ __device__ __forceinline__ void res_block(Act<8>& x, EdgeStages<DT, FINAL>& st, 
     Act<8> t;
     init_vec_lds(t, st.pipe.v(), g);
     linear<DT, 8, 4>(t, y, w, lane);
+    st.pipe.mid();
     silu_<8, FAST>(t);
     y = t;
   }
   add_(x, y);
 }
 
+// One tile's per-row inputs, loaded a tile ahead (persistent blocks): neighbour ids, the 28 edge
+// features, the edge's own row F (bf16: raw, it IS the packed MFMA operand) and the first
+// neighbour row. The loads are issued during the previous tile's last stages.
+template <class DT>
+struct EdgeIn {
+  using T = typename DT::T;
+  int4 nb;
+  Act<2> geo;
+  RawRow<T> fraw;
+  RawRow<T> xn;
+  __device__ __forceinline__ void load_ids(const EdgeArgs& a, int e) {
+    nb = *reinterpret_cast<const int4*>(a.nbr + (int64_t)e * 4);
+  }
+  __device__ __forceinline__ void load_rest(const EdgeArgs& a, int e, int g) {
+    load_edge_geo(geo, a.edge_f + (int64_t)e * NFEAT_E, g);
+    if constexpr (DT::kBF16) fraw.load(reinterpret_cast<const T*>(a.f_in) + (int64_t)e * HID, g);
+    xn.load(reinterpret_cast<const T*>(a.fn_in) + (int64_t)nb.x * HID, g);
+  }
+};
+
+template <class DT>
+__device__ __forceinline__ int tile_edge(int tile, int Et, bool& valid) {
+  const int r = tile * EdgeGeo<DT>::ROWS + (threadIdx.x >> 6) * ROWS_PER_WAVE + (threadIdx.x & 15);
+  valid = r < Et;
+  return valid ? r : Et - 1;
+}
+
 // Two 4-wave blocks per CU, each wave capped at 240 VGPRs (amdgpu_num_vgpr counts the unified
 // VGPR+AGPR file in pairs on gfx950): 2 x 240 + 32 = 512 leaves one pair-tensor wave per SIMD
 // co-resident, so the HBM-bound pair stores run under the MFMA/VALU-bound edge layers.
+// Persistent: each block walks tiles blockIdx.x, +gridDim.x, ...; the weight-stage stream runs on
+// across tiles (the last stage's DMA slot fetches stage 0 of the next tile) and the next tile's
+// inputs are prefetched under the current tile's last stages, so no tile pays a cold prologue.
 template <class DT, bool FINAL>
-__global__ __attribute__((amdgpu_flat_work_group_size(1, 64 * DI_GEO_NW), amdgpu_waves_per_eu(2, 2),
-                          amdgpu_num_vgpr(120)))
+__global__ __attribute__((amdgpu_flat_work_group_size(1, 512), amdgpu_waves_per_eu(2, 2), amdgpu_num_vgpr(120)))
 void k_edge_layer(EdgeArgs a) {
   using T = typename DT::T;
-  using G = Geo<DT>;
+  using G = EdgeGeo<DT>;
   constexpr bool FAST = DT::kBF16;
-  __shared__ __attribute__((aligned(16))) char lds[(G::DBUF ? 2 : 1) * EdgePipe<DT>::SLOT_BYTES];
+  __shared__ __attribute__((aligned(16))) char lds[edge_lds_bytes<DT>()];
   const int lane = lane_id(), g = lane >> 4;
-  const int r = row_id<G::NW>();
-  const bool valid = r < a.Et;
-  const int e = valid ? r : a.Et - 1;
+  const int ntiles = (a.Et + G::ROWS - 1) / G::ROWS;
   const T* W = reinterpret_cast<const T*>(a.wmat);
   const T* fn_in = reinterpret_cast<const T*>(a.fn_in);
   const T* qkv = reinterpret_cast<const T*>(a.qkv);
-  const T* f_row = reinterpret_cast<const T*>(a.f_in) + (int64_t)e * HID;
 
   EdgePipe<DT> pipe(lds);
-  EdgeStages<DT, FINAL> st{pipe, W, a.wvec, 0};
-  pipe.issue(W + EL_S0 * BLK, 36);
+  EdgeStages<DT, FINAL> st{pipe, W, a.wvec, 0, false};
+  pipe.issue(W + EL_S0 * BLK, EL_SIZE[0]);
+#ifdef DI_X_STAGGER
+  if (blockIdx.x & 1) __builtin_amdgcn_s_sleep(DI_X_STAGGER);
+#endif
+  if (G::PP && (threadIdx.x >> 8)) pipe.mid();  // group 1 runs half a stage behind group 0
+#ifdef DI_X_PRIO
+  if (G::PP && (threadIdx.x >> 8)) __builtin_amdgcn_s_setprio(DI_X_PRIO);
+#endif
+  EdgeIn<DT> in;
+  {
+    bool v0;
+    const int e0 = tile_edge<DT>(blockIdx.x, a.Et, v0);
+    in.load_ids(a, e0);
+    in.load_rest(a, e0, g);
+  }
 
-  const int4 nb = *reinterpret_cast<const int4*>(a.nbr + (int64_t)e * 4);
-  RawRow<T> xn;
-  xn.load(fn_in + (int64_t)nb.x * HID, g);  // first neighbour row in flight early
-  Act<2> geo;
-  load_edge_geo(geo, a.edge_f + (int64_t)e * NFEAT_E, g);
-  Op<DT, 1> gop;
-  make_op(gop, geo);
-  FRow<DT> fr;
-  fr.load(f_row, g);
-
-  // ---- neighbour-edge messages (conformation_module_message_func :384-418)
-  const T* w = st.next();  // stage 0: geometric gates + downward_proj
-  Act<4> gate;              // dir . orient . amide embeddings (64)
-  {
-    Act<4> t1;
-    zero(gate);
-    mma<4, 1>(gate, gop, w + 8 * BLK, lane);
-    zero(t1);
-    mma<4, 1>(t1, gop, w + 12 * BLK, lane);
-    mul_(gate, t1);
-    zero(t1);
-    mma<4, 1>(t1, gop, w + 16 * BLK, lane);
-    mul_(gate, t1);
-  }
-  Act<4> s;
-  zero(s);
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    Act<8> x;
-    xn.to_act(x);
-    if (j < 3) {  // prefetch the next neighbour row under this one's MFMAs
-      const int nx = j == 0 ? nb.y : (j == 1 ? nb.z : nb.w);
-      xn.load(fn_in + (int64_t)nx * HID, g);
-    }
-    // dist_linear_1(dist_linear_0(dist)), recomputed per neighbour (8 MFMAs) rather than held
-    // live across the loop: the memory clobber stops the compiler from hoisting it (32 VGPRs)
-    asm volatile("" ::: "memory");
-    Act<8> dg;
-    zero(dg);
-    mma<8, 1>(dg, gop, w, lane);
-#pragma unroll
-    for (int b = 0; b < 8; ++b)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) x.v[b][q] *= dg.v[b][q];  // gathered rows are silu(nbr_linear(F))
-    Act<4> y;
-    zero(y);
-    linear<DT, 4, 4>(y, x, w + 20 * BLK, lane);  // downward_proj
-#pragma unroll
-    for (int b = 0; b < 4; ++b)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) s.v[b][q] += silu<FAST>(y.v[b][q]) * gate.v[b][q];
-  }
-  Act<8> x;
-  w = st.next();  // stage 1: upward_proj (+ orig_msg_linear bias)
-  zero(x);
-  linear<DT, 8, 2>(x, s, w, lane);
-  silu_<8, FAST>(x);
-  {
-    Act<8> bo;
-    init_vec_lds(bo, pipe.v(), g);
-    add_(x, bo);
-  }
-  w = st.next();  // stage 2: orig_msg_linear(res) + nbr
-  mma<8, 4>(x, fr.operand(f_row, g), w, lane);
-  res_block<DT, FINAL>(x, st, lane, g);
-  res_block<DT, FINAL>(x, st, lane, g);
-  {
-    w = st.next();  // res_connect_linear
-    Act<8> y;
-    init_vec_lds(y, pipe.v(), g);
-    linear<DT, 8, 4>(y, x, w, lane);
-    silu_<8, FAST>(y);
-    fr.act(x, f_row, g);
-    add_(x, y);
-  }
-  res_block<DT, FINAL>(x, st, lane, g);
-  res_block<DT, FINAL>(x, st, lane, g);
-  {
-    w = st.next();  // final geometric gate
-    Act<8> fg;
-    zero(fg);
-    mma<8, 1>(fg, gop, w, lane);
-    mul_(x, fg);
-    w = st.next();  // final_linear
-    Act<8> y;
-    init_vec_lds(y, pipe.v(), g);
-    linear<DT, 8, 4>(y, x, w, lane);
-    silu_<8, FAST>(y);
-    fr.act(x, f_row, g);
-    add_(x, y);  // conformation output
-  }
-  // ---- attention scores (propagate_attention :76-91)
-  const int sn = a.src[e], dn = a.dst[e];
-  RawRow<T> kr, qr;  // K[src], Q[dst] in flight under the projection's MFMAs
-  kr.load(qkv + (int64_t)sn * 3 * HID + HID, g);
-  qr.load(qkv + (int64_t)dn * 3 * HID, g);
-  w = st.next();  // edge_feats_projection(BN1e(conf))
-  Act<8> p;
-  init_vec_lds(p, pipe.v(), g);
-  linear<DT, 8, 4>(p, x, w, lane);
-  {
-    Act<8> kq, qd;
-    kr.to_act(kq);
-    qr.to_act(qd);
-    const float scale = 5.656854249492381f;  // np.sqrt(32)
-#pragma unroll
-    for (int b = 0; b < 8; ++b)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        float sc = FAST ? (kq.v[b][q] * qd.v[b][q]) * (1.0f / scale) : (kq.v[b][q] * qd.v[b][q]) / scale;
-        sc = fminf(fmaxf(sc, -5.f), 5.f);
-        p.v[b][q] = sc * p.v[b][q];  // score = e_out
-      }
-  }
-  floatx4 al;
-#pragma unroll
-  for (int h = 0; h < 4; ++h) al[h] = expf_<FAST>(fminf(fmaxf(head_sum(p, h), -5.f), 5.f));
-  if (valid && g == 0) st4(a.alpha_out + (int64_t)e * 4, al);
-
-  if constexpr (!FINAL) {
-    // ---- edge output: e = in + O_e(e_out); e = e + FFN(BN2e(e)) (:697-724)
-    w = st.next();  // O_edge_feats
-    Act<8> e1;
-    init_vec_lds(e1, pipe.v(), g);
-    linear<DT, 8, 4>(e1, p, w, lane);
-    {
-      Act<8> fa;
-      fr.act(fa, f_row, g);
-      add_(e1, fa);
-    }
-    Act<8> o;
-    zero(o);
 #pragma unroll 1
-    for (int half = 0; half < 2; ++half) {
-      w = st.next();  // edge_feats_MLP.0 (BN2e folded), hidden half
-      Act<8> t;
-      init_vec_lds(t, pipe.v(), g);
-      linear<DT, 8, 4>(t, e1, w, lane);
-      silu_<8, FAST>(t);
-      w = st.next();  // edge_feats_MLP.3, input half
-      linear<DT, 8, 4>(o, t, w, lane);
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    bool valid;
+    const int e = tile_edge<DT>(tile, a.Et, valid);
+    const bool more = tile + (int)gridDim.x < ntiles;
+    bool vn;
+    const int en = tile_edge<DT>(more ? tile + gridDim.x : tile, a.Et, vn);
+    st.i = 0;
+    st.more = more;
+    const T* f_row = reinterpret_cast<const T*>(a.f_in) + (int64_t)e * HID;
+
+    const int4 nb = in.nb;
+    Op<DT, 1> gop;
+    make_op(gop, in.geo);
+    FRow<DT> fr;
+    if constexpr (DT::kBF16) fr.set_raw(in.fraw);
+
+    // ---- neighbour-edge messages (conformation_module_message_func :384-418)
+    const T* w = st.next();  // stage 0: geometric gates + downward_proj
+    Act<4> gate;              // dir . orient . amide embeddings (64)
+    {
+      Act<4> t1;
+      zero(gate);
+      mma<4, 1>(gate, gop, w + 8 * BLK, lane);
+      zero(t1);
+      mma<4, 1>(t1, gop, w + 12 * BLK, lane);
+      mul_(gate, t1);
+      zero(t1);
+      mma<4, 1>(t1, gop, w + 16 * BLK, lane);
+      mul_(gate, t1);
     }
-    add_(e1, o);
-    if (valid) store_row(e1, reinterpret_cast<T*>(a.f_out) + (int64_t)e * HID, g);
-    w = st.next();  // next layer's silu(nbr_linear(.))
-    Act<8> fn;
-    init_vec_lds(fn, pipe.v(), g);
-    linear<DT, 8, 4>(fn, e1, w, lane);
-    silu_<8, FAST>(fn);
-    if (valid) store_row(fn, reinterpret_cast<T*>(a.fn_out) + (int64_t)e * HID, g);
+    Act<4> s;
+    zero(s);
+    RawRow<T> xn = in.xn;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      Act<8> x;
+      xn.to_act(x);
+      if (j < 3) {  // prefetch the next neighbour row under this one's MFMAs
+        const int nx = j == 0 ? nb.y : (j == 1 ? nb.z : nb.w);
+        xn.load(fn_in + (int64_t)nx * HID, g);
+      }
+      // dist_linear_1(dist_linear_0(dist)), recomputed per neighbour (8 MFMAs) rather than held
+      // live across the loop: the memory clobber stops the compiler from hoisting it (32 VGPRs)
+      asm volatile("" ::: "memory");
+      Act<8> dg;
+      zero(dg);
+      mma<8, 1>(dg, gop, w, lane);
+#pragma unroll
+      for (int b = 0; b < 8; ++b)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) x.v[b][q] *= dg.v[b][q];  // gathered rows are silu(nbr_linear(F))
+      Act<4> y;
+      zero(y);
+      linear<DT, 4, 4>(y, x, w + 20 * BLK, lane);  // downward_proj
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) s.v[b][q] += silu<FAST>(y.v[b][q]) * gate.v[b][q];
+      if (j == 1) pipe.mid();
+    }
+    Act<8> x;
+    w = st.next();  // stage 1: upward_proj (+ orig_msg_linear bias)
+    zero(x);
+    linear<DT, 8, 2>(x, s, w, lane);
+    pipe.mid();
+    silu_<8, FAST>(x);
+    {
+      Act<8> bo;
+      init_vec_lds(bo, pipe.v(), g);
+      add_(x, bo);
+    }
+    w = st.next();  // stage 2: orig_msg_linear(res) + nbr
+    mma<8, 4>(x, fr.operand(f_row, g), w, lane);
+    pipe.mid();
+    res_block<DT, FINAL>(x, st, lane, g);
+    res_block<DT, FINAL>(x, st, lane, g);
+    {
+      w = st.next();  // res_connect_linear
+      Act<8> y;
+      init_vec_lds(y, pipe.v(), g);
+      linear<DT, 8, 4>(y, x, w, lane);
+      pipe.mid();
+      silu_<8, FAST>(y);
+      fr.act(x, f_row, g);
+      add_(x, y);
+    }
+    res_block<DT, FINAL>(x, st, lane, g);
+    res_block<DT, FINAL>(x, st, lane, g);
+    {
+      w = st.next();  // final geometric gate
+      if (FINAL && more) in.load_ids(a, en);
+      Act<8> fg;
+      zero(fg);
+      mma<8, 1>(fg, gop, w, lane);
+      mul_(x, fg);
+      pipe.mid();
+      w = st.next();  // final_linear
+      Act<8> y;
+      init_vec_lds(y, pipe.v(), g);
+      linear<DT, 8, 4>(y, x, w, lane);
+      pipe.mid();
+      silu_<8, FAST>(y);
+      fr.act(x, f_row, g);
+      add_(x, y);  // conformation output
+    }
+    // ---- attention scores (propagate_attention :76-91)
+    const int sn = a.src[e], dn = a.dst[e];
+    RawRow<T> kr, qr;  // K[src], Q[dst] in flight under the projection's MFMAs
+    kr.load(qkv + (int64_t)sn * 3 * HID + HID, g);
+    qr.load(qkv + (int64_t)dn * 3 * HID, g);
+    w = st.next();  // edge_feats_projection(BN1e(conf))
+    if (FINAL && more) in.load_rest(a, en, g);  // F of this tile is dead from here on
+    if (!FINAL && more) in.load_ids(a, en);
+    Act<8> p;
+    init_vec_lds(p, pipe.v(), g);
+    linear<DT, 8, 4>(p, x, w, lane);
+    pipe.mid();
+    {
+      Act<8> kq, qd;
+      kr.to_act(kq);
+      qr.to_act(qd);
+      const float scale = 5.656854249492381f;  // np.sqrt(32)
+#pragma unroll
+      for (int b = 0; b < 8; ++b)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          float sc = FAST ? (kq.v[b][q] * qd.v[b][q]) * (1.0f / scale) : (kq.v[b][q] * qd.v[b][q]) / scale;
+          sc = fminf(fmaxf(sc, -5.f), 5.f);
+          p.v[b][q] = sc * p.v[b][q];  // score = e_out
+        }
+    }
+    floatx4 al;
+#pragma unroll
+    for (int h = 0; h < 4; ++h) al[h] = expf_<FAST>(fminf(fmaxf(head_sum(p, h), -5.f), 5.f));
+    if (valid && g == 0) st4(a.alpha_out + (int64_t)e * 4, al);
+
+    if constexpr (!FINAL) {
+      // ---- edge output: e = in + O_e(e_out); e = e + FFN(BN2e(e)) (:697-724)
+      w = st.next();  // O_edge_feats
+      Act<8> e1;
+      init_vec_lds(e1, pipe.v(), g);
+      linear<DT, 8, 4>(e1, p, w, lane);
+      pipe.mid();
+      {
+        Act<8> fa;
+        fr.act(fa, f_row, g);
+        add_(e1, fa);
+      }
+      Act<8> o;
+      zero(o);
+#pragma unroll 1
+      for (int half = 0; half < 2; ++half) {
+        w = st.next();  // edge_feats_MLP.0 (BN2e folded), hidden half
+        if (half == 0 && more) in.load_rest(a, en, g);  // F of this tile is dead from here on
+        Act<8> t;
+        init_vec_lds(t, pipe.v(), g);
+        linear<DT, 8, 4>(t, e1, w, lane);
+        pipe.mid();
+        silu_<8, FAST>(t);
+        w = st.next();  // edge_feats_MLP.3, input half
+        linear<DT, 8, 4>(o, t, w, lane);
+        pipe.mid();
+      }
+      add_(e1, o);
+      if (valid) store_row(e1, reinterpret_cast<T*>(a.f_out) + (int64_t)e * HID, g);
+      w = st.next();  // next layer's silu(nbr_linear(.))
+      Act<8> fn;
+      init_vec_lds(fn, pipe.v(), g);
+      linear<DT, 8, 4>(fn, e1, w, lane);
+      pipe.mid();
+      silu_<8, FAST>(fn);
+      if (valid) store_row(fn, reinterpret_cast<T*>(a.fn_out) + (int64_t)e * HID, g);
+    }
   }
+  if (G::PP && !(threadIdx.x >> 8)) pipe.mid();  // matches group 1's leading mid()
 }
 
 // ================================================================ fused node layer
@@ -579,6 +671,16 @@ using namespace di;
 
 static inline int grid_rows(int n, int rows = ROWS_PER_BLOCK) { return (n + rows - 1) / rows; }
 
+static inline int num_cus() {
+  static const int n = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0)
+      v = 256;
+    return v;
+  }();
+  return n;
+}
+
 static inline int launch_status() {
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? DI_OK : (int)e;
@@ -641,7 +743,13 @@ extern "C" int di_edge_layer(const di_graph* g, di_dtype dt, int final_layer, co
              f_out, fn_out};
   hipStream_t s = (hipStream_t)stream;
   if (dt == DI_BF16) {
-    dim3 grid(grid_rows(a.Et, Geo<BF16T>::ROWS)), block(Geo<BF16T>::THREADS);
+    // persistent: two resident blocks per CU
+#ifndef DI_EDGE_PERSIST
+#define DI_EDGE_PERSIST 0
+#endif
+    const int tiles = grid_rows(a.Et, EdgeGeo<BF16T>::ROWS);
+    const int resident = DI_EDGE_PERSIST ? (EdgeGeo<BF16T>::PP ? 1 : 2) * num_cus() : tiles;
+    dim3 grid(tiles < resident ? tiles : resident), block(EdgeGeo<BF16T>::THREADS);
     if (final_layer) hipLaunchKernelGGL((k_edge_layer<BF16T, true>), grid, block, 0, s, a);
     else hipLaunchKernelGGL((k_edge_layer<BF16T, false>), grid, block, 0, s, a);
   } else {

@@ -22,6 +22,13 @@ VARIANTS = {
     "nodma_nobar_nosilu": ["DI_X_NODMA", "DI_X_NOBAR", "DI_X_NOSILU"],
     "strip_noldsa": ["DI_X_NODMA", "DI_X_NOBAR", "DI_X_NOSILU", "DI_X_NOLDSA"],
     "noldsa": ["DI_X_NOLDSA"],
+    "nopersist": ["DI_EDGE_PERSIST=0"],
+    "nopp": ["DI_EDGE_PP=0"],
+    "pp_persist": ["DI_EDGE_PERSIST=1"],
+    "pp_prio": ["DI_X_PRIO=1"],
+    "pp_nomid": ["DI_X_NOMID"],
+    "stagger40": ["DI_X_STAGGER=40"],
+    "stagger120": ["DI_X_STAGGER=120"],
     "nw8": ["DI_GEO_NW=8"],
     "nw8_order3": ["DI_GEO_NW=8", "DI_MMA_ORDER=3"],
 }
