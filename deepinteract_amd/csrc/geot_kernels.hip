@@ -273,7 +273,7 @@ __constant__ int EL_VEC[25] = {-1, ELV_OM, -1,
                                ELV_RES + 9 * 128, ELV_RES + 10 * 128, ELV_RES + 11 * 128,
                                -1, ELV_F, ELV_P,
                                ELV_OE, ELV_F1, -1, ELV_F1 + 128, -1, ELV_NN};
-constexpr int EL_NSTAGE_FINAL = 19, EL_NSTAGE = 25;
+constexpr int EL_NSTAGE_CONF = 18, EL_NSTAGE_FINAL = 19, EL_NSTAGE = 25;
 constexpr int EL_CAP = 36;
 
 // bf16: 8-wave ping-pong blocks (RingPipe, one block per CU, 128 rows per weight pass);
@@ -296,7 +296,8 @@ constexpr int edge_lds_bytes() {
   return (EdgeGeo<DT>::PP ? 3 : (Geo<DT>::DBUF ? 2 : 1)) * EdgePipe<DT>::SLOT_BYTES;
 }
 
-template <class DT, bool FINAL>
+// MODE: 0 intermediate layer, 1 final layer, 2 conformation module alone (di_conformation)
+template <class DT, int MODE>
 struct EdgeStages {
   using T = typename DT::T;
   EdgePipe<DT>& pipe;
@@ -307,7 +308,7 @@ struct EdgeStages {
   // wait for stage i (already issued), start stage i+1; pipe.w()/pipe.v() = stage i
   __device__ const T* next() {
     const T* w = pipe.next();
-    const int n = FINAL ? EL_NSTAGE_FINAL : EL_NSTAGE;
+    const int n = MODE == 2 ? EL_NSTAGE_CONF : (MODE == 1 ? EL_NSTAGE_FINAL : EL_NSTAGE);
     const int ni = i + 1 < n ? i + 1 : (more ? 0 : -1);
     if (ni >= 0) {
       const int vo = EL_VEC[ni];
@@ -318,8 +319,8 @@ struct EdgeStages {
   }
 };
 
-template <class DT, bool FINAL>
-__device__ __forceinline__ void res_block(Act<8>& x, EdgeStages<DT, FINAL>& st, int lane, int g) {
+template <class DT, int MODE>
+__device__ __forceinline__ void res_block(Act<8>& x, EdgeStages<DT, MODE>& st, int lane, int g) {
   constexpr bool FAST = DT::kBF16;
   Act<8> y = x;
 #pragma unroll 1
@@ -368,9 +369,10 @@ __device__ __forceinline__ int tile_edge(int tile, int Et, bool& valid) {
 // Persistent: each block walks tiles blockIdx.x, +gridDim.x, ...; the weight-stage stream runs on
 // across tiles (the last stage's DMA slot fetches stage 0 of the next tile) and the next tile's
 // inputs are prefetched under the current tile's last stages, so no tile pays a cold prologue.
-template <class DT, bool FINAL>
+template <class DT, int MODE>
 __global__ __attribute__((amdgpu_flat_work_group_size(1, 512), amdgpu_waves_per_eu(2, 2), amdgpu_num_vgpr(120)))
 void k_edge_layer(EdgeArgs a) {
+  constexpr bool FINAL = MODE == 1, CONF = MODE == 2;
   using T = typename DT::T;
   using G = EdgeGeo<DT>;
   constexpr bool FAST = DT::kBF16;
@@ -382,7 +384,7 @@ void k_edge_layer(EdgeArgs a) {
   const T* qkv = reinterpret_cast<const T*>(a.qkv);
 
   EdgePipe<DT> pipe(lds);
-  EdgeStages<DT, FINAL> st{pipe, W, a.wvec, 0, false};
+  EdgeStages<DT, MODE> st{pipe, W, a.wvec, 0, false};
   pipe.issue(W + EL_S0 * BLK, EL_SIZE[0]);
 #ifdef DI_X_STAGGER
   if (blockIdx.x & 1) __builtin_amdgcn_s_sleep(DI_X_STAGGER);
@@ -474,8 +476,8 @@ void k_edge_layer(EdgeArgs a) {
     w = st.next();  // stage 2: orig_msg_linear(res) + nbr
     mma<8, 4>(x, fr.operand(f_row, g), w, lane);
     pipe.mid();
-    res_block<DT, FINAL>(x, st, lane, g);
-    res_block<DT, FINAL>(x, st, lane, g);
+    res_block<DT, MODE>(x, st, lane, g);
+    res_block<DT, MODE>(x, st, lane, g);
     {
       w = st.next();  // res_connect_linear
       Act<8> y;
@@ -486,11 +488,11 @@ void k_edge_layer(EdgeArgs a) {
       fr.act(x, f_row, g);
       add_(x, y);
     }
-    res_block<DT, FINAL>(x, st, lane, g);
-    res_block<DT, FINAL>(x, st, lane, g);
+    res_block<DT, MODE>(x, st, lane, g);
+    res_block<DT, MODE>(x, st, lane, g);
     {
       w = st.next();  // final geometric gate
-      if (FINAL && more) in.load_ids(a, en);
+      if ((FINAL || CONF) && more) in.load_ids(a, en);
       Act<8> fg;
       zero(fg);
       mma<8, 1>(fg, gop, w, lane);
@@ -504,6 +506,11 @@ void k_edge_layer(EdgeArgs a) {
       silu_<8, FAST>(y);
       fr.act(x, f_row, g);
       add_(x, y);  // conformation output
+    }
+    if constexpr (CONF) {
+      if (more) in.load_rest(a, en, g);
+      if (valid) store_row(x, reinterpret_cast<T*>(a.f_out) + (int64_t)e * HID, g);
+      continue;
     }
     // ---- attention scores (propagate_attention :76-91)
     const int sn = a.src[e], dn = a.dst[e];
@@ -698,6 +705,7 @@ extern "C" int64_t di_blob_bytes(int kind, di_dtype dtype, int vec) {
     case 3: blk = EL_NBLK_FINAL; nvec = ELV_N_FINAL; break;
     case 4: blk = NL_NBLK; nvec = NLV_N; break;
     case 5: blk = NL_NBLK_FINAL; nvec = NLV_N_FINAL; break;
+    case 6: blk = EL_NBLK_CONF; nvec = ELV_N_CONF; break;
     default: return -1;
   }
   return vec ? nvec * 4 : blk * BLK * esz;
@@ -750,12 +758,29 @@ extern "C" int di_edge_layer(const di_graph* g, di_dtype dt, int final_layer, co
     const int tiles = grid_rows(a.Et, EdgeGeo<BF16T>::ROWS);
     const int resident = DI_EDGE_PERSIST ? (EdgeGeo<BF16T>::PP ? 1 : 2) * num_cus() : tiles;
     dim3 grid(tiles < resident ? tiles : resident), block(EdgeGeo<BF16T>::THREADS);
-    if (final_layer) hipLaunchKernelGGL((k_edge_layer<BF16T, true>), grid, block, 0, s, a);
-    else hipLaunchKernelGGL((k_edge_layer<BF16T, false>), grid, block, 0, s, a);
+    if (final_layer) hipLaunchKernelGGL((k_edge_layer<BF16T, 1>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((k_edge_layer<BF16T, 0>), grid, block, 0, s, a);
   } else {
     dim3 grid(grid_rows(a.Et, Geo<F32T>::ROWS)), block(Geo<F32T>::THREADS);
-    if (final_layer) hipLaunchKernelGGL((k_edge_layer<F32T, true>), grid, block, 0, s, a);
-    else hipLaunchKernelGGL((k_edge_layer<F32T, false>), grid, block, 0, s, a);
+    if (final_layer) hipLaunchKernelGGL((k_edge_layer<F32T, 1>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((k_edge_layer<F32T, 0>), grid, block, 0, s, a);
+  }
+  return launch_status();
+}
+
+extern "C" int di_conformation(const di_graph* g, di_dtype dt, const float* edge_f, const void* f_in,
+                               const void* fn_in, const void* wmat, const float* wvec, void* conf_out,
+                               void* stream) {
+  if (!g || !edge_f || !f_in || !fn_in || !wmat || !wvec || !conf_out || g->num_edges <= 0) return DI_EINVAL;
+  EdgeArgs a{g->num_edges, edge_f, g->src, g->dst, g->nbr, f_in, fn_in, nullptr, wmat, wvec, nullptr,
+             conf_out, nullptr};
+  hipStream_t s = (hipStream_t)stream;
+  if (dt == DI_BF16) {
+    dim3 grid(grid_rows(a.Et, EdgeGeo<BF16T>::ROWS)), block(EdgeGeo<BF16T>::THREADS);
+    hipLaunchKernelGGL((k_edge_layer<BF16T, 2>), grid, block, 0, s, a);
+  } else {
+    dim3 grid(grid_rows(a.Et, EdgeGeo<F32T>::ROWS)), block(EdgeGeo<F32T>::THREADS);
+    hipLaunchKernelGGL((k_edge_layer<F32T, 2>), grid, block, 0, s, a);
   }
   return launch_status();
 }

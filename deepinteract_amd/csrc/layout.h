@@ -34,6 +34,7 @@ constexpr int EL_F = 500;     // final_linear [8x4]
 constexpr int EL_FG = 532;    // final gate (sum of the 4 final_* geometric linears) [8x1]
 constexpr int EL_P = 540;     // edge_feats_projection . BN1e
 constexpr int EL_NBLK_FINAL = 572;
+constexpr int EL_NBLK_CONF = 540;  // kind 6: conformation module alone (stages S0 .. final_linear)
 constexpr int EL_OE = 572;
 constexpr int EL_F1 = 604;    // 2 x [8x4] (hidden halves)
 constexpr int EL_F2 = 668;    // 2 x [8x4] (input halves)
@@ -41,6 +42,7 @@ constexpr int EL_NN = 732;    // next layer's nbr_linear
 constexpr int EL_NBLK = 764;
 constexpr int ELV_OM = 0, ELV_RES = 128, ELV_RC = 1664, ELV_F = 1792, ELV_P = 1920;
 constexpr int ELV_N_FINAL = 2048;
+constexpr int ELV_N_CONF = 1920;
 constexpr int ELV_OE = 2048, ELV_F1 = 2176, ELV_NN = 2432, ELV_N = 2560;
 
 // ---- kind 4/5: node layer (aggregation + O_node + FFN [+ next Q/K/V]) ----------------------

@@ -22,8 +22,10 @@ EL_NBLK, ELV_N = 764, 2560
 EL_NBLK_FINAL, ELV_N_FINAL = 572, 2048
 NL_NBLK, NLV_N = 256, 768
 NL_NBLK_FINAL, NLV_N_FINAL = 160, 384
+EL_NBLK_CONF, ELV_N_CONF = 540, 1920
 BLOB_SIZES = {0: (EM_NBLK, EMV_N), 1: (IE_NBLK, IEV_N), 2: (EL_NBLK, ELV_N),
-              3: (EL_NBLK_FINAL, ELV_N_FINAL), 4: (NL_NBLK, NLV_N), 5: (NL_NBLK_FINAL, NLV_N_FINAL)}
+              3: (EL_NBLK_FINAL, ELV_N_FINAL), 4: (NL_NBLK, NLV_N), 5: (NL_NBLK_FINAL, NLV_N_FINAL),
+              6: (EL_NBLK_CONF, ELV_N_CONF)}
 
 
 def _np(t):
@@ -62,6 +64,37 @@ def pack_matrix(w, dtype: str) -> np.ndarray:
         for s in range(ns):
             blocks[bo, s] = w[16 * bo + r, 32 * s + c]
     return blocks.reshape(-1)
+
+
+def _pack_index_natural(dtype: str):
+    """Natural-k fragment order of di_gemm_bias_act (the B operand is read straight from x)."""
+    lane = np.arange(64)
+    if dtype == "bf16":
+        j = np.arange(8)
+        row = np.broadcast_to((lane & 15)[:, None], (64, 8))
+        col = 8 * (lane[:, None] >> 4) + j[None, :]
+        return row.reshape(-1), col.reshape(-1)
+    sub = np.arange(8)
+    row = np.broadcast_to((lane & 15)[None, :], (8, 64))
+    col = 4 * sub[:, None] + (lane[None, :] >> 4)
+    return row.reshape(-1), col.reshape(-1)
+
+
+def pack_matrix_natural(w, dtype: str) -> torch.Tensor:
+    """W [Nout, Kin] (Nout % 16 == 0; Kin zero-padded to a multiple of 32) -> packed blocks in
+    the storage dtype, block order (bo, s), for di_gemm_bias_act."""
+    w = np.asarray(w, dtype=np.float64)
+    nout, kin = w.shape
+    assert nout % 16 == 0, nout
+    w = pad2(w, nout, -(-kin // 32) * 32)
+    r, c = _pack_index_natural(dtype)
+    nbo, ns = nout // 16, w.shape[1] // 32
+    blocks = np.empty((nbo, ns, BLK), dtype=np.float64)
+    for bo in range(nbo):
+        for s in range(ns):
+            blocks[bo, s] = w[16 * bo + r, 32 * s + c]
+    t = torch.from_numpy(blocks.reshape(-1)).to(torch.float32)
+    return t.to(torch.bfloat16) if dtype == "bf16" else t
 
 
 def bn_affine(sd, name):
@@ -147,8 +180,10 @@ def _geo_rows(w, kind):
     return full
 
 
-def init_blob(sd, dtype):
-    p = "gnn_module.0.init_edge_module"
+def init_blob(sd, dtype, p="gnn_module.0.init_edge_module",
+              nbr="gnn_module.0.gt_block.0.conformation_module.nbr_linear"):
+    """nbr=None: no following layer (standalone InitEdgeModule): the fused silu(nbr_linear)
+    output is computed with zero weights and ignored."""
     bb = BlobBuilder(dtype, IE_NBLK, IEV_N)
     wc0 = _np(sd[f"{p}.combined_linear_0.weight"])  # [128, 896]
     for t, kind in enumerate(GEO_ORDER):
@@ -157,7 +192,7 @@ def init_blob(sd, dtype):
         bb.put(200 + 8 * t, _geo_rows(_np(sd[f"{p}.{kind}_linear_1.weight"]), kind))
     bb.put(240, pad2(_np(sd[f"{p}.combined_linear_1.weight"]), 32, 128))
     bb.put(248, pad2(_np(sd[f"{p}.combined_linear_2.weight"]), 128, 32))
-    w, b = lin(sd, "gnn_module.0.gt_block.0.conformation_module.nbr_linear")
+    w, b = lin(sd, nbr) if nbr else (np.zeros((128, 128)), np.zeros(128))
     bb.put(256, w)
     bb.putv(0, b)
     mat, vec = bb.finish()
@@ -167,10 +202,14 @@ def init_blob(sd, dtype):
     return mat, vec, pos_src, pos_dst
 
 
-def edge_blob(sd, li, final, dtype, cfg: GeoTConfig):
+def edge_blob(sd, li, final, dtype, cfg: GeoTConfig, conf_only=False, c=None):
+    """final: kind 3, else kind 2; conf_only: kind 6 (ConformationModule alone, key prefix c)."""
     p = f"gnn_module.0.gt_block.{li}"
-    c = f"{p}.conformation_module"
-    bb = BlobBuilder(dtype, EL_NBLK_FINAL if final else EL_NBLK, ELV_N_FINAL if final else ELV_N)
+    c = c or f"{p}.conformation_module"
+    if conf_only:
+        bb = BlobBuilder(dtype, EL_NBLK_CONF, ELV_N_CONF)
+    else:
+        bb = BlobBuilder(dtype, EL_NBLK_FINAL if final else EL_NBLK, ELV_N_FINAL if final else ELV_N)
     two = lambda a, b: _np(sd[f"{c}.{a}.weight"]) @ _np(sd[f"{c}.{b}.weight"])  # noqa: E731
     mg = np.zeros((320, 32))
     mg[0:128] = _geo_rows(two("dist_linear_1", "dist_linear_0"), "dist")
@@ -205,6 +244,8 @@ def edge_blob(sd, li, final, dtype, cfg: GeoTConfig):
     bb.put(500, w)
     bb.putv(1792, b)
     bb.put(532, fg)
+    if conf_only:
+        return bb.finish()
     s, t = bn_affine(sd, f"{p}.batch_norm1_edge_feats")
     w, b = fold_bn_before(*lin(sd, f"{p}.mha_module.edge_feats_projection"), s, t)
     bb.put(540, w)

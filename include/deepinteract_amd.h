@@ -21,6 +21,13 @@
  *                                                                    protein_feature_utils.py:322-377,
  *                                                                    deepinteract_utils.py:474-530
  *   di_build_nbr_ids  per-edge neighbour-edge ids                    deepinteract_utils.py:534-553
+ *
+ * Module-at-a-time entry points (deepinteract_amd/layers.py; same math as the fused kernels):
+ *   di_conformation   ConformationModule.forward                      deepinteract_modules.py:373-455
+ *   di_gemm_bias_act  nn.Linear (+ folded BatchNorm, + SiLU, + residual) of the GeoT modules
+ *                                                                    deepinteract_modules.py:99-104, 696-723
+ *   di_geo_attention  MultiHeadGeometricAttentionLayer.propagate_attention + h = wV/(z+1e-6)
+ *                                                                    deepinteract_modules.py:76-121
  */
 #ifndef DEEPINTERACT_AMD_H
 #define DEEPINTERACT_AMD_H
@@ -121,6 +128,24 @@ int di_geo_feats(const di_geo_args* args, void* stream);
  * (seed, e); nbr_out [Et,4] global edge ids in the di_graph.nbr layout. */
 int di_build_nbr_ids(int32_t num_edges, const int32_t* src, const int32_t* dst, const int32_t* in_ptr,
                      uint64_t seed, int32_t* nbr_out, void* stream);
+
+/* ---- module-at-a-time API ---------------------------------------------------------------- */
+/* ConformationModule alone (kind-6 blob): conf_out [Et,128] = F + SiLU(final_linear(...)), from the
+ * current edge features f_in [Et,128] and fn_in = SiLU(nbr_linear(f_in)) [Et,128]. */
+int di_conformation(const di_graph* g, di_dtype dt, const float* edge_f /*[Et,28]*/, const void* f_in,
+                    const void* fn_in, const void* wmat, const float* wvec, void* conf_out, void* stream);
+
+/* y[r,:] = res[r,:] + act(W x[r,:] + bias) for r < rows; W packed in the natural-k fragment order
+ * (packing.pack_matrix_natural: out_dim % 16 == 0, in_dim padded to 32). act: 0 none, 1 SiLU.
+ * bias / res may be NULL. x, res, y in the storage dtype; bias fp32. */
+int di_gemm_bias_act(di_dtype dt, int32_t rows, int32_t in_dim, int32_t out_dim, const void* x, int32_t x_ld,
+                     const void* w_packed, const float* bias, int32_t act, const void* res, int32_t res_ld,
+                     void* y, int32_t y_ld, void* stream);
+
+/* qkv [Nt,384] = Q|K|V, proj_e [Et,128]: e_out [Et,128] (NULL: not produced), alpha_out [Et,4]
+ * (fp32, exp(clamp(sum score))), h_out [Nt,128] = sum alpha V[src] / (sum alpha + 1e-6). */
+int di_geo_attention(const di_graph* g, di_dtype dt, const void* qkv, const void* proj_e, void* e_out,
+                     float* alpha_out, void* h_out, void* stream);
 
 #ifdef __cplusplus
 }

@@ -95,3 +95,45 @@ def test_blob_sizes_match_layout():
     assert p.pos_src.shape == (2304, 128)
     pb = packing.PackedGeoT(sd, "bf16")
     assert pb.edge[0][0].dtype == torch.bfloat16
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "f32"])
+@pytest.mark.parametrize("nout,kin", [(48, 113), (16, 32), (384, 128)])
+def test_natural_packing_matches_dense(dtype, nout, kin):
+    """di_gemm_bias_act (csrc/modules.hip): B operand read straight from x in natural k order,
+    k zero-padded to 32; emulate the ISA lane maps over the packed blocks."""
+    rng = np.random.default_rng(1)
+    W = rng.integers(-4, 5, size=(nout, kin)).astype(np.float64)
+    x = rng.integers(-4, 5, size=(16, kin)).astype(np.float64)
+    packed = packing.pack_matrix_natural(W, dtype).float().numpy().astype(np.float64)
+    ks = -(-kin // 32)
+    xp = np.zeros((16, 32 * ks))
+    xp[:, :kin] = x
+    out = np.zeros((16, nout))
+    for s in range(ks):
+        for bo in range(nout // 16):
+            blk = packed[(bo * ks + s) * 512:(bo * ks + s + 1) * 512]
+            A = np.zeros((16, 32))
+            if dtype == "bf16":
+                b = blk.reshape(64, 8)
+                for lane in range(64):
+                    for j in range(8):
+                        A[lane & 15, 8 * (lane >> 4) + j] = b[lane, j]
+            else:
+                b = blk.reshape(8, 64)
+                for sub in range(8):
+                    for lane in range(64):
+                        A[lane & 15, 4 * sub + (lane >> 4)] = b[sub, lane]
+            out[:, 16 * bo:16 * bo + 16] += (A @ xp[:, 32 * s:32 * s + 32].T).T
+    np.testing.assert_array_equal(out, x @ W.T)
+
+
+def test_conformation_blob_is_edge_blob_prefix():
+    from deepinteract_amd.weights import seeded_state_dict
+    from deepinteract_amd.config import GeoTConfig
+    sd = seeded_state_dict(0, with_head=False)
+    full_m, full_v = packing.edge_blob(sd, 0, False, "f32", GeoTConfig())
+    conf_m, conf_v = packing.edge_blob(sd, 0, False, "f32", GeoTConfig(), conf_only=True)
+    nblk, nvec = packing.BLOB_SIZES[6]
+    assert conf_m.numel() == nblk * 512 and conf_v.numel() == nvec
+    assert torch.equal(conf_m, full_m[:nblk * 512]) and torch.equal(conf_v, full_v[:nvec])
