@@ -144,7 +144,9 @@ def main():
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
     ap.add_argument("--cpu-sample", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--overlap", type=int, default=1, help="pair tensor on its own stream, overlapped with GeoT")
+    ap.add_argument("--overlap", type=int, default=1, choices=[0, 1, 2],
+                    help="0: one stream; 1: pair tensor of micro-batch m-1 on its own stream beside GeoT of m; "
+                         "2: as 1, started after InitEdge of m")
     args = ap.parse_args()
 
     ws, rank, local = dist_setup()
@@ -192,24 +194,41 @@ def main():
     s_pair = torch.cuda.Stream(dev) if args.overlap else s_geot
     done = [None, None]  # per workspace slot: event after the pair tensor that last read it
 
+    def launch_pair(h, hT, ready, slot, after=None, events=None):
+        with torch.cuda.stream(s_pair):
+            s_pair.wait_event(ready)
+            if after is not None:
+                s_pair.wait_event(after)
+            pair(h, h1r, h2r, l1, l2, out=pair_buf, events=events, hT=hT)
+            ev = torch.cuda.Event()
+            ev.record(s_pair)
+            done[slot] = ev
+
     def step(events=None):
         # GeoT of micro-batch m (compute-bound, stream A) overlaps the pair-tensor stores of
         # micro-batch m-1 (HBM-bound, stream B); two workspace slots carry the node features.
+        # overlap 2: the pair tensor of m-1 starts once InitEdge of m has been issued, so the
+        # store stream runs beside the edge layers (MFMA/VALU-bound), not beside the
+        # memory-heavy node-embedding / InitEdge prologue.
+        prev = None
         for m, gb in enumerate(mbs):
             slot = m & 1 if args.overlap else 0
+            after = torch.cuda.Event() if args.overlap == 2 else None
             with torch.cuda.stream(s_geot):
                 if done[slot] is not None:
                     s_geot.wait_event(done[slot])
-                h, _ = eng.forward(gb, clone=False, events=events, slot=slot)
+                h, _ = eng.forward(gb, clone=False, events=events, slot=slot, after_init=after)
                 hT = eng.last_hT
                 ready = torch.cuda.Event()
                 ready.record(s_geot)
-            with torch.cuda.stream(s_pair):
-                s_pair.wait_event(ready)
-                pair(h, h1r, h2r, l1, l2, out=pair_buf, events=events, hT=hT)
-                ev = torch.cuda.Event()
-                ev.record(s_pair)
-                done[slot] = ev
+            if args.overlap == 2:
+                if prev is not None:
+                    launch_pair(*prev, after=after, events=events)
+                prev = (h, hT, ready, slot)
+            else:
+                launch_pair(h, hT, ready, slot, events=events)
+        if prev is not None:
+            launch_pair(*prev, events=events)
 
     for _ in range(args.warmup):
         step()
@@ -262,7 +281,8 @@ def main():
                                f"GeoT fwd (both chains) + [256,{n_res},{n_res}] pair tensor",
                    "complexes_per_gpu_per_step": args.complexes, "micro_batch": M, "residues": [n_res, n_res],
                    "knn": k, "parallelism": f"complex-sharded dp{ws}",
-                   "streams": "GeoT || pair-tensor (2 HIP streams)" if args.overlap else "1 stream"},
+                   "streams": ["1 stream", "GeoT || pair-tensor (2 HIP streams)",
+                               "GeoT || pair-tensor (2 HIP streams, pair after InitEdge)"][args.overlap]},
         "hbm_frac_of_peak": round(hbm_frac, 4),
         "roofline": roof,
         "kernels": {n: {kk: round(v, 3) if isinstance(v, float) else v for kk, v in r.items()} for n, r in kern.items()},

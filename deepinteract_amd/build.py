@@ -39,7 +39,8 @@ def up_to_date() -> bool:
 
 
 def build(force: bool = False, verbose: bool = True, defines=(), out: str | None = None) -> str:
-    """Build the library. ``defines``/``out`` build a tuning variant (extra -D flags) into its
+    """Build the library. ``defines``/``out`` build a tuning variant (extra -D defines, or raw
+    compiler flags when an entry starts with '-') into its
     own directory, loaded with DI_LIB=<path> (kernel experiments compared in one GPU session)."""
     lib_path = out or LIB
     if not force and not defines and out is None and up_to_date():
@@ -50,7 +51,7 @@ def build(force: bool = False, verbose: bool = True, defines=(), out: str | None
 
     def compile_one(src):
         obj = os.path.join(objdir, os.path.basename(src).replace(".hip", ".o"))
-        cmd = [HIPCC, *CFLAGS, *[f"-D{d}" for d in defines], "-c", src, "-o", obj]
+        cmd = [HIPCC, *CFLAGS, *[d if d.startswith("-") else f"-D{d}" for d in defines], "-c", src, "-o", obj]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr}")

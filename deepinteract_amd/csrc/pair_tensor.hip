@@ -23,6 +23,13 @@ constexpr int PAIR_THREADS = 256;
 constexpr int PAIR_CHUNK = 65536;  // elements per work item
 constexpr int PAIR_MAX_BLOCKS = 256;  // one 4-wave block per CU: leaves the GeoT kernels their issue slots
 constexpr int PAIR_UNROLL = 4;
+// Store cache policy of the row kernel's 16-B stores (gfx950 CPol bits: 2 = nt, 16 = sc1).
+// Measured on the C3 pair tensor (4.1 GB per launch, alone): plain 681 us (6.0 TB/s), nt 875 us;
+// sc1 / sc1+nt slowed the per-vector kernel by 15 % without speeding up the concurrent GeoT.
+// The per-vector (legacy aligned) kernel keeps non-temporal stores.
+#ifndef DI_PAIR_STORE
+#define DI_PAIR_STORE 0
+#endif
 
 template <typename T>
 struct Vec16;
@@ -74,6 +81,9 @@ __global__ __launch_bounds__(PAIR_THREADS) void k_pair_tensor(const di_pair_desc
     const T* h2t = hT ? hT + (int64_t)(c - hidden) * nrows + d.h2_row : nullptr;  // row c-H of hT
     const T* h2c = h + d.h2_row * hidden + (c - hidden);                           // strided fallback
     if (ALIGNED) {
+#if !(DI_PAIR_STORE == 0 || DI_PAIR_STORE == 2)
+      const __amdgpu_buffer_rsrc_t orsrc = buf_rsrc(o);  // plane base: q * sizeof(T) < 2^31
+#endif
       // PAIR_UNROLL independent 16-B vectors per thread per trip: the hT loads (L2 hits) of a
       // trip are all in flight before its stores
       constexpr uint32_t STEP = PAIR_THREADS * VEC;
@@ -99,7 +109,14 @@ __global__ __launch_bounds__(PAIR_THREADS) void k_pair_tensor(const di_pair_desc
 #pragma unroll
         for (int u = 0; u < PAIR_UNROLL; ++u) {
           const uint32_t q = q0 + u * STEP;
-          if (q < q_end) __builtin_nontemporal_store(vals[u], reinterpret_cast<V*>(o + q));
+          if (q < q_end) {
+#if DI_PAIR_STORE == 0 || DI_PAIR_STORE == 2
+            __builtin_nontemporal_store(vals[u], reinterpret_cast<V*>(o + q));
+#else
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uintx4, vals[u]), orsrc, (int)(q * sizeof(T)), 0,
+                                                   DI_PAIR_STORE);
+#endif
+          }
         }
       }
     } else {
@@ -107,6 +124,78 @@ __global__ __launch_bounds__(PAIR_THREADS) void k_pair_tensor(const di_pair_desc
         uint32_t i, j;
         plane_rc(q, l2, inv_l2, i, j);
         o[q] = second ? (h2t ? h2t[j] : h2c[j * hidden]) : h1c[i * hidden];
+      }
+    }
+  }
+}
+
+// Row-streaming form of the aligned path (every plane offset, L2 and chain-2 row 16-B aligned).
+// A channel plane is L1 identical-shape rows of L2 elements: chain-2 rows are all the same vector
+// hT[c - H, 0:L2], chain-1 row i is the constant h1[i, c]. A work item is (complex, channel,
+// PAIR_ROWS rows); a wave owns a contiguous run of 64 of them (a cache line split between rows
+// i and i+1 is completed by the same wave back to back). Per 128-chunk segment of the row it loads
+// what its rows need ONCE (two 16-B row-vector pieces per lane, or one chain-1 value per row, one
+// per lane, broadcast with readlane), then issues only stores: buffer_store_dwordx4 with a
+// per-lane constant voffset and the row offset in an SGPR, so a 2-KB row costs two store
+// instructions plus scalar address arithmetic, and no load sits between stores.
+// <= 32 VGPRs: one wave per SIMD co-resides with the edge kernels (2 x 240 VGPRs).
+#ifndef DI_PAIR_ROW_WAVES
+#define DI_PAIR_ROW_WAVES 4
+#endif
+constexpr int PAIR_ROW_THREADS = 64 * DI_PAIR_ROW_WAVES;
+constexpr int PAIR_ROWS = 64 * DI_PAIR_ROW_WAVES;  // rows per work item (64 per wave)
+constexpr int PAIR_SEG = 128;                      // 16-B chunks per row segment (2 per lane)
+template <typename T>
+__global__ __launch_bounds__(PAIR_ROW_THREADS) __attribute__((amdgpu_num_vgpr(32)))
+void k_pair_rows(const di_pair_desc* __restrict__ descs, int hidden, const T* __restrict__ h,
+                 const T* __restrict__ hT, int nrows, int rblocks, int items, T* __restrict__ out) {
+  using V = typename Vec16<T>::V;
+  constexpr int VEC = Vec16<T>::N;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  for (int item = blockIdx.x; item < items; item += gridDim.x) {
+    const int rb = item % rblocks;
+    const int rest = item / rblocks;
+    const int c = rest % (2 * hidden);
+    const int cpx = rest / (2 * hidden);
+    const di_pair_desc d = descs[cpx];
+    const int r0 = rb * PAIR_ROWS + 64 * wave;  // this wave's rows [r0, r1)
+    const int r1 = r0 + 64 < d.l1 ? r0 + 64 : d.l1;
+    if (r0 >= r1) continue;  // uniform per wave
+    const int nch = d.l2 / VEC;  // 16-B chunks per row
+    const uint32_t pitch = (uint32_t)d.l2 * sizeof(T);
+    T* o = out + d.out_off + (int64_t)c * ((int64_t)d.l1 * d.l2);
+    const __amdgpu_buffer_rsrc_t r = buf_rsrc(o);
+    const bool second = c >= hidden;
+    uint32_t hv = 0;  // chain 1: lane l holds the value of row r0 + l
+    if (!second && r0 + lane < r1) {
+      if constexpr (sizeof(T) == 2) {
+        hv = h[(d.h1_row + r0 + lane) * hidden + c];
+        hv |= hv << 16;
+      } else {
+        hv = __builtin_bit_cast(uint32_t, h[(d.h1_row + r0 + lane) * hidden + c]);
+      }
+    }
+    const T* src = hT + (int64_t)(c - hidden) * nrows + d.h2_row;
+    for (int seg = 0; seg < nch; seg += PAIR_SEG) {
+      const int k0 = seg + lane, k1 = seg + 64 + lane;  // this lane's chunks of the segment
+      const bool two = seg + 64 < nch;                  // uniform: the segment has a second piece
+      V v0, v1;
+      if (second) {
+        if (k0 < nch) v0 = *reinterpret_cast<const V*>(src + k0 * VEC);
+        if (k1 < nch) v1 = *reinterpret_cast<const V*>(src + k1 * VEC);
+      }
+      for (int i = r0; i < r1; ++i) {
+        const int soff = (int)(i * pitch);
+        if (!second) {
+          const uint32_t b = (uint32_t)__builtin_amdgcn_readlane((int)hv, i - r0);
+          v0 = __builtin_bit_cast(V, (uintx4){b, b, b, b});
+          v1 = v0;
+        }
+        if (k0 < nch)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uintx4, v0), r, k0 * 16, soff, DI_PAIR_STORE);
+        if (two && k1 < nch)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uintx4, v1), r, k1 * 16, soff, DI_PAIR_STORE);
       }
     }
   }
@@ -136,6 +225,24 @@ extern "C" int di_pair_tensor(di_dtype dt, const di_pair_desc* descs, int32_t nu
   hipStream_t s = (hipStream_t)stream;
   // aligned16: every channel plane (L1*L2), out_off, L2 and h2_row is a multiple of 16 bytes of
   // elements: 16-B vector loads and non-temporal 16-B stores.
+  const int vec = dt == DI_BF16 ? 8 : 4;
+#ifndef DI_PAIR_LEGACY
+  if (aligned16) {
+    const int rblocks = (max_l1 + PAIR_ROWS - 1) / PAIR_ROWS;
+    const int64_t ritems64 = (int64_t)num_complexes * 2 * hidden * rblocks;
+    if (ritems64 > INT32_MAX) return DI_ERANGE;
+    const int ritems = (int)ritems64;
+    const unsigned rgrid = (unsigned)(ritems < max_blocks ? ritems : max_blocks);
+    if (dt == DI_BF16)
+      hipLaunchKernelGGL((k_pair_rows<u16>), dim3(rgrid), dim3(PAIR_ROW_THREADS), 0, s, descs, hidden, (const u16*)h,
+                         (const u16*)hT, num_rows, rblocks, ritems, (u16*)out);
+    else
+      hipLaunchKernelGGL((k_pair_rows<float>), dim3(rgrid), dim3(PAIR_ROW_THREADS), 0, s, descs, hidden,
+                         (const float*)h, (const float*)hT, num_rows, rblocks, ritems, (float*)out);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? DI_OK : (int)e;
+  }
+#endif
   if (dt == DI_BF16) {
     if (aligned16)
       hipLaunchKernelGGL((k_pair_tensor<u16, true>), dim3(grid), dim3(PAIR_THREADS), 0, s, descs, hidden,

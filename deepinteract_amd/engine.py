@@ -95,11 +95,13 @@ class GeoTEngine:
             })
         return self._ws[slot][1]
 
-    def forward(self, gb: GraphBatch, clone: bool = True, events=None, slot: int = 0):
+    def forward(self, gb: GraphBatch, clone: bool = True, events=None, slot: int = 0, after_init=None):
         """-> (node feats [Nt,128], edge feats [Et,128]) in the engine dtype.
 
         events: optional dict kernel-name -> list; (start, end) torch.cuda.Event pairs are recorded
-        around every launch on the launch stream (for per-kernel timing in bench.py)."""
+        around every launch on the launch stream (for per-kernel timing in bench.py).
+        after_init: optional torch.cuda.Event recorded right after the InitEdge launch (lets a
+        concurrent HBM-bound consumer start once the memory-heavy prologue has passed)."""
         lib, p, dt = self.lib, self.packed, _DI_DT[self.dtype]
         ws = self.workspace(gb.num_nodes, gb.num_edges, slot)
         g = ctypes.byref(gb.c_graph)
@@ -113,6 +115,8 @@ class GeoTEngine:
         _lib.check(lib.di_init_edge(g, dt, _ptr(gb.edge_f), _ptr(p.init[0]), _ptr(p.init[1]),
                                     _ptr(p.pos_src), _ptr(p.pos_dst), _ptr(f[0]), _ptr(fn[0]), st),
                    "di_init_edge")
+        if after_init is not None:
+            after_init.record(torch.cuda.current_stream())
         L = p.num_layers
         cur = 0
         for li in range(L):

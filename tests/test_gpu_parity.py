@@ -103,6 +103,30 @@ def test_pair_tensor_batched_bf16_unaligned():
         assert torch.equal(v, ref)
 
 
+@pytest.mark.parametrize("dtype,sizes", [
+    (torch.bfloat16, [(16, 24), (264, 8), (520, 1000), (8, 4104)]),   # 4104: 5 row segments
+    (torch.float32, [(12, 4), (300, 1000), (4, 2052)]),
+])
+def test_pair_tensor_batched_aligned(dtype, sizes):
+    """Ragged aligned batch through the row-streaming kernel: planes spanning several row blocks,
+    rows spanning several 128-chunk segments, varying L1/L2 per complex."""
+    from deepinteract_amd.engine import PairTensorOp
+    torch.manual_seed(1)
+    rows = sum(a + b for a, b in sizes)
+    h = torch.randn(rows, 128, device="cuda").to(dtype)
+    h1r, h2r, r = [], [], 0
+    for a, b in sizes:
+        h1r.append(r)
+        h2r.append(r + a)
+        r += a + b
+    _, views = PairTensorOp()(h, h1r, h2r, [a for a, _ in sizes], [b for _, b in sizes], hT=h.t().contiguous())
+    torch.cuda.synchronize()
+    for (a, b), s1, s2, v in zip(sizes, h1r, h2r, views):
+        ref = torch.cat((h[s1:s1 + a].t().unsqueeze(0).unsqueeze(3).expand(1, 128, a, b),
+                         h[s2:s2 + b].t().unsqueeze(0).unsqueeze(2).expand(1, 128, a, b)), 1)
+        assert torch.equal(v, ref)
+
+
 @pytest.mark.parametrize("case", ["knn1k", "tiny", "c1", "c2"])
 def test_knn_bit_exact(case):
     from deepinteract_amd.builder import knn

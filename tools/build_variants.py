@@ -31,6 +31,17 @@ VARIANTS = {
     "stagger120": ["DI_X_STAGGER=120"],
     "nw8": ["DI_GEO_NW=8"],
     "nw8_order3": ["DI_GEO_NW=8", "DI_MMA_ORDER=3"],
+    "noslp": ["-fno-slp-vectorize"],
+    "prow_strided": ["DI_PAIR_ROWS_STRIDED"],
+    "prow_plain": ["DI_PAIR_STORE=0"],
+    "prow_legacy": ["DI_PAIR_LEGACY"],
+    "prow_w1": ["DI_PAIR_ROW_WAVES=1"],
+    "prow_w2": ["DI_PAIR_ROW_WAVES=2"],
+    "nw8_nobar": ["DI_GEO_NW=8", "DI_X_NOBAR"],
+    "nw8_nodma": ["DI_GEO_NW=8", "DI_X_NODMA"],
+    "nw8_nodma_nobar": ["DI_GEO_NW=8", "DI_X_NODMA", "DI_X_NOBAR"],
+    "pair_sc1": ["DI_PAIR_STORE=16"],
+    "pair_sc1nt": ["DI_PAIR_STORE=18"],
 }
 
 if __name__ == "__main__":

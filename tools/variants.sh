@@ -7,6 +7,6 @@ cd "$R"
 ARGS="${BENCH_ARGS:---no-cpu --overlap 0 --complexes 256 --steps 2 --warmup 1}"
 specs=()
 for n in "$@"; do
-  specs+=("var_$n:300:DI_LIB=$R/deepinteract_amd/lib/variants/$n/libdeepinteract_amd.so python bench.py $ARGS > gpurun_out/var_$n.json")
+  specs+=("var${TAG}_$n:300:DI_LIB=$R/deepinteract_amd/lib/variants/$n/libdeepinteract_amd.so python bench.py $ARGS > gpurun_out/var${TAG}_$n.json")
 done
-exec "$R/tools/gpu_run.sh" "${specs[@]}"
+"$R/tools/gpu_run.sh" "${specs[@]}"
