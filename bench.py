@@ -144,11 +144,21 @@ def main():
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
     ap.add_argument("--cpu-sample", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--pair-cus", type=int, default=0,
+                    help="K > 0: pair tensor on a CU-masked stream of K dedicated CUs (K blocks x 8 waves), "
+                         "GeoT on the other CUs (needs --overlap 1)")
+    ap.add_argument("--cu-layout", default="stride", choices=["stride", "contig"])
+    ap.add_argument("--pair-kernel", default=None, choices=["rows", "vector"],
+                    help="aligned pair-tensor kernel (default: rows alone, vector beside GeoT)")
+    ap.add_argument("--pair-blocks", type=int, default=0)
+    ap.add_argument("--pair-waves", type=int, default=0)
     ap.add_argument("--overlap", type=int, default=1, choices=[0, 1, 2],
                     help="0: one stream; 1: pair tensor of micro-batch m-1 on its own stream beside GeoT of m; "
                          "2: as 1, started after InitEdge of m")
     args = ap.parse_args()
 
+    if args.pair_kernel is None:
+        args.pair_kernel = "vector" if args.overlap and not args.pair_cus else "rows"
     ws, rank, local = dist_setup()
     dev = torch.device("cuda", local)
     from deepinteract_amd import synth
@@ -161,7 +171,13 @@ def main():
     assert args.complexes % M == 0
     sd = seeded_state_dict(0, with_head=False)
     eng = GeoTEngine(sd, args.dtype, device=dev)
-    pair = PairTensorOp(dev)
+    num_cus = torch.cuda.get_device_properties(dev).multi_processor_count
+    if args.pair_cus:
+        if not args.overlap:
+            raise SystemExit("--pair-cus needs --overlap 1 or 2")
+        pair = PairTensorOp(dev, blocks=args.pair_cus, waves_per_block=8, kernel=args.pair_kernel)
+    else:
+        pair = PairTensorOp(dev, blocks=args.pair_blocks, waves_per_block=args.pair_waves, kernel=args.pair_kernel)
 
     # ---- inputs: a pool of distinct complexes built on the device (kNN + features + ids) ----
     P = min(args.pool, args.complexes)
@@ -190,8 +206,14 @@ def main():
     esz = 2 if args.dtype == "bf16" else 4
     pair_buf = torch.empty(M * 2 * H * n_res * n_res, dtype=tdt, device=dev)
 
-    s_geot = torch.cuda.current_stream(dev)
-    s_pair = torch.cuda.Stream(dev) if args.overlap else s_geot
+    if args.pair_cus:
+        from deepinteract_amd.streams import masked_stream, split_cus
+        cus_pair, cus_geot = split_cus(num_cus, args.pair_cus, args.cu_layout)
+        s_geot = masked_stream(dev, cus_geot, num_cus)
+        s_pair = masked_stream(dev, cus_pair, num_cus)
+    else:
+        s_geot = torch.cuda.current_stream(dev)
+        s_pair = torch.cuda.Stream(dev) if args.overlap else s_geot
     done = [None, None]  # per workspace slot: event after the pair tensor that last read it
 
     def launch_pair(h, hT, ready, slot, after=None, events=None):
@@ -282,7 +304,10 @@ def main():
                    "complexes_per_gpu_per_step": args.complexes, "micro_batch": M, "residues": [n_res, n_res],
                    "knn": k, "parallelism": f"complex-sharded dp{ws}",
                    "streams": ["1 stream", "GeoT || pair-tensor (2 HIP streams)",
-                               "GeoT || pair-tensor (2 HIP streams, pair after InitEdge)"][args.overlap]},
+                               "GeoT || pair-tensor (2 HIP streams, pair after InitEdge)"][args.overlap]
+                   + (f"; pair on {args.pair_cus} dedicated CUs ({args.cu_layout}), GeoT on "
+                      f"{num_cus - args.pair_cus}" if args.pair_cus else "")
+                   + f"; pair kernel {args.pair_kernel}"},
         "hbm_frac_of_peak": round(hbm_frac, 4),
         "roofline": roof,
         "kernels": {n: {kk: round(v, 3) if isinstance(v, float) else v for kk, v in r.items()} for n, r in kern.items()},

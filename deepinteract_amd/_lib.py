@@ -41,6 +41,7 @@ _SIGS = {
                       ctypes.c_int),
     "di_node_layer": ([ctypes.POINTER(DiGraph), _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P], ctypes.c_int),
     "di_pair_tensor": ([_I, _P, _I, _I, _I, _I, _I, _P, _P, _I, _P, _P], ctypes.c_int),
+    "di_pair_config": ([_I, _I, _I], ctypes.c_int),
     "di_knn_topk": ([_I, _P, _P, _I, _I, _P, _P, _P], ctypes.c_int),
     "di_geo_feats": ([ctypes.POINTER(DiGeoArgs), _P], ctypes.c_int),
     "di_build_nbr_ids": ([_I, _P, _P, _P, ctypes.c_uint64, _P, _P], ctypes.c_int),

@@ -260,8 +260,37 @@ __device__ __forceinline__ void unpack_op(Act<2 * NS>& a, const Op<BF16T, NS>& o
 #ifndef DI_MMA_ORDER
 #define DI_MMA_ORDER 3
 #endif
+// DMA pump: with a weight pipe passed in, one pending LDS-DMA piece of the NEXT stage is issued
+// after every DI_DMA_PUMP MFMAs (0: the stage's pieces are issued in one burst at stage start),
+// so the issue cost of the weight stream hides between this wave's MFMAs. Measured (C3 edge
+// layer, bf16): burst 503 us, pump every 1/2/4 MFMAs 576/575/559 us (extra spills) -> off.
+#ifndef DI_DMA_PUMP
+#define DI_DMA_PUMP 0
+#endif
+constexpr int BUF_RSRC_W3 = 0x00020000;  // gfx9 raw buffer: DATA_FORMAT 32, no swizzle / stride
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* g) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(g), 0, 0x7fffffff, BUF_RSRC_W3);
+}
+
+// Pending LDS-DMA pieces of the next weight stage: 1-KiB pieces [pi, pk) of src -> dst, stepping
+// by the block's wave count (wave-uniform state).
+struct DmaPump {
+  const char* src = nullptr;
+  char* dst = nullptr;
+  int pi = 0, pk = 0, step = 1;
+  __device__ __forceinline__ void pump() {
+    if (pi < pk) {
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(buf_rsrc(src),
+                                               (__attribute__((address_space(3))) void*)(dst + pi * 1024), 16,
+                                               (threadIdx.x & 63) * 16, pi * 1024, 0, 0);
+      pi += step;
+    }
+  }
+};
 template <int NBO, int NS>
-__device__ __forceinline__ void mma(Act<NBO>& out, const Op<BF16T, NS>& op, const u16* w, int lane) {
+__device__ __forceinline__ void mma(Act<NBO>& out, const Op<BF16T, NS>& op, const u16* w, int lane,
+                                    DmaPump* pp = nullptr) {
   if constexpr (DI_MMA_ORDER == 0 || DI_MMA_ORDER == 2) {  // k-step major
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
@@ -282,18 +311,22 @@ __device__ __forceinline__ void mma(Act<NBO>& out, const Op<BF16T, NS>& op, cons
 #pragma unroll
     for (int b0 = 0; b0 < NBO; b0 += G) {
 #pragma unroll
-      for (int s = 0; s < NS; ++s)
+      for (int s = 0; s < NS; ++s) {
 #pragma unroll
         for (int bo = b0; bo < b0 + G; ++bo) {
           const bf16x8 af = *reinterpret_cast<const bf16x8*>(w + (bo * NS + s) * BLK + lane * 8);
           out.v[bo] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, op.f[s], out.v[bo], 0, 0, 0);
         }
+        if constexpr (DI_DMA_PUMP > 0)
+          if (pp && ((b0 / G) * NS + s) % (DI_DMA_PUMP < G ? 1 : DI_DMA_PUMP / G) == 0) pp->pump();
+      }
       if constexpr (DI_MMA_ORDER == 1) __builtin_amdgcn_sched_barrier(0);
     }
   }
 }
 template <int NBO, int NS>
-__device__ __forceinline__ void mma(Act<NBO>& out, const Op<F32T, NS>& op, const float* w, int lane) {
+__device__ __forceinline__ void mma(Act<NBO>& out, const Op<F32T, NS>& op, const float* w, int lane,
+                                    DmaPump* = nullptr) {
 #pragma unroll
   for (int s = 0; s < NS; ++s)
 #pragma unroll
@@ -311,10 +344,11 @@ __device__ __forceinline__ void mma(Act<NBO>& out, const Op<F32T, NS>& op, const
 
 // convenience: out += W . a   (a has 2*NS blocks)
 template <class DT, int NBO, int NS>
-__device__ __forceinline__ void linear(Act<NBO>& out, const Act<2 * NS>& a, const typename DT::T* w, int lane) {
+__device__ __forceinline__ void linear(Act<NBO>& out, const Act<2 * NS>& a, const typename DT::T* w, int lane,
+                                       DmaPump* pp = nullptr) {
   Op<DT, NS> op;
   make_op(op, a);
-  mma<NBO, NS>(out, op, w, lane);
+  mma<NBO, NS>(out, op, w, lane, pp);
 }
 
 // ------------------------------------------------------------------ weight staging
@@ -324,12 +358,6 @@ __device__ __forceinline__ void linear(Act<NBO>& out, const Act<2 * NS>& a, cons
 // Issued as buffer_load_dwordx4 ... lds with an SGPR buffer resource and SGPR offset, and the
 // wave index made wave-uniform (readfirstlane): per 1 KiB piece the loop is scalar except the
 // load itself (s_mov m0, s_add, buffer_load; the lane offset is a loop-invariant VGPR).
-constexpr int BUF_RSRC_W3 = 0x00020000;  // gfx9 raw buffer: DATA_FORMAT 32, no swizzle / stride
-
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* g) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(g), 0, 0x7fffffff, BUF_RSRC_W3);
-}
-
 template <int NW, typename T>
 __device__ __forceinline__ void dma_blocks(T* lds, const T* g, int nblk) {
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -379,8 +407,18 @@ struct WPipe {
   __device__ __forceinline__ float* slot_v(int s) const {
     return reinterpret_cast<float*>(base + (DBUF ? s : 0) * SLOT_BYTES + CAP * BLK * (int)sizeof(T));
   }
+  // pumped DMA (DBUF and DI_DMA_PUMP): the next stage's pieces, issued between MFMAs
+  DmaPump dp;
+  __device__ __forceinline__ DmaPump* pump_ptr() { return (DBUF && DI_DMA_PUMP > 0) ? &dp : nullptr; }
   __device__ __forceinline__ void issue(const T* g, int nblk, const float* gv = nullptr, int nvec = 0) {
-    if constexpr (DBUF) {
+    if constexpr (DBUF && DI_DMA_PUMP > 0) {
+      dp.src = reinterpret_cast<const char*>(g);
+      dp.dst = reinterpret_cast<char*>(slot_w(cur ^ 1));
+      dp.pi = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+      dp.pk = nblk * BLK * (int)sizeof(T) / 1024;
+      dp.step = NW;
+      if (gv) dma_vec<NW>(slot_v(cur ^ 1), gv, nvec / 128);
+    } else if constexpr (DBUF) {
       dma_blocks<NW>(slot_w(cur ^ 1), g, nblk);
       if (gv) dma_vec<NW>(slot_v(cur ^ 1), gv, nvec / 128);
     } else {
@@ -392,6 +430,8 @@ struct WPipe {
   }
   __device__ __forceinline__ const T* next() {
     if constexpr (DBUF) {
+      if constexpr (DI_DMA_PUMP > 0)
+        while (dp.pi < dp.pk) dp.pump();  // pieces the stage's MFMAs did not carry
 #ifndef DI_X_NOBAR  // timing experiment only: results are wrong without the barrier
       __syncthreads();
 #endif
@@ -432,6 +472,7 @@ struct RingPipe {
     return reinterpret_cast<float*>(base + s * SLOT_BYTES + CAP * BLK * (int)sizeof(T));
   }
   __device__ __forceinline__ int nxt(int s) const { return s == NSLOT - 1 ? 0 : s + 1; }
+  __device__ __forceinline__ DmaPump* pump_ptr() { return nullptr; }
   // DMA of the stage AFTER the current one (group 0 only)
   __device__ __forceinline__ void issue(const T* g, int nblk, const float* gv = nullptr, int nvec = 0) {
     if (loader) {

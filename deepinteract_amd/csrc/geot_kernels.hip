@@ -188,6 +188,7 @@ void k_init_edge(InitArgs a) {
   const int e = valid ? r : a.Et - 1;
   const T* W = reinterpret_cast<const T*>(a.wmat);
   WPipe<T, G::NW, G::DBUF, CAP> pipe(lds);
+  DmaPump* PP = pipe.pump_ptr();
   pipe.issue(W + IE_T0 * BLK, 40);
 
   Act<2> geo;
@@ -206,9 +207,9 @@ void k_init_edge(InitArgs a) {
     else pipe.issue(W + IE_GEO1 * BLK, 40);
     Act<8> y;
     zero(y);
-    mma<8, 1>(y, gop, w, lane);
+    mma<8, 1>(y, gop, w, lane, PP);
     if (t > 0) silu_<8, FAST>(y);
-    linear<DT, 8, 4>(acc, y, w + 8 * BLK, lane);
+    linear<DT, 8, 4>(acc, y, w + 8 * BLK, lane, PP);
   }
   silu_<8, FAST>(acc);  // combined_edge_logits
   // gating: (em1 + silu(d1) + silu(r1) + silu(o1) + silu(a1)) * c
@@ -221,7 +222,7 @@ void k_init_edge(InitArgs a) {
     for (int t = 0; t < 5; ++t) {
       Act<8> y;
       zero(y);
-      mma<8, 1>(y, gop, w + 8 * t * BLK, lane);
+      mma<8, 1>(y, gop, w + 8 * t * BLK, lane, PP);
       if (t > 0) silu_<8, FAST>(y);
       add_(gs, y);
     }
@@ -234,9 +235,9 @@ void k_init_edge(InitArgs a) {
     pipe.issue(W + IE_NBR * BLK, MAT128);
     Act<2> z;
     zero(z);
-    linear<DT, 2, 4>(z, acc, w, lane);
+    linear<DT, 2, 4>(z, acc, w, lane, PP);
     zero(f);
-    linear<DT, 8, 1>(f, z, w + 8 * BLK, lane);
+    linear<DT, 8, 1>(f, z, w + 8 * BLK, lane, PP);
   }
   if (valid) store_row(f, reinterpret_cast<T*>(a.f_out) + (int64_t)e * HID, g);
   // layer-0 silu(nbr_linear(F)), applied once per edge and gathered by the conformation module
@@ -245,7 +246,7 @@ void k_init_edge(InitArgs a) {
     const T* w = pipe.next();
     Act<8> fn;
     init_vec(fn, a.wvec + IEV_NBR, g);
-    linear<DT, 8, 4>(fn, f, w, lane);
+    linear<DT, 8, 4>(fn, f, w, lane, PP);
     silu_<8, FAST>(fn);
     if (valid) store_row(fn, reinterpret_cast<T*>(a.fn_out) + (int64_t)e * HID, g);
   }
@@ -322,13 +323,14 @@ struct EdgeStages {
 template <class DT, int MODE>
 __device__ __forceinline__ void res_block(Act<8>& x, EdgeStages<DT, MODE>& st, int lane, int g) {
   constexpr bool FAST = DT::kBF16;
+  DmaPump* PP = st.pipe.pump_ptr();
   Act<8> y = x;
 #pragma unroll 1
   for (int l = 0; l < 3; ++l) {
     const typename DT::T* w = st.next();
     Act<8> t;
     init_vec_lds(t, st.pipe.v(), g);
-    linear<DT, 8, 4>(t, y, w, lane);
+    linear<DT, 8, 4>(t, y, w, lane, PP);
     st.pipe.mid();
     silu_<8, FAST>(t);
     y = t;
@@ -384,6 +386,7 @@ void k_edge_layer(EdgeArgs a) {
   const T* qkv = reinterpret_cast<const T*>(a.qkv);
 
   EdgePipe<DT> pipe(lds);
+  DmaPump* PP = pipe.pump_ptr();
   EdgeStages<DT, MODE> st{pipe, W, a.wvec, 0, false};
   pipe.issue(W + EL_S0 * BLK, EL_SIZE[0]);
 #ifdef DI_X_STAGGER
@@ -424,12 +427,12 @@ void k_edge_layer(EdgeArgs a) {
     {
       Act<4> t1;
       zero(gate);
-      mma<4, 1>(gate, gop, w + 8 * BLK, lane);
+      mma<4, 1>(gate, gop, w + 8 * BLK, lane, PP);
       zero(t1);
-      mma<4, 1>(t1, gop, w + 12 * BLK, lane);
+      mma<4, 1>(t1, gop, w + 12 * BLK, lane, PP);
       mul_(gate, t1);
       zero(t1);
-      mma<4, 1>(t1, gop, w + 16 * BLK, lane);
+      mma<4, 1>(t1, gop, w + 16 * BLK, lane, PP);
       mul_(gate, t1);
     }
     Act<4> s;
@@ -448,14 +451,14 @@ void k_edge_layer(EdgeArgs a) {
       asm volatile("" ::: "memory");
       Act<8> dg;
       zero(dg);
-      mma<8, 1>(dg, gop, w, lane);
+      mma<8, 1>(dg, gop, w, lane, PP);
 #pragma unroll
       for (int b = 0; b < 8; ++b)
 #pragma unroll
         for (int q = 0; q < 4; ++q) x.v[b][q] *= dg.v[b][q];  // gathered rows are silu(nbr_linear(F))
       Act<4> y;
       zero(y);
-      linear<DT, 4, 4>(y, x, w + 20 * BLK, lane);  // downward_proj
+      linear<DT, 4, 4>(y, x, w + 20 * BLK, lane, PP);  // downward_proj
 #pragma unroll
       for (int b = 0; b < 4; ++b)
 #pragma unroll
@@ -465,7 +468,7 @@ void k_edge_layer(EdgeArgs a) {
     Act<8> x;
     w = st.next();  // stage 1: upward_proj (+ orig_msg_linear bias)
     zero(x);
-    linear<DT, 8, 2>(x, s, w, lane);
+    linear<DT, 8, 2>(x, s, w, lane, PP);
     pipe.mid();
     silu_<8, FAST>(x);
     {
@@ -474,7 +477,7 @@ void k_edge_layer(EdgeArgs a) {
       add_(x, bo);
     }
     w = st.next();  // stage 2: orig_msg_linear(res) + nbr
-    mma<8, 4>(x, fr.operand(f_row, g), w, lane);
+    mma<8, 4>(x, fr.operand(f_row, g), w, lane, PP);
     pipe.mid();
     res_block<DT, MODE>(x, st, lane, g);
     res_block<DT, MODE>(x, st, lane, g);
@@ -482,7 +485,7 @@ void k_edge_layer(EdgeArgs a) {
       w = st.next();  // res_connect_linear
       Act<8> y;
       init_vec_lds(y, pipe.v(), g);
-      linear<DT, 8, 4>(y, x, w, lane);
+      linear<DT, 8, 4>(y, x, w, lane, PP);
       pipe.mid();
       silu_<8, FAST>(y);
       fr.act(x, f_row, g);
@@ -495,13 +498,13 @@ void k_edge_layer(EdgeArgs a) {
       if ((FINAL || CONF) && more) in.load_ids(a, en);
       Act<8> fg;
       zero(fg);
-      mma<8, 1>(fg, gop, w, lane);
+      mma<8, 1>(fg, gop, w, lane, PP);
       mul_(x, fg);
       pipe.mid();
       w = st.next();  // final_linear
       Act<8> y;
       init_vec_lds(y, pipe.v(), g);
-      linear<DT, 8, 4>(y, x, w, lane);
+      linear<DT, 8, 4>(y, x, w, lane, PP);
       pipe.mid();
       silu_<8, FAST>(y);
       fr.act(x, f_row, g);
@@ -522,7 +525,7 @@ void k_edge_layer(EdgeArgs a) {
     if (!FINAL && more) in.load_ids(a, en);
     Act<8> p;
     init_vec_lds(p, pipe.v(), g);
-    linear<DT, 8, 4>(p, x, w, lane);
+    linear<DT, 8, 4>(p, x, w, lane, PP);
     pipe.mid();
     {
       Act<8> kq, qd;
@@ -548,7 +551,7 @@ void k_edge_layer(EdgeArgs a) {
       w = st.next();  // O_edge_feats
       Act<8> e1;
       init_vec_lds(e1, pipe.v(), g);
-      linear<DT, 8, 4>(e1, p, w, lane);
+      linear<DT, 8, 4>(e1, p, w, lane, PP);
       pipe.mid();
       {
         Act<8> fa;
@@ -563,11 +566,11 @@ void k_edge_layer(EdgeArgs a) {
         if (half == 0 && more) in.load_rest(a, en, g);  // F of this tile is dead from here on
         Act<8> t;
         init_vec_lds(t, pipe.v(), g);
-        linear<DT, 8, 4>(t, e1, w, lane);
+        linear<DT, 8, 4>(t, e1, w, lane, PP);
         pipe.mid();
         silu_<8, FAST>(t);
         w = st.next();  // edge_feats_MLP.3, input half
-        linear<DT, 8, 4>(o, t, w, lane);
+        linear<DT, 8, 4>(o, t, w, lane, PP);
         pipe.mid();
       }
       add_(e1, o);
@@ -575,7 +578,7 @@ void k_edge_layer(EdgeArgs a) {
       w = st.next();  // next layer's silu(nbr_linear(.))
       Act<8> fn;
       init_vec_lds(fn, pipe.v(), g);
-      linear<DT, 8, 4>(fn, e1, w, lane);
+      linear<DT, 8, 4>(fn, e1, w, lane, PP);
       pipe.mid();
       silu_<8, FAST>(fn);
       if (valid) store_row(fn, reinterpret_cast<T*>(a.fn_out) + (int64_t)e * HID, g);

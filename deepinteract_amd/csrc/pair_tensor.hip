@@ -139,18 +139,17 @@ __global__ __launch_bounds__(PAIR_THREADS) void k_pair_tensor(const di_pair_desc
 // per-lane constant voffset and the row offset in an SGPR, so a 2-KB row costs two store
 // instructions plus scalar address arithmetic, and no load sits between stores.
 // <= 32 VGPRs: one wave per SIMD co-resides with the edge kernels (2 x 240 VGPRs).
-#ifndef DI_PAIR_ROW_WAVES
-#define DI_PAIR_ROW_WAVES 4
-#endif
-constexpr int PAIR_ROW_THREADS = 64 * DI_PAIR_ROW_WAVES;
-constexpr int PAIR_ROWS = 64 * DI_PAIR_ROW_WAVES;  // rows per work item (64 per wave)
-constexpr int PAIR_SEG = 128;                      // 16-B chunks per row segment (2 per lane)
+// Block size is a launch parameter (di_pair_config): 4 waves x one block per CU when the kernel
+// shares every CU with GeoT, 8 waves on a few dedicated CUs (CU-masked stream): 64 CUs alone
+// store 5.6 TB/s, 32 CUs 3.4 TB/s (C3 micro-batch of 8 complexes).
+constexpr int PAIR_SEG = 128;  // 16-B chunks per row segment (2 per lane)
 template <typename T>
-__global__ __launch_bounds__(PAIR_ROW_THREADS) __attribute__((amdgpu_num_vgpr(32)))
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_num_vgpr(32)))
 void k_pair_rows(const di_pair_desc* __restrict__ descs, int hidden, const T* __restrict__ h,
                  const T* __restrict__ hT, int nrows, int rblocks, int items, T* __restrict__ out) {
   using V = typename Vec16<T>::V;
   constexpr int VEC = Vec16<T>::N;
+  const int PAIR_ROWS = (int)blockDim.x;  // rows per work item: 64 per wave
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   for (int item = blockIdx.x; item < items; item += gridDim.x) {
@@ -205,6 +204,24 @@ void k_pair_rows(const di_pair_desc* __restrict__ descs, int hidden, const T* __
 
 using namespace di;
 
+// resident grid of the persistent pair kernels and waves per row-kernel block (di_pair_config)
+static int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  const int v = e ? atoi(e) : 0;
+  return v > 0 ? v : dflt;
+}
+static int g_pair_blocks = env_int("DI_PAIR_BLOCKS", PAIR_MAX_BLOCKS);
+static int g_pair_waves = env_int("DI_PAIR_WAVES", 4);
+static int g_pair_kernel = env_int("DI_PAIR_KERNEL", 1);  // 1 row-streaming, 2 per-vector (aligned path)
+
+extern "C" int di_pair_config(int32_t blocks, int32_t waves_per_block, int32_t kernel) {
+  if (blocks < 0 || waves_per_block < 0 || waves_per_block > 16 || kernel < 0 || kernel > 2) return DI_EINVAL;
+  if (blocks > 0) g_pair_blocks = blocks;
+  if (waves_per_block > 0) g_pair_waves = waves_per_block;
+  if (kernel > 0) g_pair_kernel = kernel;
+  return DI_OK;
+}
+
 extern "C" int di_pair_tensor(di_dtype dt, const di_pair_desc* descs, int32_t num_complexes, int32_t max_l1,
                               int32_t max_l2, int32_t hidden, int32_t aligned16, const void* h, const void* hT,
                               int32_t num_rows, void* out, void* stream) {
@@ -216,28 +233,25 @@ extern "C" int di_pair_tensor(di_dtype dt, const di_pair_desc* descs, int32_t nu
   const int64_t items64 = (int64_t)num_complexes * 2 * hidden * chunks;
   if (items64 > INT32_MAX) return DI_ERANGE;
   const int items = (int)items64;
-  static const int max_blocks = [] {
-    const char* e = getenv("DI_PAIR_BLOCKS");  // tuning knob: resident blocks of the persistent grid
-    const int v = e ? atoi(e) : 0;
-    return v > 0 ? v : PAIR_MAX_BLOCKS;
-  }();
+  const int max_blocks = g_pair_blocks;
   const unsigned grid = (unsigned)(items < max_blocks ? items : max_blocks);
   hipStream_t s = (hipStream_t)stream;
   // aligned16: every channel plane (L1*L2), out_off, L2 and h2_row is a multiple of 16 bytes of
   // elements: 16-B vector loads and non-temporal 16-B stores.
   const int vec = dt == DI_BF16 ? 8 : 4;
 #ifndef DI_PAIR_LEGACY
-  if (aligned16) {
-    const int rblocks = (max_l1 + PAIR_ROWS - 1) / PAIR_ROWS;
+  if (aligned16 && g_pair_kernel == 1) {
+    const int rows = 64 * g_pair_waves;  // rows per work item
+    const int rblocks = (max_l1 + rows - 1) / rows;
     const int64_t ritems64 = (int64_t)num_complexes * 2 * hidden * rblocks;
     if (ritems64 > INT32_MAX) return DI_ERANGE;
     const int ritems = (int)ritems64;
     const unsigned rgrid = (unsigned)(ritems < max_blocks ? ritems : max_blocks);
     if (dt == DI_BF16)
-      hipLaunchKernelGGL((k_pair_rows<u16>), dim3(rgrid), dim3(PAIR_ROW_THREADS), 0, s, descs, hidden, (const u16*)h,
+      hipLaunchKernelGGL((k_pair_rows<u16>), dim3(rgrid), dim3(rows), 0, s, descs, hidden, (const u16*)h,
                          (const u16*)hT, num_rows, rblocks, ritems, (u16*)out);
     else
-      hipLaunchKernelGGL((k_pair_rows<float>), dim3(rgrid), dim3(PAIR_ROW_THREADS), 0, s, descs, hidden,
+      hipLaunchKernelGGL((k_pair_rows<float>), dim3(rgrid), dim3(rows), 0, s, descs, hidden,
                          (const float*)h, (const float*)hT, num_rows, rblocks, ritems, (float*)out);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? DI_OK : (int)e;

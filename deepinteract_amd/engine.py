@@ -148,10 +148,17 @@ class GeoTEngine:
 class PairTensorOp:
     """construct_interact_tensor (deepinteract_utils.py:158-172) for a batch of complexes."""
 
-    def __init__(self, device="cuda"):
+    KERNELS = {"rows": 1, "vector": 2}
+
+    def __init__(self, device="cuda", blocks: int = 0, waves_per_block: int = 0, kernel: str | None = None):
+        """blocks / waves_per_block / kernel ("rows" | "vector"): launch shape and kernel of the
+        16-B-aligned path (di_pair_config; 0 / None keep the library's current setting)."""
         self.lib = _lib.load()
         self.device = torch.device(device)
         self._desc_cache = {}
+        k = self.KERNELS[kernel] if kernel else 0
+        if blocks or waves_per_block or k:
+            _lib.check(self.lib.di_pair_config(blocks, waves_per_block, k), "di_pair_config")
 
     def descs(self, h1_rows, h2_rows, l1s, l2s, hidden):
         key = (tuple(h1_rows), tuple(h2_rows), tuple(l1s), tuple(l2s), hidden)

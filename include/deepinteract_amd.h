@@ -100,6 +100,14 @@ int di_node_layer(const di_graph* g, di_dtype dt, int final_layer, const float* 
  * (di_node_layer's hT_out), which turns chain-2 column reads into 16-B vector loads.
  * aligned16 != 0 promises every L1*L2 plane, out_off, L2 and h2_row are multiples of 16 bytes
  * worth of elements (vector loads/stores). Output stores are non-temporal (write-once stream). */
+/* Launch shape of the persistent pair-tensor kernels (process-wide; 0 keeps a value): `blocks`
+ * resident blocks, `waves_per_block` (1..16) waves per row-streaming block, `kernel` for the
+ * 16-B-aligned case: 1 row-streaming (loads hoisted out of the store stream; fastest alone),
+ * 2 per-vector (one load per 16-B store; lighter on a GPU shared with GeoT). Defaults 256 / 4 /
+ * 1 (env DI_PAIR_BLOCKS / DI_PAIR_WAVES / DI_PAIR_KERNEL). Not a reference interface: a
+ * scheduling knob of this build. */
+int di_pair_config(int32_t blocks, int32_t waves_per_block, int32_t kernel);
+
 int di_pair_tensor(di_dtype dt, const di_pair_desc* descs /*device [B]*/, int32_t num_complexes,
                    int32_t max_l1, int32_t max_l2, int32_t hidden, int32_t aligned16, const void* h,
                    const void* hT, int32_t num_rows, void* out, void* stream);

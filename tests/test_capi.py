@@ -38,6 +38,9 @@ def test_invalid_arguments_rejected_without_gpu():
     assert lib.di_node_embed(None, 0, 113, None, None, None, None, None, None) == -1
     assert lib.di_pair_tensor(0, None, 0, 0, 0, 128, 1, None, None, 0, None, None) == -1
     assert lib.di_knn_topk(1, None, None, 20, 10, None, None, None) == -1
+    assert lib.di_pair_config(-1, 4, 0) == -1 and lib.di_pair_config(0, 17, 0) == -1
+    assert lib.di_pair_config(0, 0, 3) == -1
+    assert lib.di_pair_config(0, 0, 0) == 0  # keeps the current launch shape
 
 
 def test_ctypes_struct_layouts():

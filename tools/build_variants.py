@@ -36,6 +36,11 @@ VARIANTS = {
     "prow_plain": ["DI_PAIR_STORE=0"],
     "prow_legacy": ["DI_PAIR_LEGACY"],
     "prow_w1": ["DI_PAIR_ROW_WAVES=1"],
+    "prow_w8": ["DI_PAIR_ROW_WAVES=8"],
+    "prow_w16": ["DI_PAIR_ROW_WAVES=16"],
+    "pump1": ["DI_DMA_PUMP=1"],
+    "pump2": ["DI_DMA_PUMP=2"],
+    "pump4": ["DI_DMA_PUMP=4"],
     "prow_w2": ["DI_PAIR_ROW_WAVES=2"],
     "nw8_nobar": ["DI_GEO_NW=8", "DI_X_NOBAR"],
     "nw8_nodma": ["DI_GEO_NW=8", "DI_X_NODMA"],
