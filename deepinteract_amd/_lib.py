@@ -75,6 +75,8 @@ def load(build_if_missing: bool = True):
         _build.build()
     lib = ctypes.CDLL(path or _build.LIB)
     for name, (argtypes, restype) in _SIGS.items():
+        if path and not hasattr(lib, name):  # an older tuning variant (DI_LIB) may lack newer entry points
+            continue
         fn = getattr(lib, name)
         fn.argtypes = argtypes
         fn.restype = restype

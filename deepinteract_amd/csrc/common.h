@@ -97,6 +97,20 @@ __device__ __forceinline__ float silu(float x) {
   else return x / (1.0f + expf(-x));
 }
 
+// SiLU of a pre-activation held in log2 units (bf16 path): for a' = log2(e) * a,
+// a' * rcp(1 + 2^-a') = log2(e) * silu(a) in 4 VALU ops (v_exp_f32 is 2^x; the negation is a free
+// source modifier). The host packing scales the producing layer's weights and bias by log2(e) and
+// the consuming layer's (or gate's) weights by ln(2) (packing.py, "log2-unit SiLU"); used where
+// the SiLU output only feeds a linear layer or a gate. The fp32 path is unscaled: plain silu.
+constexpr float LN2 = 0.6931471805599453f;
+template <bool FAST>
+constexpr float silu2_unit() { return FAST ? LN2 : 1.0f; }  // silu = silu2 * silu2_unit
+template <bool FAST>
+__device__ __forceinline__ float silu2(float x) {
+  if constexpr (FAST) return x * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-x));
+  else return silu<false>(x);
+}
+
 // ------------------------------------------------------------------ activations
 template <int NB>  // NB blocks of 16 features
 struct Act {
@@ -195,6 +209,21 @@ __device__ __forceinline__ void silu_(Act<NB>& a) {
   for (int b = 0; b < NB; ++b)
 #pragma unroll
     for (int r = 0; r < 4; ++r) a.v[b][r] = silu<FAST>(a.v[b][r]);
+}
+
+template <int NB, bool FAST>
+__device__ __forceinline__ void silu2_(Act<NB>& a) {
+#pragma unroll
+  for (int b = 0; b < NB; ++b)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) a.v[b][r] = silu2<FAST>(a.v[b][r]);
+}
+
+// a += k * b (one v_fma per value: folds the ln(2) of a log2-unit SiLU output into a residual add)
+template <int NB>
+__device__ __forceinline__ void add_scaled_(Act<NB>& a, const Act<NB>& b_, float k) {
+#pragma unroll
+  for (int b = 0; b < NB; ++b) a.v[b] += k * b_.v[b];
 }
 
 template <int NB>

@@ -208,10 +208,10 @@ void k_init_edge(InitArgs a) {
     Act<8> y;
     zero(y);
     mma<8, 1>(y, gop, w, lane, PP);
-    if (t > 0) silu_<8, FAST>(y);
+    if (t > 0) silu2_<8, FAST>(y);
     linear<DT, 8, 4>(acc, y, w + 8 * BLK, lane, PP);
   }
-  silu_<8, FAST>(acc);  // combined_edge_logits
+  silu2_<8, FAST>(acc);  // combined_edge_logits (log2 units: feeds the gate product -> linear)
   // gating: (em1 + silu(d1) + silu(r1) + silu(o1) + silu(a1)) * c
   {
     const T* w = pipe.next();
@@ -223,7 +223,7 @@ void k_init_edge(InitArgs a) {
       Act<8> y;
       zero(y);
       mma<8, 1>(y, gop, w + 8 * t * BLK, lane, PP);
-      if (t > 0) silu_<8, FAST>(y);
+      if (t > 0) silu2_<8, FAST>(y);
       add_(gs, y);
     }
     mul_(acc, gs);
@@ -332,10 +332,10 @@ __device__ __forceinline__ void res_block(Act<8>& x, EdgeStages<DT, MODE>& st, i
     init_vec_lds(t, st.pipe.v(), g);
     linear<DT, 8, 4>(t, y, w, lane, PP);
     st.pipe.mid();
-    silu_<8, FAST>(t);
+    silu2_<8, FAST>(t);  // log2 units: folded into the next linear / the residual fma
     y = t;
   }
-  add_(x, y);
+  add_scaled_(x, y, silu2_unit<FAST>());
 }
 
 // One tile's per-row inputs, loaded a tile ahead (persistent blocks): neighbour ids, the 28 edge
@@ -462,7 +462,7 @@ void k_edge_layer(EdgeArgs a) {
 #pragma unroll
       for (int b = 0; b < 4; ++b)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) s.v[b][q] += silu<FAST>(y.v[b][q]) * gate.v[b][q];
+        for (int q = 0; q < 4; ++q) s.v[b][q] += silu2<FAST>(y.v[b][q]) * gate.v[b][q];
       if (j == 1) pipe.mid();
     }
     Act<8> x;
@@ -470,11 +470,12 @@ void k_edge_layer(EdgeArgs a) {
     zero(x);
     linear<DT, 8, 2>(x, s, w, lane, PP);
     pipe.mid();
-    silu_<8, FAST>(x);
+    silu2_<8, FAST>(x);
     {
       Act<8> bo;
       init_vec_lds(bo, pipe.v(), g);
-      add_(x, bo);
+#pragma unroll
+      for (int b = 0; b < 8; ++b) x.v[b] = silu2_unit<FAST>() * x.v[b] + bo.v[b];
     }
     w = st.next();  // stage 2: orig_msg_linear(res) + nbr
     mma<8, 4>(x, fr.operand(f_row, g), w, lane, PP);
@@ -487,9 +488,9 @@ void k_edge_layer(EdgeArgs a) {
       init_vec_lds(y, pipe.v(), g);
       linear<DT, 8, 4>(y, x, w, lane, PP);
       pipe.mid();
-      silu_<8, FAST>(y);
+      silu2_<8, FAST>(y);
       fr.act(x, f_row, g);
-      add_(x, y);
+      add_scaled_(x, y, silu2_unit<FAST>());
     }
     res_block<DT, MODE>(x, st, lane, g);
     res_block<DT, MODE>(x, st, lane, g);
@@ -506,9 +507,9 @@ void k_edge_layer(EdgeArgs a) {
       init_vec_lds(y, pipe.v(), g);
       linear<DT, 8, 4>(y, x, w, lane, PP);
       pipe.mid();
-      silu_<8, FAST>(y);
+      silu2_<8, FAST>(y);
       fr.act(x, f_row, g);
-      add_(x, y);  // conformation output
+      add_scaled_(x, y, silu2_unit<FAST>());  // conformation output
     }
     if constexpr (CONF) {
       if (more) in.load_rest(a, en, g);
@@ -568,7 +569,7 @@ void k_edge_layer(EdgeArgs a) {
         init_vec_lds(t, pipe.v(), g);
         linear<DT, 8, 4>(t, e1, w, lane, PP);
         pipe.mid();
-        silu_<8, FAST>(t);
+        silu2_<8, FAST>(t);
         w = st.next();  // edge_feats_MLP.3, input half
         linear<DT, 8, 4>(o, t, w, lane, PP);
         pipe.mid();
@@ -641,7 +642,7 @@ __global__ __launch_bounds__(THREADS, 2) void k_node_layer(NodeArgs a) {
     Act<8> t;
     init_vec(t, V + NLV_F1 + 128 * half, g);
     linear<DT, 8, 4>(t, n, w, lane);
-    silu_<8, FAST>(t);
+    silu2_<8, FAST>(t);
     w = pipe.next();
     if (half == 0) pipe.issue(W + (NL_F1 + MAT128) * BLK, MAT128);
     else if (!FINAL) pipe.issue(W + NL_Q * BLK, MAT128);

@@ -157,7 +157,7 @@ class PairTensorOp:
         self.device = torch.device(device)
         self._desc_cache = {}
         k = self.KERNELS[kernel] if kernel else 0
-        if blocks or waves_per_block or k:
+        if (blocks or waves_per_block or k) and hasattr(self.lib, "di_pair_config"):
             _lib.check(self.lib.di_pair_config(blocks, waves_per_block, k), "di_pair_config")
 
     def descs(self, h1_rows, h2_rows, l1s, l2s, hidden):

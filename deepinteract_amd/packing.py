@@ -14,6 +14,16 @@ from .config import GeoTConfig
 
 BN_EPS = 1e-5
 BLK = 512
+# log2-unit SiLU (bf16 blobs only; csrc/common.h silu2): a layer whose SiLU output feeds only a
+# linear layer or a gate gets its weights and bias scaled by L2E, so the kernel evaluates
+# a' * rcp(1 + 2^-a') = L2E * silu(a) without the v_mul by log2(e); the consumer's weights (or
+# one gate factor) are scaled by 1/L2E. Exact in real arithmetic; one bf16 rounding of the
+# scaled weights.
+L2E = 1.4426950408889634
+
+
+def _l2e(dtype: str) -> float:
+    return L2E if dtype == "bf16" else 1.0
 
 # ---- csrc/layout.h mirror -------------------------------------------------------------------
 EM_NBLK, EMV_N = 128, 384
@@ -185,20 +195,24 @@ def init_blob(sd, dtype, p="gnn_module.0.init_edge_module",
     """nbr=None: no following layer (standalone InitEdgeModule): the fused silu(nbr_linear)
     output is computed with zero weights and ignored."""
     bb = BlobBuilder(dtype, IE_NBLK, IEV_N)
+    sc = _l2e(dtype)  # log2-unit SiLU: geometric projections, combined logits and gates (silu2)
     wc0 = _np(sd[f"{p}.combined_linear_0.weight"])  # [128, 896]
     for t, kind in enumerate(GEO_ORDER):
-        bb.put(40 * t, _geo_rows(_np(sd[f"{p}.{kind}_linear_0.weight"]), kind))
-        bb.put(40 * t + 8, wc0[:, 256 + 128 * t: 384 + 128 * t])
-        bb.put(200 + 8 * t, _geo_rows(_np(sd[f"{p}.{kind}_linear_1.weight"]), kind))
-    bb.put(240, pad2(_np(sd[f"{p}.combined_linear_1.weight"]), 32, 128))
+        # t > 0: silu2(sc * W_t0 g) = sc * silu(W_t0 g), consumed by wc0 (x 1/sc), accumulated into
+        # sc * acc (x sc): net 1. t = 0 (no SiLU): the wc0 slice carries the sc.
+        bb.put(40 * t, _geo_rows(_np(sd[f"{p}.{kind}_linear_0.weight"]), kind) * (sc if t > 0 else 1.0))
+        bb.put(40 * t + 8, wc0[:, 256 + 128 * t: 384 + 128 * t] * (1.0 if t > 0 else sc))
+        bb.put(200 + 8 * t, _geo_rows(_np(sd[f"{p}.{kind}_linear_1.weight"]), kind) * sc)  # gs' = sc * gs
+    # silu2(sc * acc) * (sc * gs) = sc^2 * (silu(acc) * gs)
+    bb.put(240, pad2(_np(sd[f"{p}.combined_linear_1.weight"]), 32, 128) / (sc * sc))
     bb.put(248, pad2(_np(sd[f"{p}.combined_linear_2.weight"]), 128, 32))
     w, b = lin(sd, nbr) if nbr else (np.zeros((128, 128)), np.zeros(128))
     bb.put(256, w)
     bb.putv(0, b)
     mat, vec = bb.finish()
     emb = _np(sd[f"{p}.node_embedding.weight"])
-    pos_src = torch.from_numpy(emb @ wc0[:, 0:128].T).to(torch.float32)
-    pos_dst = torch.from_numpy(emb @ wc0[:, 128:256].T).to(torch.float32)
+    pos_src = torch.from_numpy(emb @ wc0[:, 0:128].T * sc).to(torch.float32)
+    pos_dst = torch.from_numpy(emb @ wc0[:, 128:256].T * sc).to(torch.float32)
     return mat, vec, pos_src, pos_dst
 
 
@@ -210,10 +224,11 @@ def edge_blob(sd, li, final, dtype, cfg: GeoTConfig, conf_only=False, c=None):
         bb = BlobBuilder(dtype, EL_NBLK_CONF, ELV_N_CONF)
     else:
         bb = BlobBuilder(dtype, EL_NBLK_FINAL if final else EL_NBLK, ELV_N_FINAL if final else ELV_N)
+    sc = _l2e(dtype)  # log2-unit SiLU: downward_proj, ResBlock layers 0-1, edge FFN (silu2)
     two = lambda a, b: _np(sd[f"{c}.{a}.weight"]) @ _np(sd[f"{c}.{b}.weight"])  # noqa: E731
     mg = np.zeros((320, 32))
     mg[0:128] = _geo_rows(two("dist_linear_1", "dist_linear_0"), "dist")
-    mg[128:192] = _geo_rows(two("dir_linear_1", "dir_linear_0"), "dir")
+    mg[128:192] = _geo_rows(two("dir_linear_1", "dir_linear_0"), "dir") / sc  # gate x 1/sc
     mg[192:256] = _geo_rows(two("orient_linear_1", "orient_linear_0"), "orient")
     mg[256:320] = _geo_rows(two("amide_linear_1", "amide_linear_0"), "amide")
     fg = np.zeros((128, 32))
@@ -221,8 +236,8 @@ def edge_blob(sd, li, final, dtype, cfg: GeoTConfig, conf_only=False, c=None):
                        ("orient", "final_orient_linear"), ("amide", "final_amide_linear")):
         fg += _geo_rows(_np(sd[f"{c}.{name}.weight"]), kind)
     bb.put(0, mg)
-    bb.put(20, _np(sd[f"{c}.downward_proj.weight"]))
-    bb.put(36, _np(sd[f"{c}.upward_proj.weight"]))
+    bb.put(20, _np(sd[f"{c}.downward_proj.weight"]) * sc)
+    bb.put(36, _np(sd[f"{c}.upward_proj.weight"]) * sc)  # silu2, ln2 folded into the bias add
     w, b = lin(sd, f"{c}.orig_msg_linear")
     bb.put(52, w)
     bb.putv(0, b)
@@ -234,15 +249,17 @@ def edge_blob(sd, li, final, dtype, cfg: GeoTConfig, conf_only=False, c=None):
             for l in (0, 3, 6):
                 w, b = lin(sd, f"{r}.{l}")
                 w, b = fold_bn_after(w, b, s, t)
-                bb.put(84 + 32 * i, w)
-                bb.putv(128 + 128 * i, b)
+                w_in = 1.0 if l == 0 else 1.0 / sc   # input in log2 units after layers 0 and 3
+                w_out = sc                           # every layer feeds silu2 (layer 6: ln2 in the residual fma)
+                bb.put(84 + 32 * i, w * (w_in * w_out))
+                bb.putv(128 + 128 * i, b * w_out)
                 i += 1
-    w, b = lin(sd, f"{c}.res_connect_linear")
-    bb.put(468, w)
-    bb.putv(1664, b)
-    w, b = lin(sd, f"{c}.final_linear")
-    bb.put(500, w)
-    bb.putv(1792, b)
+    w, b = lin(sd, f"{c}.res_connect_linear")  # silu2, ln2 folded into the residual fma
+    bb.put(468, w * sc)
+    bb.putv(1664, b * sc)
+    w, b = lin(sd, f"{c}.final_linear")  # silu2, ln2 folded into the residual fma
+    bb.put(500, w * sc)
+    bb.putv(1792, b * sc)
     bb.put(532, fg)
     if conf_only:
         return bb.finish()
@@ -256,10 +273,10 @@ def edge_blob(sd, li, final, dtype, cfg: GeoTConfig, conf_only=False, c=None):
         bb.putv(2048, b)
         s, t = bn_affine(sd, f"{p}.batch_norm2_edge_feats")
         w1, b1 = fold_bn_before(*lin(sd, f"{p}.edge_feats_MLP.0"), s, t)
-        bb.put(604, w1[:128])
-        bb.put(636, w1[128:])
-        bb.putv(2176, b1)
-        w2 = _np(sd[f"{p}.edge_feats_MLP.3.weight"])
+        bb.put(604, w1[:128] * sc)
+        bb.put(636, w1[128:] * sc)
+        bb.putv(2176, b1 * sc)
+        w2 = _np(sd[f"{p}.edge_feats_MLP.3.weight"]) / sc
         bb.put(668, w2[:, :128])
         bb.put(700, w2[:, 128:])
         w, b = lin(sd, f"gnn_module.0.gt_block.{li + 1}.conformation_module.nbr_linear")
@@ -275,11 +292,12 @@ def node_blob(sd, li, final, dtype):
     bb.put(0, w)
     bb.putv(0, b)
     s, t = bn_affine(sd, f"{p}.batch_norm2_node_feats")
+    sc = _l2e(dtype)  # log2-unit SiLU in the node FFN (silu2)
     w1, b1 = fold_bn_before(*lin(sd, f"{p}.node_feats_MLP.0"), s, t)
-    bb.put(32, w1[:128])
-    bb.put(64, w1[128:])
-    bb.putv(128, b1)
-    w2 = _np(sd[f"{p}.node_feats_MLP.3.weight"])
+    bb.put(32, w1[:128] * sc)
+    bb.put(64, w1[128:] * sc)
+    bb.putv(128, b1 * sc)
+    w2 = _np(sd[f"{p}.node_feats_MLP.3.weight"]) / sc
     bb.put(96, w2[:, :128])
     bb.put(128, w2[:, 128:])
     if not final:

@@ -26,9 +26,16 @@ def silu(x):
     return x / (1.0 + np.exp(-x))
 
 
+def silu2(x):
+    """log2-unit SiLU of the bf16 kernels (csrc/common.h): x * sigmoid(x * ln 2)."""
+    return x / (1.0 + np.exp2(-x))
+
+
 class Emu:
     def __init__(self, packed: packing.PackedGeoT):
         self.p, self.dt = packed, packed.dtype
+        self.s2 = silu2 if packed.dtype == "bf16" else silu
+        self.u = np.log(2.0) if packed.dtype == "bf16" else 1.0  # silu = silu2 * u
 
     def M(self, blob, off, nout, kin):
         return _unpack(blob[0], off, nout // 16, kin // 32, self.dt)
@@ -52,13 +59,14 @@ class Emu:
         ib = p.init
         pos = np.arange(N)  # per-chain graph
         acc = p.pos_src.numpy()[pos[src]] + p.pos_dst.numpy()[pos[dst]]
+        s2 = self.s2
         for t in range(5):
             y = G @ self.M(ib, 40 * t, 128, 32).T
             if t > 0:
-                y = silu(y)
+                y = s2(y)
             acc = acc + y @ self.M(ib, 40 * t + 8, 128, 128).T
-        c = silu(acc)
-        gs = sum((G @ self.M(ib, 200 + 8 * t, 128, 32).T) if t == 0 else silu(G @ self.M(ib, 200 + 8 * t, 128, 32).T)
+        c = s2(acc)
+        gs = sum((G @ self.M(ib, 200 + 8 * t, 128, 32).T) if t == 0 else s2(G @ self.M(ib, 200 + 8 * t, 128, 32).T)
                  for t in range(5))
         c = c * gs
         z = c @ self.M(ib, 240, 32, 128).T
@@ -78,18 +86,19 @@ class Emu:
             s = 0
             for j in range(4):
                 x = Fn[nbr[:, j]] * dg
-                s = s + silu(x @ Wd.T) * gate
-            x = silu(s @ self.M(eb, 36, 128, 64).T) + V[0:128] + F @ self.M(eb, 52, 128, 128).T
+                s = s + s2(x @ Wd.T) * gate
+            u = self.u
+            x = u * s2(s @ self.M(eb, 36, 128, 64).T) + V[0:128] + F @ self.M(eb, 52, 128, 128).T
             for rb in range(4):
                 if rb == 2:
-                    x = F + silu(x @ self.M(eb, 468, 128, 128).T + V[1664:1792])
+                    x = F + u * s2(x @ self.M(eb, 468, 128, 128).T + V[1664:1792])
                 y = x
                 for l in range(3):
                     i = 3 * rb + l
-                    y = silu(y @ self.M(eb, 84 + 32 * i, 128, 128).T + V[128 + 128 * i:256 + 128 * i])
-                x = x + y
+                    y = s2(y @ self.M(eb, 84 + 32 * i, 128, 128).T + V[128 + 128 * i:256 + 128 * i])
+                x = x + u * y
             x = x * (G @ fgm.T)
-            conf = F + silu(x @ self.M(eb, 500, 128, 128).T + V[1792:1920])
+            conf = F + u * s2(x @ self.M(eb, 500, 128, 128).T + V[1792:1920])
             P = conf @ self.M(eb, 540, 128, 128).T + V[1920:2048]
             sc = np.clip(qkv[src, 128:256] * qkv[dst, 0:128] / np.sqrt(32), -5, 5) * P
             alpha = np.exp(np.clip(sc.reshape(E, 4, 32).sum(-1), -5, 5))
@@ -97,7 +106,7 @@ class Emu:
                 e1 = F + sc @ self.M(eb, 572, 128, 128).T + V[2048:2176]
                 o = 0
                 for half in range(2):
-                    t_ = silu(e1 @ self.M(eb, 604 + 32 * half, 128, 128).T + V[2176 + 128 * half:2304 + 128 * half])
+                    t_ = s2(e1 @ self.M(eb, 604 + 32 * half, 128, 128).T + V[2176 + 128 * half:2304 + 128 * half])
                     o = o + t_ @ self.M(eb, 668 + 32 * half, 128, 128).T
                 F_next = e1 + o
                 Fn = silu(F_next @ self.M(eb, 732, 128, 128).T + V[2432:2560])
@@ -112,7 +121,7 @@ class Emu:
             n = h + hatt @ self.M(nb, 0, 128, 128).T + NV[0:128]
             o = 0
             for half in range(2):
-                t_ = silu(n @ self.M(nb, 32 + 32 * half, 128, 128).T + NV[128 + 128 * half:256 + 128 * half])
+                t_ = s2(n @ self.M(nb, 32 + 32 * half, 128, 128).T + NV[128 + 128 * half:256 + 128 * half])
                 o = o + t_ @ self.M(nb, 96 + 32 * half, 128, 128).T
             h = n + o
             if not final:

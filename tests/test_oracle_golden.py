@@ -88,3 +88,16 @@ def test_packed_blob_emulation_matches_reference(sd):
     h, e = Emu(PackedGeoT(sd, "f32")).geot(it)
     assert rel_max(h, z["g1_node_out"]) < 1e-5
     assert rel_max(e, z["g1_edge_out"]) < 1e-5
+
+
+def test_packed_bf16_blob_emulation_log2_units(sd):
+    """bf16 blobs carry the log2-unit SiLU scaling (packing.L2E; csrc/common.h silu2): replayed in
+    float64 with the kernels' silu2 they reproduce the reference up to bf16 weight rounding."""
+    from blob_emulator import Emu
+    from deepinteract_amd.packing import PackedGeoT
+    z = load_case("tiny")
+    it = chain_item(z, "g1")
+    h, e = Emu(PackedGeoT(sd, "bf16")).geot(it)
+    assert rel_max(h, z["g1_node_out"]) < 2e-2
+    assert rel_max(e, z["g1_edge_out"]) < 2e-2
+
