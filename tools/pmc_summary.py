@@ -18,9 +18,9 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 NAMES = {
-    "k_node_embed": "node_embed", "k_init_edge": "init_edge", "k_edge_layer<di::BF16T, false>": "edge_layer",
-    "k_edge_layer<di::BF16T, true>": "edge_layer_final", "k_node_layer<di::BF16T, false>": "node_layer",
-    "k_node_layer<di::BF16T, true>": "node_layer_final", "k_pair_tensor": "pair_tensor",
+    "k_node_embed": "node_embed", "k_init_edge": "init_edge", "k_edge_layer<di::BF16T, 0>": "edge_layer",
+    "k_edge_layer<di::BF16T, 1>": "edge_layer_final", "k_node_layer<di::BF16T, false>": "node_layer",
+    "k_node_layer<di::BF16T, true>": "node_layer_final", "k_pair_tensor": "pair_tensor", "k_pair_rows": "pair_tensor",
     "k_knn": "knn", "k_geo_feats": "geo_feats", "k_geo_stats": "geo_stats", "k_nbr_ids": "nbr_ids",
 }
 
@@ -32,14 +32,16 @@ def bench_name(kernel):
     return None
 
 
-def main(tag, src=os.path.join(ROOT, "gpurun_out")):
+def main(tag, src=os.path.join(ROOT, "gpurun_out"), prefix="prof", traffic_json=True):
     prof = os.path.join(ROOT, "profiles")
     os.makedirs(prof, exist_ok=True)
-    shutil.copy(os.path.join(src, "prof_stats", "run_kernel_stats.csv"), os.path.join(prof, f"{tag}_kernel_stats.csv"))
+    stats = os.path.join(src, f"{prefix}_stats", "run_kernel_stats.csv")
+    if os.path.exists(stats):
+        shutil.copy(stats, os.path.join(prof, f"{tag}_kernel_stats.csv"))
     agg = collections.defaultdict(dict)
     for kind, counter in (("fetch", "FETCH_SIZE"), ("write", "WRITE_SIZE")):
         vals = collections.defaultdict(list)
-        for r in csv.DictReader(open(os.path.join(src, f"prof_{kind}", "run_counter_collection.csv"))):
+        for r in csv.DictReader(open(os.path.join(src, f"{prefix}_{kind}", "run_counter_collection.csv"))):
             if r["Counter_Name"] == counter:
                 vals[r["Kernel_Name"]].append(float(r["Counter_Value"]))
         for k, v in vals.items():
@@ -55,10 +57,13 @@ def main(tag, src=os.path.join(ROOT, "gpurun_out")):
             name = bench_name(k)
             if name:
                 traffic[name] = {"hbm_bytes_per_launch": hbm, "fetch_kib": f, "write_kib": wr, "source": f"{tag}_pmc.csv"}
-    with open(os.path.join(prof, "pmc_traffic.json"), "w") as fh:
-        json.dump(traffic, fh, indent=1)
+    if traffic_json:
+        with open(os.path.join(prof, "pmc_traffic.json"), "w") as fh:
+            json.dump(traffic, fh, indent=1)
     print(json.dumps(traffic, indent=1))
 
 
 if __name__ == "__main__":
-    main(sys.argv[1] if len(sys.argv) > 1 else "r1")
+    # usage: pmc_summary.py <tag> [<prefix> [--no-traffic-json]]
+    a = sys.argv[1:]
+    main(a[0] if a else "r1", prefix=a[1] if len(a) > 1 else "prof", traffic_json="--no-traffic-json" not in a)
