@@ -201,3 +201,65 @@ class PairTensorOp:
         views = [out[o:o + 2 * hidden * l1 * l2].view(1, 2 * hidden, l1, l2)
                  for o, l1, l2 in zip(offs, l1s, l2s)]
         return out, views
+
+
+class HeadPrologueOp:
+    """ELU(InstanceNorm2d(conv2d_1(T))) of the contact head for a batch of complexes, with the
+    pair tensor T never materialised (di_head_prologue): the 1x1 conv of the
+    outer concat separates per chain and the InstanceNorm statistics are analytic. Output: the
+    head body's input, [1, C, L1, L2] per complex, in the dtype of h."""
+
+    def __init__(self, conv_w, conv_b, in_gamma, in_beta, eps=1e-6, device="cuda"):
+        self.lib = _lib.load()
+        self.device = torch.device(device)
+        f = lambda t: t.detach().to(self.device, torch.float32).contiguous()  # noqa: E731
+        self.w = f(conv_w).reshape(conv_w.shape[0], -1)  # [C, 2H(,1,1)] -> [C, 2H]
+        self.b, self.g, self.beta = f(conv_b), f(in_gamma), f(in_beta)
+        self.eps = float(eps)
+        self.channels = self.w.shape[0]
+        self._desc_cache = {}
+
+    @classmethod
+    def from_head(cls, head, device="cuda"):
+        """From a ResNet2DInputWithOptAttention (conv2d_1 + inorm_1)."""
+        return cls(head.conv2d_1.weight, head.conv2d_1.bias, head.inorm_1.weight, head.inorm_1.bias,
+                   head.inorm_1.eps, device)
+
+    def __call__(self, h, h1_rows, h2_rows, l1s, l2s, out=None, events=None):
+        hidden, C = h.shape[1], self.channels
+        if h.dtype not in (torch.float32, torch.bfloat16):
+            raise TypeError(h.dtype)
+        if self.w.shape[1] != 2 * hidden:
+            raise ValueError(f"conv2d_1 expects {self.w.shape[1]} input channels, h gives 2x{hidden}")
+        dt = _lib.DI_BF16 if h.dtype == torch.bfloat16 else _lib.DI_F32
+        # descriptors with out_off in units of the [C, L1, L2] output
+        key = ("prologue", tuple(h1_rows), tuple(h2_rows), tuple(l1s), tuple(l2s), C)
+        if key not in self._desc_cache:
+            arr = (_lib.DiPairDesc * len(l1s))()
+            off, offs = 0, []
+            for i, (a, b, l1, l2) in enumerate(zip(h1_rows, h2_rows, l1s, l2s)):
+                arr[i] = _lib.DiPairDesc(a, b, off, l1, l2)
+                offs.append(off)
+                off += C * l1 * l2
+            t = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8).to(self.device)
+            self._desc_cache[key] = (t, offs, off)
+        d, offs, total = self._desc_cache[key]
+        if out is None:
+            out = torch.empty(total, dtype=h.dtype, device=h.device)
+        elif out.numel() < total or out.dtype != h.dtype:
+            raise ValueError("head-prologue output buffer too small or of the wrong dtype")
+        m1, m2 = max(l1s), max(l2s)
+        nbytes = self.lib.di_head_prologue_work_bytes(len(l1s), m1, m2, C)
+        work = torch.empty((nbytes + 3) // 4, dtype=torch.float32, device=h.device)
+        vec = 16 // h.element_size()
+        aligned = out.data_ptr() % 16 == 0 and all(l2 % vec == 0 for l2 in l2s) and all(o % vec == 0 for o in offs)
+        tick = _Ticker(events)
+        tick("head_prologue")
+        _lib.check(self.lib.di_head_prologue(dt, _ptr(d), len(l1s), m1, m2, hidden, C, int(aligned),
+                                             _ptr(h.contiguous()), _ptr(self.w), _ptr(self.b), _ptr(self.g),
+                                             _ptr(self.beta), self.eps, _ptr(work), _ptr(out), _stream()),
+                   "di_head_prologue")
+        tick(None)
+        views = [out[o:o + C * l1 * l2].view(1, C, l1, l2) for o, l1, l2 in zip(offs, l1s, l2s)]
+        return out, views
+

@@ -73,7 +73,11 @@ class ResNet2DInputWithOptAttention(nn.Module):
         self.phase2_conv = nn.Conv2d(num_channels, num_classes, 1)
 
     def forward(self, t):
-        x = F.elu(self.inorm_1(self.conv2d_1(t)))
+        return self.body(F.elu(self.inorm_1(self.conv2d_1(t))))
+
+    def body(self, x):
+        """Everything after the prologue ELU(inorm_1(conv2d_1(t))) (which HeadPrologueOp fuses
+        with the pair tensor on HIP)."""
         x = F.elu(self.base_resnet(x))
         x = F.elu(self.phase2_resnet(x))
         return self.phase2_conv(x)

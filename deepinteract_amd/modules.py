@@ -20,7 +20,7 @@ import torch
 import torch.nn as nn
 
 from .config import GeoTConfig, NODE_COUNT_LIMIT, RESIDUE_COUNT_LIMIT
-from .engine import GeoTEngine, PairTensorOp
+from .engine import GeoTEngine, HeadPrologueOp, PairTensorOp
 from .graph import GraphBatch, ResidueGraph, batch as batch_graphs, unbatch
 from .head import ResNet2DInputWithOptAttention, contact_probs
 
@@ -78,7 +78,8 @@ class LitGINI(nn.Module):
     def __init__(self, num_node_input_feats=113, num_gnn_layers=2, num_gnn_hidden_channels=128,
                  num_gnn_attention_heads=4, knn=20, num_interact_layers=14, num_interact_hidden_channels=128,
                  num_classes=2, max_num_graph_nodes=NODE_COUNT_LIMIT, max_num_residues=RESIDUE_COUNT_LIMIT,
-                 dtype="f32", head_dtype=torch.float32, precise_head=False, **kwargs):
+                 dtype="f32", head_dtype=torch.float32, precise_head=False, fuse_head_prologue=False,
+                 **kwargs):
         super().__init__()
         self.cfg = GeoTConfig(num_node_input_feats=num_node_input_feats, num_gnn_layers=num_gnn_layers,
                               num_gnn_hidden_channels=num_gnn_hidden_channels,
@@ -91,6 +92,10 @@ class LitGINI(nn.Module):
         # FFT variants drift ~1e-3 relative over the 58 residual blocks); GEMM-based fp32 convs
         # keep logits within 1e-4 of the reference CPU path.
         self.precise_head = precise_head
+        # fuse_head_prologue: ELU(inorm_1(conv2d_1(T))) straight from the node features on HIP
+        # (di_head_prologue), never materialising the [2H, L1, L2] pair tensor T
+        self.fuse_head_prologue = fuse_head_prologue
+        self.prologue_op = None
         self.max_num_residues = max_num_residues
         self.interact_module = ResNet2DInputWithOptAttention(num_interact_layers, 2 * num_gnn_hidden_channels,
                                                              num_interact_hidden_channels, num_classes)
@@ -103,6 +108,8 @@ class LitGINI(nn.Module):
         dev = next(self.interact_module.parameters()).device
         self.engine = GeoTEngine(sd, self.dtype, self.cfg, device=dev)
         self.pair_op = PairTensorOp(dev)
+        if self.fuse_head_prologue:
+            self.prologue_op = HeadPrologueOp.from_head(self.interact_module, dev)
         return self
 
     # --- reference API ------------------------------------------------------------------
@@ -115,12 +122,15 @@ class LitGINI(nn.Module):
         graph.ndata["f"], graph.edata["f"] = h, e
         return [h[a:b] for a, b in zip(gb.node_off[:-1], gb.node_off[1:])]
 
-    def interact_forward(self, interact_tensor):
+    def interact_forward(self, interact_tensor, prologue_done=False):
+        """Head on an interaction tensor; prologue_done: the input is already
+        ELU(inorm_1(conv2d_1(T))) (HeadPrologueOp)."""
         x = interact_tensor.to(self.head_dtype)
+        fn = self.interact_module.body if prologue_done else self.interact_module
         if self.precise_head:
             with torch.backends.cudnn.flags(enabled=False):
-                return self.interact_module(x)
-        return self.interact_module(x)
+                return fn(x)
+        return fn(x)
 
     def shared_step(self, graph1, graph2, return_representations=False):
         g1s, g2s = _graph_list(graph1), _graph_list(graph2)
@@ -147,8 +157,12 @@ class LitGINI(nn.Module):
         h2r = [off[b] for _, b in pairs]
         l1 = [gb.nodes_per_graph[a] for a, _ in pairs]
         l2 = [gb.nodes_per_graph[b] for _, b in pairs]
-        _, views = self.pair_op(h, h1r, h2r, l1, l2, hT=self.engine.last_hT)
-        logits = [self.interact_forward(v) for v in views]
+        if self.prologue_op is not None:
+            _, views = self.prologue_op(h, h1r, h2r, l1, l2)
+            logits = [self.interact_forward(v, prologue_done=True) for v in views]
+        else:
+            _, views = self.pair_op(h, h1r, h2r, l1, l2, hT=self.engine.last_hT)
+            logits = [self.interact_forward(v) for v in views]
         return logits, h, e
 
     def predict_batch(self, gb: GraphBatch, pairs):

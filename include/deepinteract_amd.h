@@ -16,6 +16,8 @@
  *   di_node_layer   send_and_recv(u_mul_e/copy_e, sum) gSpMM         deepinteract_modules.py:93-96,116
  *                   + O_node / node FFN                               deepinteract_modules.py:696-723, 923-943
  *   di_pair_tensor  construct_interact_tensor (pad=False)            deepinteract_utils.py:158-172
+ *   di_head_prologue  ELU(inorm_1(conv2d_1(T))) of the head, T never materialised
+ *                                                                    deepinteract_modules.py:1181-1184, 1228-1232
  *   di_knn_topk     dgl.knn_graph + topk(pairwise_squared_distance)  graph_utils.py:107-108
  *   di_geo_feats    GeometricProteinFeatures('full') + edge/node feature assembly
  *                                                                    protein_feature_utils.py:322-377,
@@ -111,6 +113,21 @@ int di_pair_config(int32_t blocks, int32_t waves_per_block, int32_t kernel);
 int di_pair_tensor(di_dtype dt, const di_pair_desc* descs /*device [B]*/, int32_t num_complexes,
                    int32_t max_l1, int32_t max_l2, int32_t hidden, int32_t aligned16, const void* h,
                    const void* hT, int32_t num_rows, void* out, void* stream);
+
+/* Fused head prologue: x = ELU(InstanceNorm2d(conv2d_1(T))) of the contact
+ * head (ResNet2DInputWithOptAttention.forward, deepinteract_modules.py:1181-1184, 1228-1232) for a
+ * batch of complexes WITHOUT materialising the pair tensor T: the 1x1 conv of the outer concat
+ * separates into W[:, :H] h1[i] + W[:, H:] h2[j] + b and the InstanceNorm statistics of that
+ * separable sum are analytic. h: [rows, hidden] node features in `dt` (16-B aligned, hidden a
+ * multiple of 8, <= 256); conv_w [channels, 2*hidden], conv_b, in_gamma, in_beta [channels] fp32;
+ * work: device scratch of di_head_prologue_work_bytes() bytes; out: per complex [channels, L1, L2]
+ * in `dt` at descs[i].out_off (elements). aligned16: every L2 and out_off a multiple of 16 bytes
+ * of `dt` (row-streaming store kernel). */
+int di_head_prologue(di_dtype dt, const di_pair_desc* descs /*device [B]*/, int32_t num_complexes, int32_t max_l1,
+                     int32_t max_l2, int32_t hidden, int32_t channels, int32_t aligned16, const void* h,
+                     const float* conv_w, const float* conv_b, const float* in_gamma, const float* in_beta,
+                     float eps, float* work, void* out, void* stream);
+int64_t di_head_prologue_work_bytes(int32_t num_complexes, int32_t max_l1, int32_t max_l2, int32_t channels);
 
 /* ---- graph builder ----------------------------------------------------------------------- */
 /* Cα kNN per chain: idx_out [Nt,k] chain-local neighbour ids (ascending squared distance,

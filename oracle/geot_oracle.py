@@ -348,10 +348,17 @@ def _resnet(x, sd, prefix, mname, chunks, inorm, extra):
     return x
 
 
+def head_prologue(sd, t):
+    """First line of ResNet2DInputWithOptAttention.forward (deepinteract_modules.py:1231-1232):
+    ELU(inorm_1(conv2d_1(t))) on the materialised pair tensor t."""
+    p = "interact_module"
+    return F.elu(_inorm(_conv(t, sd, f"{p}.conv2d_1"), sd, f"{p}.inorm_1"))
+
+
 def head_forward(sd, t, num_chunks=14):
     """ResNet2DInputWithOptAttention.forward (deepinteract_modules.py:1228-1248), no attention."""
     p = "interact_module"
-    x = F.elu(_inorm(_conv(t, sd, f"{p}.conv2d_1"), sd, f"{p}.inorm_1"))
+    x = head_prologue(sd, t)
     x = F.elu(_resnet(x, sd, f"{p}.base_resnet", "base_resnet", num_chunks, True, False))
     x = F.elu(_resnet(x, sd, f"{p}.phase2_resnet", "bin_resnet", 1, False, True))
     return _conv(x, sd, f"{p}.phase2_conv")

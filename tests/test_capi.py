@@ -41,6 +41,15 @@ def test_invalid_arguments_rejected_without_gpu():
     assert lib.di_pair_config(-1, 4, 0) == -1 and lib.di_pair_config(0, 17, 0) == -1
     assert lib.di_pair_config(0, 0, 3) == -1
     assert lib.di_pair_config(0, 0, 0) == 0  # keeps the current launch shape
+    assert lib.di_head_prologue(0, None, 1, 8, 8, 128, 128, 1, None, None, None, None, None, 1e-6,
+                                None, None, None) == -1
+
+
+def test_head_prologue_work_bytes():
+    lib = _lib.load()
+    # per (complex, channel): a', b', e^a', e^b' fp32 tables + one int32 flag
+    assert lib.di_head_prologue_work_bytes(8, 1000, 900, 128) == 8 * 128 * (2 * 1900 * 4 + 4)
+    assert lib.di_head_prologue_work_bytes(0, 10, 10, 128) == 0
 
 
 def test_ctypes_struct_layouts():
