@@ -16,6 +16,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -131,6 +132,51 @@ def cpu_baseline(n_res, k, sample, threads):
     return sample / dt, dt
 
 
+def head_prologue_record(h1r, h2r, l1, l2, gb, eng, dev, tdt, reps=5):
+    """Supplementary, outside the metric: the head's first line
+    ELU(inorm_1(conv2d_1(T))) for one micro-batch, fused on HIP from the GeoT node features
+    (di_head_prologue; T never materialised). Algorithmic bytes = the [128, L1, L2] output."""
+    from deepinteract_amd.engine import HeadPrologueOp
+    g = torch.Generator().manual_seed(7)
+    C = 128
+    w = torch.randn(C, 2 * H, 1, 1, generator=g) / math.sqrt(2 * H)
+    op = HeadPrologueOp(w, 0.1 * torch.randn(C, generator=g), 1 + 0.1 * torch.randn(C, generator=g),
+                        0.1 * torch.randn(C, generator=g), 1e-6, dev)
+    h, _ = eng.forward(gb, clone=False)
+    out = torch.empty(sum(C * a * b for a, b in zip(l1, l2)), dtype=tdt, device=dev)
+    ev = {}
+    op(h, h1r, h2r, l1, l2, out=out)
+    torch.cuda.synchronize()
+    for _ in range(reps):
+        op(h, h1r, h2r, l1, l2, out=out, events=ev)
+    torch.cuda.synchronize()
+    us = float(np.mean([s.elapsed_time(e) for s, e in ev["head_prologue"]])) * 1e3
+    byts = out.numel() * out.element_size()
+    return {"op": "ELU(inorm_1(conv2d_1(T))), T never materialised", "complexes": len(l1), "avg_us": round(us, 1),
+            "gbs": round(byts / us / 1e3, 1), "frac_hbm": round(byts / us / 1e3 / HBM_PEAK_GBS, 4),
+            "bytes_per_launch": byts}
+
+
+def allgather_record(ws, complexes, n_res, dev, reps=3):
+    """Supplementary, outside the metric: the one RCCL all-gather of fp32 contact
+    maps ([L1, L2] per complex, every rank's complexes to every rank), timed after the metric."""
+    import torch.distributed as dist
+    per_rank = complexes * n_res * n_res
+    send = torch.zeros(per_rank, dtype=torch.float32, device=dev)
+    recv = torch.empty(per_rank * ws, dtype=torch.float32, device=dev)
+    dist.all_gather_into_tensor(recv, send)
+    torch.cuda.synchronize()
+    barrier(ws)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        dist.all_gather_into_tensor(recv, send)
+    torch.cuda.synchronize()
+    dt = max_over_ranks(ws, (time.perf_counter() - t0) / reps)
+    del send, recv
+    return {"bytes_per_rank": per_rank * 4, "ms": round(dt * 1e3, 3),
+            "algbw_GBs": round(per_rank * 4 * (ws - 1) / dt / 1e9, 1), "collective": "all_gather_into_tensor (RCCL)"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -144,6 +190,7 @@ def main():
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
     ap.add_argument("--cpu-sample", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-prologue", action="store_true", help="skip the supplementary fused-head-prologue line")
     ap.add_argument("--pair-cus", type=int, default=0,
                     help="K > 0: pair tensor on a CU-masked stream of K dedicated CUs (K blocks x 8 waves), "
                          "GeoT on the other CUs (needs --overlap 1)")
@@ -152,6 +199,8 @@ def main():
                     help="aligned pair-tensor kernel (default: rows alone, vector beside GeoT)")
     ap.add_argument("--pair-blocks", type=int, default=0)
     ap.add_argument("--pair-waves", type=int, default=0)
+    ap.add_argument("--pair-pace", type=int, default=None,
+                    help="store-rate pacing of the pair kernel: s_sleep(1) per row / vector trip")
     ap.add_argument("--overlap", type=int, default=1, choices=[0, 1, 2],
                     help="0: one stream; 1: pair tensor of micro-batch m-1 on its own stream beside GeoT of m; "
                          "2: as 1, started after InitEdge of m")
@@ -177,7 +226,8 @@ def main():
             raise SystemExit("--pair-cus needs --overlap 1 or 2")
         pair = PairTensorOp(dev, blocks=args.pair_cus, waves_per_block=8, kernel=args.pair_kernel)
     else:
-        pair = PairTensorOp(dev, blocks=args.pair_blocks, waves_per_block=args.pair_waves, kernel=args.pair_kernel)
+        pair = PairTensorOp(dev, blocks=args.pair_blocks, waves_per_block=args.pair_waves, kernel=args.pair_kernel,
+                            pace=args.pair_pace)
 
     # ---- inputs: a pool of distinct complexes built on the device (kNN + features + ids) ----
     P = min(args.pool, args.complexes)
@@ -265,6 +315,10 @@ def main():
     elapsed = time.perf_counter() - t0
     elapsed = max_over_ranks(ws, elapsed)
     total = args.complexes * args.steps * ws
+
+    # ---- supplementary (outside the metric): fused head prologue, contact-map all-gather ----
+    prologue = head_prologue_record(h1r, h2r, l1, l2, mbs[-1], eng, dev, tdt) if not args.no_prologue else None
+    gather = allgather_record(ws, args.complexes, n_res, dev) if ws > 1 else None
     value = total / elapsed
 
     # ---- per-kernel timing (HIP events on the launch stream, inside the timed region) -------
@@ -307,12 +361,17 @@ def main():
                                "GeoT || pair-tensor (2 HIP streams, pair after InitEdge)"][args.overlap]
                    + (f"; pair on {args.pair_cus} dedicated CUs ({args.cu_layout}), GeoT on "
                       f"{num_cus - args.pair_cus}" if args.pair_cus else "")
-                   + f"; pair kernel {args.pair_kernel}"},
+                   + f"; pair kernel {args.pair_kernel}"
+                   + (f", pace {args.pair_pace}" if args.pair_pace else "")},
         "hbm_frac_of_peak": round(hbm_frac, 4),
         "roofline": roof,
         "kernels": {n: {kk: round(v, 3) if isinstance(v, float) else v for kk, v in r.items()} for n, r in kern.items()},
         "builder": {"complexes": P, "build_s": round(t_build, 4), "synth_host_s": round(t_synth, 3)},
     }
+    if prologue is not None:
+        out["head_prologue"] = prologue
+    if gather is not None:
+        out["contact_map_allgather"] = gather
     if rank == 0 and ws == 1 and not args.no_cpu:
         threads = min(16, os.cpu_count() or 1)
         cps, dt = cpu_baseline(n_res, k, args.cpu_sample, threads)

@@ -42,6 +42,7 @@ _SIGS = {
     "di_node_layer": ([ctypes.POINTER(DiGraph), _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P], ctypes.c_int),
     "di_pair_tensor": ([_I, _P, _I, _I, _I, _I, _I, _P, _P, _I, _P, _P], ctypes.c_int),
     "di_pair_config": ([_I, _I, _I], ctypes.c_int),
+    "di_pair_pace": ([_I], ctypes.c_int),
     "di_head_prologue": ([_I, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, ctypes.c_float, _P, _P, _P],
                          ctypes.c_int),
     "di_head_prologue_work_bytes": ([_I, _I, _I, _I], ctypes.c_int64),

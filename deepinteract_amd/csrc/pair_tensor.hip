@@ -60,7 +60,7 @@ template <typename T, bool ALIGNED>
 __global__ __launch_bounds__(PAIR_THREADS) void k_pair_tensor(const di_pair_desc* __restrict__ descs, int hidden,
                                                             const T* __restrict__ h, const T* __restrict__ hT,
                                                             int nrows, int chunks, int items,
-                                                            T* __restrict__ out) {
+                                                            T* __restrict__ out, int pace) {
   using V = typename Vec16<T>::V;
   constexpr int VEC = Vec16<T>::N;
   for (int item = blockIdx.x; item < items; item += gridDim.x) {
@@ -118,6 +118,7 @@ __global__ __launch_bounds__(PAIR_THREADS) void k_pair_tensor(const di_pair_desc
 #endif
           }
         }
+        for (int t = 0; t < pace; ++t) __builtin_amdgcn_s_sleep(1);  // store-rate pacing (di_pair_pace)
       }
     } else {
       for (uint32_t q = q_begin + threadIdx.x; q < q_end; q += PAIR_THREADS) {
@@ -146,7 +147,7 @@ constexpr int PAIR_SEG = 128;  // 16-B chunks per row segment (2 per lane)
 template <typename T>
 __global__ __launch_bounds__(1024) __attribute__((amdgpu_num_vgpr(32)))
 void k_pair_rows(const di_pair_desc* __restrict__ descs, int hidden, const T* __restrict__ h,
-                 const T* __restrict__ hT, int nrows, int rblocks, int items, T* __restrict__ out) {
+                 const T* __restrict__ hT, int nrows, int rblocks, int items, T* __restrict__ out, int pace) {
   using V = typename Vec16<T>::V;
   constexpr int VEC = Vec16<T>::N;
   const int PAIR_ROWS = (int)blockDim.x;  // rows per work item: 64 per wave
@@ -195,6 +196,7 @@ void k_pair_rows(const di_pair_desc* __restrict__ descs, int hidden, const T* __
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uintx4, v0), r, k0 * 16, soff, DI_PAIR_STORE);
         if (two && k1 < nch)
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uintx4, v1), r, k1 * 16, soff, DI_PAIR_STORE);
+        for (int t = 0; t < pace; ++t) __builtin_amdgcn_s_sleep(1);  // store-rate pacing (di_pair_pace)
       }
     }
   }
@@ -213,6 +215,16 @@ static int env_int(const char* name, int dflt) {
 static int g_pair_blocks = env_int("DI_PAIR_BLOCKS", PAIR_MAX_BLOCKS);
 static int g_pair_waves = env_int("DI_PAIR_WAVES", 4);
 static int g_pair_kernel = env_int("DI_PAIR_KERNEL", 1);  // 1 row-streaming, 2 per-vector (aligned path)
+static int g_pair_pace = env_int("DI_PAIR_PACE", 0);      // s_sleep(1) (~64 clk) per row / per trip of stores
+
+// Store-rate pacing of the aligned pair kernels when they share the GPU with GeoT: each wave
+// sleeps `pace` x 64 clocks after every row (row kernel) or every PAIR_UNROLL-vector trip
+// (vector kernel), so the store stream leaves the memory pipeline headroom for GeoT's loads.
+extern "C" int di_pair_pace(int32_t pace) {
+  if (pace < 0 || pace > 1000) return DI_EINVAL;
+  g_pair_pace = pace;
+  return DI_OK;
+}
 
 extern "C" int di_pair_config(int32_t blocks, int32_t waves_per_block, int32_t kernel) {
   if (blocks < 0 || waves_per_block < 0 || waves_per_block > 16 || kernel < 0 || kernel > 2) return DI_EINVAL;
@@ -249,10 +261,10 @@ extern "C" int di_pair_tensor(di_dtype dt, const di_pair_desc* descs, int32_t nu
     const unsigned rgrid = (unsigned)(ritems < max_blocks ? ritems : max_blocks);
     if (dt == DI_BF16)
       hipLaunchKernelGGL((k_pair_rows<u16>), dim3(rgrid), dim3(rows), 0, s, descs, hidden, (const u16*)h,
-                         (const u16*)hT, num_rows, rblocks, ritems, (u16*)out);
+                         (const u16*)hT, num_rows, rblocks, ritems, (u16*)out, g_pair_pace);
     else
       hipLaunchKernelGGL((k_pair_rows<float>), dim3(rgrid), dim3(rows), 0, s, descs, hidden,
-                         (const float*)h, (const float*)hT, num_rows, rblocks, ritems, (float*)out);
+                         (const float*)h, (const float*)hT, num_rows, rblocks, ritems, (float*)out, g_pair_pace);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? DI_OK : (int)e;
   }
@@ -260,17 +272,17 @@ extern "C" int di_pair_tensor(di_dtype dt, const di_pair_desc* descs, int32_t nu
   if (dt == DI_BF16) {
     if (aligned16)
       hipLaunchKernelGGL((k_pair_tensor<u16, true>), dim3(grid), dim3(PAIR_THREADS), 0, s, descs, hidden,
-                         (const u16*)h, (const u16*)hT, num_rows, chunks, items, (u16*)out);
+                         (const u16*)h, (const u16*)hT, num_rows, chunks, items, (u16*)out, g_pair_pace);
     else
       hipLaunchKernelGGL((k_pair_tensor<u16, false>), dim3(grid), dim3(PAIR_THREADS), 0, s, descs, hidden,
-                         (const u16*)h, (const u16*)hT, num_rows, chunks, items, (u16*)out);
+                         (const u16*)h, (const u16*)hT, num_rows, chunks, items, (u16*)out, g_pair_pace);
   } else {
     if (aligned16)
       hipLaunchKernelGGL((k_pair_tensor<float, true>), dim3(grid), dim3(PAIR_THREADS), 0, s, descs, hidden,
-                         (const float*)h, (const float*)hT, num_rows, chunks, items, (float*)out);
+                         (const float*)h, (const float*)hT, num_rows, chunks, items, (float*)out, g_pair_pace);
     else
       hipLaunchKernelGGL((k_pair_tensor<float, false>), dim3(grid), dim3(PAIR_THREADS), 0, s, descs, hidden,
-                         (const float*)h, (const float*)hT, num_rows, chunks, items, (float*)out);
+                         (const float*)h, (const float*)hT, num_rows, chunks, items, (float*)out, g_pair_pace);
   }
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? DI_OK : (int)e;

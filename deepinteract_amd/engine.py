@@ -150,15 +150,19 @@ class PairTensorOp:
 
     KERNELS = {"rows": 1, "vector": 2}
 
-    def __init__(self, device="cuda", blocks: int = 0, waves_per_block: int = 0, kernel: str | None = None):
+    def __init__(self, device="cuda", blocks: int = 0, waves_per_block: int = 0, kernel: str | None = None,
+                 pace: int | None = None):
         """blocks / waves_per_block / kernel ("rows" | "vector"): launch shape and kernel of the
-        16-B-aligned path (di_pair_config; 0 / None keep the library's current setting)."""
+        16-B-aligned path (di_pair_config; 0 / None keep the library's current setting); pace:
+        store-rate pacing, s_sleep(1) per row / vector trip (di_pair_pace; None keeps it)."""
         self.lib = _lib.load()
         self.device = torch.device(device)
         self._desc_cache = {}
         k = self.KERNELS[kernel] if kernel else 0
         if (blocks or waves_per_block or k) and hasattr(self.lib, "di_pair_config"):
             _lib.check(self.lib.di_pair_config(blocks, waves_per_block, k), "di_pair_config")
+        if pace is not None:
+            _lib.check(self.lib.di_pair_pace(int(pace)), "di_pair_pace")
 
     def descs(self, h1_rows, h2_rows, l1s, l2s, hidden):
         key = (tuple(h1_rows), tuple(h2_rows), tuple(l1s), tuple(l2s), hidden)

@@ -112,6 +112,43 @@ class LitGINI(nn.Module):
             self.prologue_op = HeadPrologueOp.from_head(self.interact_module, dev)
         return self
 
+    @classmethod
+    def load_from_checkpoint(cls, checkpoint_path, map_location=None, strict=True, safe_globals=None, **kwargs):
+        """LightningModule.load_from_checkpoint as lit_model_predict.py:214-219 calls it: build the
+        network from the checkpoint's hyper-parameters (shapes inferred from the state dict where
+        absent) and load its ``state_dict``. ``kwargs`` override hyper-parameters; the reference's
+        training-only overrides (use_wandb_logger, batch_size, lr, weight_decay, dropout_rate) are
+        accepted and have no effect on inference. The file is read with ``torch.load(weights_only=
+        True)`` (``weights.read_checkpoint``). strict: every key this build needs must be present
+        with its shape; keys outside node_in_embedding / gnn_module / interact_module are ignored."""
+        from .weights import check_state_dict, infer_config, read_checkpoint
+        sd, arch = read_checkpoint(checkpoint_path, safe_globals=safe_globals)
+        net_prefixes = ("node_in_embedding.", "gnn_module.", "interact_module.")
+        sd = type(sd)((k, v) for k, v in sd.items() if k.startswith(net_prefixes))
+        arch.update({k: v for k, v in kwargs.items() if k in arch or k.startswith("num_") or k == "knn"})
+        cfg = infer_config(sd, **arch)
+        problems = check_state_dict(sd, cfg)
+        if strict and problems:
+            raise RuntimeError(f"{checkpoint_path}: state dict does not match LitGINI ({len(problems)} problems): "
+                               + "; ".join(problems[:8]))
+        opts = {k: kwargs[k] for k in ("dtype", "head_dtype", "precise_head", "fuse_head_prologue") if k in kwargs}
+        model = cls(num_node_input_feats=cfg.num_node_input_feats, num_gnn_layers=cfg.num_gnn_layers,
+                    num_gnn_hidden_channels=cfg.num_gnn_hidden_channels,
+                    num_gnn_attention_heads=cfg.num_gnn_attention_heads, knn=cfg.knn,
+                    num_interact_layers=cfg.num_interact_layers,
+                    num_interact_hidden_channels=cfg.num_interact_hidden_channels, num_classes=cfg.num_classes,
+                    max_num_graph_nodes=cfg.node_count_limit,
+                    max_num_residues=int(arch.get("max_num_residues", RESIDUE_COUNT_LIMIT)), **opts)
+        if map_location is not None:
+            model = model.to(map_location)
+        return model.eval().load_reference_state_dict(sd)
+
+    def freeze(self):
+        """LightningModule.freeze (lit_model_predict.py:220): eval mode, no gradients."""
+        for p in self.parameters():
+            p.requires_grad_(False)
+        return self.eval()
+
     # --- reference API ------------------------------------------------------------------
     def gnn_forward(self, graph):
         """node_in_embedding + GeoT for a (batched) graph; returns per-graph node features and

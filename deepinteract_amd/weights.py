@@ -14,6 +14,7 @@ from __future__ import annotations
 
 import hashlib
 import math
+import re
 import zlib
 from collections import OrderedDict
 
@@ -207,3 +208,61 @@ def state_dict_sha256(sd) -> str:
         h.update(k.encode())
         h.update(sd[k].detach().cpu().contiguous().numpy().tobytes())
     return h.hexdigest()
+
+
+# hyper-parameters of the reference LitGINI (deepinteract_modules.py:1481-1489) that shape the
+# inference network; everything else in a checkpoint's hyper_parameters (optimiser, logging,
+# training flags) has no effect on predict.
+_ARCH_HPARAMS = ("num_node_input_feats", "num_gnn_layers", "num_gnn_hidden_channels", "num_gnn_attention_heads",
+                 "knn", "num_interact_layers", "num_interact_hidden_channels", "num_classes",
+                 "max_num_graph_nodes", "max_num_residues")
+
+
+def read_checkpoint(path, safe_globals=None):
+    """A PyTorch-Lightning checkpoint of the reference LitGINI (as lit_model_predict.py:214 loads
+    it) -> (state_dict, architecture hparams). Loaded with ``torch.load(weights_only=True)``
+    only: nothing in the file is executed. The reference saves ``gnn_activ_fn=nn.SiLU()`` among
+    its hyper-parameters, so ``torch.nn.SiLU`` is allow-listed for the weights-only unpickler;
+    a file that needs any other global is refused (extract its ``state_dict`` first)."""
+    allowed = [torch.nn.SiLU] + list(safe_globals or [])
+    with torch.serialization.safe_globals(allowed):
+        ckpt = torch.load(path, map_location="cpu", weights_only=True)
+    if isinstance(ckpt, dict) and "state_dict" in ckpt:
+        sd, hp = ckpt["state_dict"], dict(ckpt.get("hyper_parameters") or {})
+    elif isinstance(ckpt, dict) and all(isinstance(v, torch.Tensor) for v in ckpt.values()):
+        sd, hp = ckpt, {}  # a bare state dict
+    else:
+        raise ValueError(f"{path}: neither a Lightning checkpoint nor a state dict")
+    arch = {k: hp[k] for k in _ARCH_HPARAMS if k in hp and isinstance(hp[k], (int, float))}
+    return OrderedDict((k, v) for k, v in sd.items()), arch
+
+
+def infer_config(sd, **overrides) -> GeoTConfig:
+    """GeoTConfig from a reference-keyed state dict's shapes (node_in_embedding, gt_block count,
+    base_resnet chunk count), overridden by explicit hyper-parameters."""
+    w = sd["node_in_embedding.weight"]
+    layers = {int(k.split(".")[3]) for k in sd if k.startswith("gnn_module.0.gt_block.")}
+    pat = re.compile(r"^interact_module\.base_resnet\.resnet_base_resnet_(\d+)_(?:1|2|4|8)_")
+    chunks = {int(m.group(1)) for m in map(pat.match, sd) if m}
+    kw = dict(num_node_input_feats=int(w.shape[1]), num_gnn_hidden_channels=int(w.shape[0]),
+              num_gnn_layers=len(layers) or GeoTConfig().num_gnn_layers)
+    if chunks:
+        kw["num_interact_layers"] = max(chunks) + 1
+    for k in ("num_gnn_attention_heads", "knn", "num_interact_hidden_channels", "num_classes",
+              "num_node_input_feats", "num_gnn_layers", "num_gnn_hidden_channels", "num_interact_layers"):
+        if k in overrides:
+            kw[k] = int(overrides[k])
+    if "max_num_graph_nodes" in overrides:
+        kw["node_count_limit"] = int(overrides["max_num_graph_nodes"])
+    return GeoTConfig(**kw)
+
+
+def check_state_dict(sd, cfg: GeoTConfig, with_head: bool = True):
+    """Strict key / shape check of a reference-keyed state dict against this build's layout
+    (geot_keys + head_keys). Returns the list of problems (empty when it matches)."""
+    want = {k: shape for k, shape, _ in geot_keys(cfg) + (head_keys(cfg) if with_head else [])}
+    problems = [f"missing {k}" for k in want if k not in sd]
+    problems += [f"unexpected {k}" for k in sd if k not in want]
+    problems += [f"shape {k}: {tuple(sd[k].shape)} != {tuple(s)}" for k, s in want.items()
+                 if k in sd and tuple(sd[k].shape) != tuple(s)]
+    return problems

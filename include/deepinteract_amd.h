@@ -109,6 +109,10 @@ int di_node_layer(const di_graph* g, di_dtype dt, int final_layer, const float* 
  * 1 (env DI_PAIR_BLOCKS / DI_PAIR_WAVES / DI_PAIR_KERNEL). Not a reference interface: a
  * scheduling knob of this build. */
 int di_pair_config(int32_t blocks, int32_t waves_per_block, int32_t kernel);
+/* Store-rate pacing of the aligned pair kernels (scheduling knob, not a reference interface):
+ * every wave sleeps pace x ~64 clocks after each row (row kernel) / vector trip (vector kernel),
+ * leaving the memory pipeline headroom for a concurrent GeoT stream. Default 0 (env DI_PAIR_PACE). */
+int di_pair_pace(int32_t pace);
 
 int di_pair_tensor(di_dtype dt, const di_pair_desc* descs /*device [B]*/, int32_t num_complexes,
                    int32_t max_l1, int32_t max_l2, int32_t hidden, int32_t aligned16, const void* h,

@@ -104,3 +104,24 @@ def test_fused_prologue_end_to_end_logits(case):
     torch.cuda.synchronize()
     assert rel_max(logits[0].cpu().numpy(), z["logits"]) < 1e-4
     assert rel_max(probs[0].cpu().numpy(), z["probs"]) < 1e-4
+
+
+def test_load_from_checkpoint_end_to_end_logits(tmp_path):
+    """LitGINI.load_from_checkpoint on a Lightning-format file (weights-only read) reproduces the
+    golden logits made by the reference's code from the same seeded weights."""
+    import os
+    from deepinteract_amd.graph import GraphBatch
+    from deepinteract_amd.modules import LitGINI
+    from deepinteract_amd.weights import seeded_state_dict
+    z = load_case("tiny")
+    p = os.path.join(tmp_path, "LitGINI.ckpt")
+    torch.save({"state_dict": seeded_state_dict(0),
+                "hyper_parameters": {"gnn_activ_fn": torch.nn.SiLU(), "num_gnn_layers": 2, "knn": 20}}, p)
+    model = LitGINI.load_from_checkpoint(p, map_location="cuda", use_wandb_logger=False, batch_size=1,
+                                         precise_head=True).freeze()
+    gb = GraphBatch.from_arrays([chain_item(z, "g1"), chain_item(z, "g2")], "cuda")
+    with torch.no_grad():
+        logits, probs = model.predict_batch(gb, [(0, 1)])
+    torch.cuda.synchronize()
+    assert rel_max(logits[0].cpu().numpy(), z["logits"]) < 1e-4
+    assert rel_max(probs[0].cpu().numpy(), z["probs"]) < 1e-4
