@@ -75,6 +75,16 @@ struct NodeArgs {
   void* qkv_out;
 };
 
+// Wave priority of the GeoT kernels (s_setprio at entry; 0 = hardware default, no instruction):
+// beside the pair-tensor store stream (priority 0) the GeoT waves win every issue tie.
+#ifndef DI_GEOT_PRIO
+#define DI_GEOT_PRIO 0
+#endif
+#define DI_GEOT_ENTRY() \
+  do {                                                              \
+    if (DI_GEOT_PRIO > 0) __builtin_amdgcn_s_setprio(DI_GEOT_PRIO); \
+  } while (0)
+
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 template <int NW>
 __device__ __forceinline__ int row_id() {
@@ -137,6 +147,7 @@ struct FRow<F32T> {
 template <class DT>
 __global__ __launch_bounds__(THREADS) void k_node_embed(EmbedArgs a) {
   using T = typename DT::T;
+  DI_GEOT_ENTRY();
   __shared__ __attribute__((aligned(16))) T lds[2 * MAT128 * BLK];
   const int lane = lane_id(), g = lane >> 4;
   const int r = row_id<WAVES>();
@@ -178,6 +189,7 @@ template <class DT>
 __global__ __attribute__((amdgpu_flat_work_group_size(1, 64 * DI_GEO_NW), amdgpu_waves_per_eu(2, 2)))
 void k_init_edge(InitArgs a) {
   using T = typename DT::T;
+  DI_GEOT_ENTRY();
   using G = Geo<DT>;
   constexpr bool FAST = DT::kBF16;
   constexpr int CAP = G::CAP;
@@ -365,6 +377,21 @@ __device__ __forceinline__ int tile_edge(int tile, int Et, bool& valid) {
   return valid ? r : Et - 1;
 }
 
+// XCD-aware tile order for the one-tile-per-block grid (8 * ceil(T/8) blocks). The dispatcher
+// deals workgroups round-robin over the 8 XCDs (block b -> XCD b % 8), each with its own L2, so
+// block b takes tile (b % 8) * ceil(T/8) + b / 8: every XCD walks one contiguous eighth of the
+// edge array, and the neighbour-edge rows a tile gathers (Fn rows of sequence/space-near nodes,
+// the dst node's own rows in the adjacent tile) are mostly already in that XCD's L2.
+#ifndef DI_XCD_TILES
+#define DI_XCD_TILES 0
+#endif
+__host__ __device__ inline int xcd_grid(int ntiles) { return DI_XCD_TILES ? 8 * ((ntiles + 7) / 8) : ntiles; }
+__device__ __forceinline__ int xcd_tile(int b, int ntiles) {
+  if (!DI_XCD_TILES) return b;
+  const int q = (ntiles + 7) >> 3;
+  return (b & 7) * q + (b >> 3);
+}
+
 // Two 4-wave blocks per CU, each wave capped at 240 VGPRs (amdgpu_num_vgpr counts the unified
 // VGPR+AGPR file in pairs on gfx950): 2 x 240 + 32 = 512 leaves one pair-tensor wave per SIMD
 // co-resident, so the HBM-bound pair stores run under the MFMA/VALU-bound edge layers.
@@ -375,6 +402,7 @@ template <class DT, int MODE>
 __global__ __attribute__((amdgpu_flat_work_group_size(1, 512), amdgpu_waves_per_eu(2, 2), amdgpu_num_vgpr(120)))
 void k_edge_layer(EdgeArgs a) {
   constexpr bool FINAL = MODE == 1, CONF = MODE == 2;
+  DI_GEOT_ENTRY();
   using T = typename DT::T;
   using G = EdgeGeo<DT>;
   constexpr bool FAST = DT::kBF16;
@@ -384,6 +412,10 @@ void k_edge_layer(EdgeArgs a) {
   const T* W = reinterpret_cast<const T*>(a.wmat);
   const T* fn_in = reinterpret_cast<const T*>(a.fn_in);
   const T* qkv = reinterpret_cast<const T*>(a.qkv);
+
+  // first tile: XCD-aware when every block owns one tile; persistent grids stride by gridDim.x
+  const int first = (int)gridDim.x >= ntiles ? xcd_tile(blockIdx.x, ntiles) : (int)blockIdx.x;
+  if (first >= ntiles) return;  // padding block of the XCD-aware grid (uniform, before any DMA)
 
   EdgePipe<DT> pipe(lds);
   DmaPump* PP = pipe.pump_ptr();
@@ -399,13 +431,13 @@ void k_edge_layer(EdgeArgs a) {
   EdgeIn<DT> in;
   {
     bool v0;
-    const int e0 = tile_edge<DT>(blockIdx.x, a.Et, v0);
+    const int e0 = tile_edge<DT>(first, a.Et, v0);
     in.load_ids(a, e0);
     in.load_rest(a, e0, g);
   }
 
 #pragma unroll 1
-  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+  for (int tile = first; tile < ntiles; tile += gridDim.x) {
     bool valid;
     const int e = tile_edge<DT>(tile, a.Et, valid);
     const bool more = tile + (int)gridDim.x < ntiles;
@@ -592,6 +624,7 @@ void k_edge_layer(EdgeArgs a) {
 template <class DT, bool FINAL>
 __global__ __launch_bounds__(THREADS, 2) void k_node_layer(NodeArgs a) {
   using T = typename DT::T;
+  DI_GEOT_ENTRY();
   constexpr bool FAST = DT::kBF16;
   constexpr bool DB = DT::kBF16;
   __shared__ __attribute__((aligned(16))) T lds[(DB ? 2 : 1) * MAT128 * BLK];
@@ -760,12 +793,12 @@ extern "C" int di_edge_layer(const di_graph* g, di_dtype dt, int final_layer, co
 #define DI_EDGE_PERSIST 0
 #endif
     const int tiles = grid_rows(a.Et, EdgeGeo<BF16T>::ROWS);
-    const int resident = DI_EDGE_PERSIST ? (EdgeGeo<BF16T>::PP ? 1 : 2) * num_cus() : tiles;
-    dim3 grid(tiles < resident ? tiles : resident), block(EdgeGeo<BF16T>::THREADS);
+    const int resident = DI_EDGE_PERSIST ? (EdgeGeo<BF16T>::PP ? 1 : 2) * num_cus() : xcd_grid(tiles);
+    dim3 grid(DI_EDGE_PERSIST && tiles > resident ? resident : xcd_grid(tiles)), block(EdgeGeo<BF16T>::THREADS);
     if (final_layer) hipLaunchKernelGGL((k_edge_layer<BF16T, 1>), grid, block, 0, s, a);
     else hipLaunchKernelGGL((k_edge_layer<BF16T, 0>), grid, block, 0, s, a);
   } else {
-    dim3 grid(grid_rows(a.Et, Geo<F32T>::ROWS)), block(Geo<F32T>::THREADS);
+    dim3 grid(xcd_grid(grid_rows(a.Et, EdgeGeo<F32T>::ROWS))), block(EdgeGeo<F32T>::THREADS);
     if (final_layer) hipLaunchKernelGGL((k_edge_layer<F32T, 1>), grid, block, 0, s, a);
     else hipLaunchKernelGGL((k_edge_layer<F32T, 0>), grid, block, 0, s, a);
   }
@@ -780,10 +813,10 @@ extern "C" int di_conformation(const di_graph* g, di_dtype dt, const float* edge
              conf_out, nullptr};
   hipStream_t s = (hipStream_t)stream;
   if (dt == DI_BF16) {
-    dim3 grid(grid_rows(a.Et, EdgeGeo<BF16T>::ROWS)), block(EdgeGeo<BF16T>::THREADS);
+    dim3 grid(xcd_grid(grid_rows(a.Et, EdgeGeo<BF16T>::ROWS))), block(EdgeGeo<BF16T>::THREADS);
     hipLaunchKernelGGL((k_edge_layer<BF16T, 2>), grid, block, 0, s, a);
   } else {
-    dim3 grid(grid_rows(a.Et, EdgeGeo<F32T>::ROWS)), block(EdgeGeo<F32T>::THREADS);
+    dim3 grid(xcd_grid(grid_rows(a.Et, EdgeGeo<F32T>::ROWS))), block(EdgeGeo<F32T>::THREADS);
     hipLaunchKernelGGL((k_edge_layer<F32T, 2>), grid, block, 0, s, a);
   }
   return launch_status();

@@ -47,6 +47,10 @@ VARIANTS = {
     "nw8_nodma_nobar": ["DI_GEO_NW=8", "DI_X_NODMA", "DI_X_NOBAR"],
     "pair_sc1": ["DI_PAIR_STORE=16"],
     "pair_sc1nt": ["DI_PAIR_STORE=18"],
+    "xcd": ["DI_XCD_TILES=1"],
+    "prio1": ["DI_GEOT_PRIO=1"],
+    "prio3": ["DI_GEOT_PRIO=3"],
+    "persist_prio2": ["DI_EDGE_PERSIST=1", "DI_GEOT_PRIO=2"],
 }
 
 if __name__ == "__main__":
