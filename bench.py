@@ -28,6 +28,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "complexes/sec GeoT+pair-tensor fwd (2×1k res, k=20, 1/8 GPU); % HBM peak"
+METRIC_C5 = "complexes/sec GeoT+pair-tensor fwd (C5 sizing stress: 2×4k res, k=30, 4 GeoT layers)"
 HBM_PEAK_GBS = 8000.0
 MFMA_PEAK_TFLOPS = {"bf16": 2500.0, "f32": 157.3}
 # SURVEY.md §8d algorithmic MAC per unit (edge or node), per launch kind
@@ -204,7 +205,29 @@ def main():
     ap.add_argument("--overlap", type=int, default=1, choices=[0, 1, 2],
                     help="0: one stream; 1: pair tensor of micro-batch m-1 on its own stream beside GeoT of m; "
                          "2: as 1, started after InitEdge of m")
+    ap.add_argument("--config", default="c3", choices=["c3", "c5"],
+                    help="c3: the metric's workload (BASELINE configs[2]); c5: the 2x4000-residue, k=30, "
+                         "4-layer sizing stress (BASELINE configs[4]; no oracle at N > 2304)")
+    ap.add_argument("--layers", type=int, default=None, help="GeoT layers (default 2; c5: 4)")
+    ap.add_argument("--node-limit", type=int, default=None,
+                    help="max_num_graph_nodes of the synthetic model (default 2304; c5: 4096)")
     args = ap.parse_args()
+    if args.config == "c5":
+        # BASELINE.json configs[4]: 2x4000 residues, k=30, 4 GeoT layers. The reference's
+        # nn.Embedding(max_num_graph_nodes=2304) cannot index 4000 residues, so the synthetic model is
+        # built with max_num_graph_nodes=4096 (a LitGINI hyper-parameter); a [256,4000,4000] bf16
+        # pair tensor is 8.19 GB, so micro-batches of 2 complexes.
+        for key, val in (("residues", 4000), ("knn", 30), ("layers", 4), ("node_limit", 4096)):
+            if getattr(args, key) in (None, ap.get_default(key)):
+                setattr(args, key, val)
+        if args.complexes == ap.get_default("complexes"):
+            args.complexes = 32
+        if args.micro_batch == ap.get_default("micro_batch"):
+            args.micro_batch = 2
+        args.pool = min(args.pool, 2)
+        args.no_cpu = args.no_prologue = True
+    args.layers = args.layers or 2
+    args.node_limit = args.node_limit or 2304
 
     if args.pair_kernel is None:
         args.pair_kernel = "vector" if args.overlap and not args.pair_cus else "rows"
@@ -218,8 +241,10 @@ def main():
 
     n_res, k, M = args.residues, args.knn, args.micro_batch
     assert args.complexes % M == 0
-    sd = seeded_state_dict(0, with_head=False)
-    eng = GeoTEngine(sd, args.dtype, device=dev)
+    from deepinteract_amd.config import GeoTConfig
+    cfg = GeoTConfig(num_gnn_layers=args.layers, knn=k, node_count_limit=args.node_limit)
+    sd = seeded_state_dict(0, cfg, with_head=False)
+    eng = GeoTEngine(sd, args.dtype, cfg, device=dev)
     num_cus = torch.cuda.get_device_properties(dev).multi_processor_count
     if args.pair_cus:
         if not args.overlap:
@@ -240,7 +265,8 @@ def main():
     t_synth = time.perf_counter() - tb
     torch.cuda.synchronize()
     tb = time.perf_counter()
-    pool_gb = [build_graph_batch([a, b], k=k, seed=c + 1, device=dev) for c, (a, b) in enumerate(pool)]
+    pool_gb = [build_graph_batch([a, b], k=k, seed=c + 1, device=dev, node_count_limit=args.node_limit)
+               for c, (a, b) in enumerate(pool)]
     torch.cuda.synchronize()
     t_build = time.perf_counter() - tb
     # resident batch: complexes -> micro-batches (copies of pool complexes, distinct HBM buffers)
@@ -343,20 +369,25 @@ def main():
     else:
         roof = {"kernel": dom, "bound": "hbm", "achieved": round(d["gbs"], 1), "peak": HBM_PEAK_GBS, "unit": "GB/s"}
     roof["frac"] = round(roof["achieved"] / roof["peak"], 4)
-    traffic = load_pmc_traffic(dom)
+    # the committed PMC summary was collected on the default workload (C3, micro-batch 8, bf16):
+    # any other shape reports traffic null rather than borrowing those per-launch bytes
+    pmc_shape = (args.config, M, n_res, k, args.layers, args.dtype) == ("c3", 8, 1000, 20, 2, "bf16")
+    traffic = load_pmc_traffic(dom) if pmc_shape else None
     roof["traffic"] = traffic
     bytes_c = algorithmic_bytes_per_complex(n_res, n_res, k, esz)
     hbm_frac = bytes_c * value / ws / (HBM_PEAK_GBS * 1e9)
 
     out = {
-        "metric": METRIC, "value": round(value, 2), "unit": "complexes/s", "n_gpus": ws,
+        "metric": METRIC if args.config == "c3" else METRIC_C5, "value": round(value, 2), "unit": "complexes/s", "n_gpus": ws,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
         "data": "synthetic (seeded random-walk chains, on-device graph build; seeded random weights)",
-        "config": {"workload": f"C3: 2x{n_res}-residue heterodimers, k={k}, 2 GeoT layers, 128 hidden, 4 heads; "
+        "config": {"workload": f"{args.config.upper()}: 2x{n_res}-residue heterodimers, k={k}, {args.layers} GeoT "
+                               f"layers, 128 hidden, 4 heads; "
                                f"GeoT fwd (both chains) + [256,{n_res},{n_res}] pair tensor",
                    "complexes_per_gpu_per_step": args.complexes, "micro_batch": M, "residues": [n_res, n_res],
-                   "knn": k, "parallelism": f"complex-sharded dp{ws}",
+                   "knn": k, "layers": args.layers, "max_num_graph_nodes": args.node_limit,
+                   "parallelism": f"complex-sharded dp{ws}",
                    "streams": ["1 stream", "GeoT || pair-tensor (2 HIP streams)",
                                "GeoT || pair-tensor (2 HIP streams, pair after InitEdge)"][args.overlap]
                    + (f"; pair on {args.pair_cus} dedicated CUs ({args.cu_layout}), GeoT on "

@@ -16,7 +16,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from .config import GEO_NBRHD_SIZE, KNN
+from .config import GEO_NBRHD_SIZE, KNN, NODE_COUNT_LIMIT
 from .graph import GraphBatch
 
 
@@ -50,7 +50,8 @@ def knn(cas, k=KNN, device="cuda"):
     return idx, d2
 
 
-def build_graph_batch(chains, k=KNN, nb=GEO_NBRHD_SIZE, seed=0, device="cuda", return_aux=False):
+def build_graph_batch(chains, k=KNN, nb=GEO_NBRHD_SIZE, seed=0, device="cuda", return_aux=False,
+                      node_count_limit=NODE_COUNT_LIMIT):
     """Build the kernels' GraphBatch for a list of chains entirely on the device."""
     if nb != 2:
         raise NotImplementedError("geo_nbrhd_size=2 (the reference's setting, lit_model_predict.py:156)")
@@ -74,7 +75,7 @@ def build_graph_batch(chains, k=KNN, nb=GEO_NBRHD_SIZE, seed=0, device="cuda", r
     src = (idx + node_base[:, None]).reshape(-1).contiguous()
     dst = torch.arange(nt, dtype=torch.int32, device=device).repeat_interleave(k).contiguous()
     nbr = torch.empty(nt * k, 4, dtype=torch.int32, device=device)
-    gb = GraphBatch(src, dst, nbr, node_f, edge_f, sizes, [n * k for n in sizes])
+    gb = GraphBatch(src, dst, nbr, node_f, edge_f, sizes, [n * k for n in sizes], node_count_limit=node_count_limit)
     _lib.check(lib.di_build_nbr_ids(gb.num_edges, _p(gb.src), _p(gb.dst), _p(gb.in_ptr), ctypes.c_uint64(seed),
                                     _p(nbr), _stream()), "di_build_nbr_ids")
     if return_aux:

@@ -103,6 +103,10 @@ class GeoTEngine:
         after_init: optional torch.cuda.Event recorded right after the InitEdge launch (lets a
         concurrent HBM-bound consumer start once the memory-heavy prologue has passed)."""
         lib, p, dt = self.lib, self.packed, _DI_DT[self.dtype]
+        if max(gb.nodes_per_graph) > p.pos_src.shape[0]:
+            # InitEdge gathers positional rows node_pos < max_num_graph_nodes (nn.Embedding, :153, :210)
+            raise IndexError(f"chain of {max(gb.nodes_per_graph)} residues exceeds this model's "
+                             f"max_num_graph_nodes={p.pos_src.shape[0]}")
         ws = self.workspace(gb.num_nodes, gb.num_edges, slot)
         g = ctypes.byref(gb.c_graph)
         st = _stream()

@@ -121,7 +121,8 @@ class GraphBatch:
     positional-embedding row is the node's index within its own chain.
     """
 
-    def __init__(self, src, dst, nbr, node_f, edge_f, nodes_per_graph, edges_per_graph):
+    def __init__(self, src, dst, nbr, node_f, edge_f, nodes_per_graph, edges_per_graph,
+                 node_count_limit=NODE_COUNT_LIMIT):
         self.src, self.dst, self.nbr = src, dst, nbr
         self.node_f, self.edge_f = node_f, edge_f
         self.nodes_per_graph = [int(x) for x in nodes_per_graph]
@@ -129,10 +130,13 @@ class GraphBatch:
         dev = src.device
         self.num_nodes = int(sum(self.nodes_per_graph))
         self.num_edges = int(sum(self.edges_per_graph))
+        # max_num_graph_nodes of the model (LitGINI hyper-parameter, default NODE_COUNT_LIMIT = 2304):
+        # the row count of InitEdge's positional nn.Embedding
+        self.node_count_limit = int(node_count_limit)
         for n in self.nodes_per_graph:
-            if n > NODE_COUNT_LIMIT:
-                # the reference's nn.Embedding(NODE_COUNT_LIMIT) raises IndexError (:153, :210)
-                raise IndexError(f"chain of {n} residues exceeds NODE_COUNT_LIMIT={NODE_COUNT_LIMIT}")
+            if n > self.node_count_limit:
+                # the reference's nn.Embedding(max_num_graph_nodes) raises IndexError (:153, :210)
+                raise IndexError(f"chain of {n} residues exceeds NODE_COUNT_LIMIT={self.node_count_limit}")
         self.node_pos = torch.cat([torch.arange(n, dtype=torch.int32, device=dev)
                                    for n in self.nodes_per_graph])
         if self.num_edges and bool((self.dst[1:] < self.dst[:-1]).any()):
@@ -153,7 +157,7 @@ class GraphBatch:
         return self._c
 
     @classmethod
-    def from_graphs(cls, graphs, device=None):
+    def from_graphs(cls, graphs, device=None, node_count_limit=NODE_COUNT_LIMIT):
         """From ResidueGraph / DGLGraph objects carrying ndata['f'] [N,113] (raw node features),
         edata['f'] [E,28], edata['src_nbr_e_ids'|'dst_nbr_e_ids'] [E,2] (per-graph local ids)."""
         srcs, dsts, nbrs, nfs, efs, nn, ne = [], [], [], [], [], [], []
@@ -172,10 +176,10 @@ class GraphBatch:
             noff += g.num_nodes()
             eoff += g.num_edges()
         return cls(torch.cat(srcs).contiguous(), torch.cat(dsts).contiguous(), torch.cat(nbrs).contiguous(),
-                   torch.cat(nfs).contiguous(), torch.cat(efs).contiguous(), nn, ne)
+                   torch.cat(nfs).contiguous(), torch.cat(efs).contiguous(), nn, ne, node_count_limit=node_count_limit)
 
     @classmethod
-    def from_arrays(cls, items, device):
+    def from_arrays(cls, items, device, node_count_limit=NODE_COUNT_LIMIT):
         """items: dicts with num_nodes, src, dst, src_nbr, dst_nbr (local), node_f, edge_f."""
         srcs, dsts, nbrs, nfs, efs, nn, ne = [], [], [], [], [], [], []
         noff = eoff = 0
@@ -193,7 +197,7 @@ class GraphBatch:
             noff += n
             eoff += e
         cat = lambda xs: torch.cat(xs).to(device).contiguous()  # noqa: E731
-        return cls(cat(srcs), cat(dsts), cat(nbrs), cat(nfs), cat(efs), nn, ne)
+        return cls(cat(srcs), cat(dsts), cat(nbrs), cat(nfs), cat(efs), nn, ne, node_count_limit=node_count_limit)
 
 
 def concat_batches(batches: Sequence[GraphBatch]) -> GraphBatch:
@@ -211,4 +215,5 @@ def concat_batches(batches: Sequence[GraphBatch]) -> GraphBatch:
         noff += b.num_nodes
         eoff += b.num_edges
     return GraphBatch(torch.cat(srcs).contiguous(), torch.cat(dsts).contiguous(), torch.cat(nbrs).contiguous(),
-                      torch.cat(nfs).contiguous(), torch.cat(efs).contiguous(), nn, ne)
+                      torch.cat(nfs).contiguous(), torch.cat(efs).contiguous(), nn, ne,
+                      node_count_limit=max(b.node_count_limit for b in batches))

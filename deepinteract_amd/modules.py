@@ -48,8 +48,10 @@ class DGLGeometricTransformer(nn.Module):
         self.cfg = GeoTConfig(num_gnn_layers=num_layers, num_gnn_hidden_channels=num_hidden_channels,
                               num_gnn_attention_heads=num_attention_heads, knn=knn,
                               node_count_limit=node_count_limit, num_node_input_feats=num_hidden_channels)
-        if num_hidden_channels != 128 or num_attention_heads != 4 or node_count_limit != NODE_COUNT_LIMIT:
-            raise NotImplementedError("kernels are specialised for 128 hidden channels, 4 heads, 2304 nodes")
+        if num_hidden_channels != 128 or num_attention_heads != 4:
+            raise NotImplementedError("kernels are specialised for 128 hidden channels, 4 heads")
+        if not 0 < node_count_limit <= 4096:
+            raise NotImplementedError("max_num_graph_nodes above 4096 (the on-device kNN's row limit)")
         self.dtype = dtype
         self.engine = None
 
@@ -63,7 +65,8 @@ class DGLGeometricTransformer(nn.Module):
         if self.engine is None:
             raise RuntimeError("load_reference_state_dict() first")
         bnn, bne = graph.batch_num_nodes(), graph.batch_num_edges()
-        gb = GraphBatch.from_graphs(_graph_list(graph), device=self.engine.device)
+        gb = GraphBatch.from_graphs(_graph_list(graph), device=self.engine.device,
+                                     node_count_limit=self.cfg.node_count_limit)
         h, e = self.engine.forward(gb)
         graph.ndata["f"] = h.to(torch.float32) if self.dtype == "f32" else h
         graph.edata["f"] = e.to(torch.float32) if self.dtype == "f32" else e
@@ -154,7 +157,7 @@ class LitGINI(nn.Module):
         """node_in_embedding + GeoT for a (batched) graph; returns per-graph node features and
         writes ndata['f'] / edata['f'] like the reference (:1660-1679)."""
         graphs = _graph_list(graph)
-        gb = GraphBatch.from_graphs(graphs, device=self.engine.device)
+        gb = GraphBatch.from_graphs(graphs, device=self.engine.device, node_count_limit=self.cfg.node_count_limit)
         h, e = self.engine.forward(gb)
         graph.ndata["f"], graph.edata["f"] = h, e
         return [h[a:b] for a, b in zip(gb.node_off[:-1], gb.node_off[1:])]
@@ -171,7 +174,8 @@ class LitGINI(nn.Module):
 
     def shared_step(self, graph1, graph2, return_representations=False):
         g1s, g2s = _graph_list(graph1), _graph_list(graph2)
-        gb = GraphBatch.from_graphs(g1s + g2s, device=self.engine.device)
+        gb = GraphBatch.from_graphs(g1s + g2s, device=self.engine.device,
+                                     node_count_limit=self.cfg.node_count_limit)
         logits_list, h, e = self._forward_batch(gb, [(i, len(g1s) + i) for i in range(len(g1s))])
         n1 = gb.node_off[len(g1s)]
         e1 = gb.edge_off[len(g1s)]

@@ -1,0 +1,68 @@
+"""BASELINE.json configs[4] (C5 sizing stress: 2x4000 residues, k=30, 4 GeoT layers) at parity-test
+scale: the same model class (4 layers, k=30, max_num_graph_nodes=4096) on a chain LONGER than the
+reference's 2304-row positional table, so InitEdge gathers positional rows >= 2304.
+
+The reference itself raises IndexError beyond 2304 residues (nn.Embedding(max_num_graph_nodes),
+deepinteract_modules.py:153, :210), so no reference-generated fixture can exist for N > 2304:
+parity here is against the CPU oracle (oracle/geot_oracle.py, the restatement pinned to the
+reference's modules at N <= 2304 by tests/test_oracle_golden.py) run with the same 4096-row
+table — "parity unpinned" beyond the oracle's own golden pinning. Graph tensors (kNN, features,
+neighbour ids) come from the oracle builder so both sides see identical inputs.
+Tolerance: fp32 <= 1e-4 relative (north_star), as in test_gpu_parity.py.
+"""
+import numpy as np
+import pytest
+import torch
+
+from gpu_common import rel_max
+
+pytestmark = pytest.mark.gpu
+
+F32_TOL = 1e-4
+
+
+def _item(g):
+    return {"num_nodes": g["num_nodes"], "src": g["src"], "dst": g["dst"], "src_nbr": g["src_nbr"],
+            "dst_nbr": g["dst_nbr"], "node_f": g["node_f"], "edge_f": g["edge_f"]}
+
+
+def test_c5_class_beyond_2304_residues():
+    import oracle.geot_oracle as O
+    from deepinteract_amd import synth
+    from deepinteract_amd.config import GeoTConfig
+    from deepinteract_amd.engine import GeoTEngine
+    from deepinteract_amd.graph import GraphBatch
+    from deepinteract_amd.weights import seeded_state_dict
+
+    cfg = GeoTConfig(num_gnn_layers=4, knn=30, node_count_limit=4096)
+    sd = seeded_state_dict(3, cfg, with_head=False)
+    ch1, ch2 = synth.synthetic_complex(5, 2400, 40)
+    torch.set_num_threads(16)
+    g1 = O.build_graph(ch1, k=30, seed=11)
+    g2 = O.build_graph(ch2, k=30, seed=12)
+    eng = GeoTEngine(sd, "f32", cfg)
+    gb = GraphBatch.from_arrays([_item(g1), _item(g2)], "cuda", node_count_limit=4096)
+    h, e = eng.forward(gb)
+    torch.cuda.synchronize()
+    h, e = h.cpu().numpy(), e.cpu().numpy()
+    n1, e1 = gb.nodes_per_graph[0], gb.edges_per_graph[0]
+    with torch.no_grad():
+        ref = [O.geot_forward(sd, g, num_layers=4) for g in (g1, g2)]
+    for (hn, en), hs, es in zip(ref, (h[:n1], h[n1:]), (e[:e1], e[e1:])):
+        assert rel_max(hs, hn.numpy()) < F32_TOL
+        assert rel_max(es, en.numpy()) < F32_TOL
+    # the rows past the reference's 2304-row table are the ones this case exists for
+    assert rel_max(h[2304:n1], ref[0][0].numpy()[2304:]) < F32_TOL
+
+
+def test_c5_class_engine_rejects_chain_beyond_its_table():
+    from deepinteract_amd import synth
+    from deepinteract_amd.builder import build_graph_batch
+    from deepinteract_amd.engine import GeoTEngine
+    from deepinteract_amd.weights import seeded_state_dict
+
+    eng = GeoTEngine(seeded_state_dict(0, with_head=False), "bf16")  # 2304-row table
+    ch1, ch2 = synth.synthetic_complex(1, 2320, 32)
+    gb = build_graph_batch([ch1, ch2], k=20, seed=1, device="cuda", node_count_limit=4096)
+    with pytest.raises(IndexError):
+        eng.forward(gb)

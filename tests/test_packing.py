@@ -137,3 +137,27 @@ def test_conformation_blob_is_edge_blob_prefix():
     nblk, nvec = packing.BLOB_SIZES[6]
     assert conf_m.numel() == nblk * 512 and conf_v.numel() == nvec
     assert torch.equal(conf_m, full_m[:nblk * 512]) and torch.equal(conf_v, full_v[:nvec])
+
+
+def test_node_count_limit_is_the_models_table_size():
+    """GraphBatch enforces the model's max_num_graph_nodes (default NODE_COUNT_LIMIT=2304, the
+    reference's IndexError), and a larger model (C5 class, 4096 rows) accepts longer chains."""
+    import pytest
+    import torch
+    from deepinteract_amd.config import NODE_COUNT_LIMIT, GeoTConfig
+    from deepinteract_amd.graph import GraphBatch
+    from deepinteract_amd.weights import seeded_state_dict
+
+    def gb(n, **kw):
+        z = torch.zeros(n, dtype=torch.int32)
+        ar = torch.arange(n, dtype=torch.int32)
+        return GraphBatch(z, ar, torch.zeros(n, 4, dtype=torch.int32), None, None, [n], [n], **kw)
+
+    assert NODE_COUNT_LIMIT == 2304
+    gb(2304)
+    with pytest.raises(IndexError):
+        gb(2305)
+    assert gb(4000, node_count_limit=4096).node_count_limit == 4096
+    sd = seeded_state_dict(0, GeoTConfig(num_gnn_layers=4, knn=30, node_count_limit=4096), with_head=False)
+    assert sd["gnn_module.0.init_edge_module.node_embedding.weight"].shape == (4096, 128)
+    assert any(k.startswith("gnn_module.0.gt_block.3.") for k in sd)
