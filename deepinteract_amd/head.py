@@ -6,9 +6,71 @@ of the default model (``use_interact_attention=False``) and is not implemented.
 """
 from __future__ import annotations
 
+import ctypes
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
+
+
+class HeadNormOps:
+    """The head's HBM-bound passes on HIP (csrc/head_ops.hip): ELU(InstanceNorm2d(x))
+    in 3 plane passes instead of torch's 5, and SEBlock gate + residual add in 3 instead of 5.
+    Inputs: one [1, C, H, W] NCHW-contiguous image, fp32 or bf16, on the GPU. No CPU fallback:
+    constructing it without the HIP library / a GPU raises."""
+
+    def __init__(self, device):
+        from . import _lib
+        if not torch.cuda.is_available():
+            raise RuntimeError("HeadNormOps needs a ROCm GPU (no CPU fallback)")
+        self._lib = _lib
+        self.lib = _lib.load()
+        self.device = torch.device(device)
+        self._work = None
+
+    def _dt(self, x):
+        if x.dtype == torch.float32:
+            return self._lib.DI_F32
+        if x.dtype == torch.bfloat16:
+            return self._lib.DI_BF16
+        raise TypeError(f"head ops take fp32 / bf16, got {x.dtype}")
+
+    @staticmethod
+    def _check(x):
+        if x.dim() != 4 or x.shape[0] != 1 or not x.is_contiguous() or not x.is_cuda:
+            raise ValueError("head ops take one contiguous NCHW [1, C, H, W] GPU image")
+
+    def _stream(self):
+        return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+    def inorm_elu(self, x, norm: nn.InstanceNorm2d, out=None):
+        """F.elu(norm(x)); out may be x (in place)."""
+        self._check(x)
+        C, hw = x.shape[1], x.shape[2] * x.shape[3]
+        y = torch.empty_like(x) if out is None else out
+        nb = self.lib.di_inorm_work_bytes(C, hw)
+        if self._work is None or self._work.numel() * 8 < nb:
+            self._work = torch.empty((nb + 7) // 8, dtype=torch.float64, device=x.device)
+        g = norm.weight.detach().float().contiguous()
+        b = norm.bias.detach().float().contiguous()
+        self._lib.check(self.lib.di_inorm_elu(self._dt(x), ctypes.c_void_p(x.data_ptr()), C, hw,
+                                              ctypes.c_void_p(g.data_ptr()), ctypes.c_void_p(b.data_ptr()),
+                                              ctypes.c_float(norm.eps), ctypes.c_void_p(self._work.data_ptr()),
+                                              ctypes.c_void_p(y.data_ptr()), self._stream()), "di_inorm_elu")
+        return y
+
+    def se_scale_add(self, x, scale, res, out=None):
+        """x * scale[None, :, None, None] + res; out may be x or res (in place)."""
+        self._check(x)
+        self._check(res)
+        C, hw = x.shape[1], x.shape[2] * x.shape[3]
+        s = scale.detach().reshape(-1).float().contiguous()
+        y = torch.empty_like(x) if out is None else out
+        self._lib.check(self.lib.di_se_scale_add(self._dt(x), ctypes.c_void_p(x.data_ptr()),
+                                                 ctypes.c_void_p(s.data_ptr()), ctypes.c_void_p(res.data_ptr()),
+                                                 C, hw, ctypes.c_void_p(y.data_ptr()), self._stream()),
+                        "di_se_scale_add")
+        return y
 
 
 class SEBlock(nn.Module):
@@ -17,10 +79,12 @@ class SEBlock(nn.Module):
         self.linear1 = nn.Linear(ch, ch // ratio)
         self.linear2 = nn.Linear(ch // ratio, ch)
 
-    def forward(self, x):
+    def gate(self, x):
         s = x.mean(dim=(2, 3))
-        s = torch.sigmoid(F.relu(self.linear2(F.relu(self.linear1(s)))))
-        return x * s[:, :, None, None]
+        return torch.sigmoid(F.relu(self.linear2(F.relu(self.linear1(s)))))
+
+    def forward(self, x):
+        return x * self.gate(x)[:, :, None, None]
 
 
 class ResNet(nn.Module):
@@ -29,6 +93,7 @@ class ResNet(nn.Module):
         super().__init__()
         self.module_name, self.inorm = module_name, inorm
         self.initial_projection = initial_projection
+        self.ops = None  # HeadNormOps: fused norm/ELU and SE/residual passes on HIP
         C = num_channels
         self.blocks = []
         if initial_projection:
@@ -52,13 +117,22 @@ class ResNet(nn.Module):
         m = self._modules
         if self.initial_projection:
             x = m[f"resnet_{self.module_name}_init_proj"](x)
+        ops = self.ops
         for r in self.blocks:
             res = x
             for i in (1, 2, 3):
-                if self.inorm:
-                    x = m[f"{r}_inorm_{i}"](x)
-                x = m[f"{r}_conv2d_{i}"](F.elu(x))
-            x = m[f"{r}_se_block"](x) + res
+                if self.inorm and ops is not None:
+                    x = ops.inorm_elu(x, m[f"{r}_inorm_{i}"], out=None if i == 1 else x)
+                else:
+                    if self.inorm:
+                        x = m[f"{r}_inorm_{i}"](x)
+                    x = F.elu(x)
+                x = m[f"{r}_conv2d_{i}"](x)
+            se = m[f"{r}_se_block"]
+            if ops is not None:
+                x = ops.se_scale_add(x, se.gate(x), res, out=x)
+            else:
+                x = se(x) + res
         return x
 
 
@@ -71,9 +145,18 @@ class ResNet2DInputWithOptAttention(nn.Module):
         self.phase2_resnet = ResNet(num_channels, 1, "bin_resnet", inorm=False, initial_projection=True,
                                     extra_blocks=True)
         self.phase2_conv = nn.Conv2d(num_channels, num_classes, 1)
+        self.ops = None
+
+    def use_hip_norm_ops(self, ops):
+        """Route the InstanceNorm+ELU and SE+residual passes through HeadNormOps (or None: torch)."""
+        self.ops = self.base_resnet.ops = self.phase2_resnet.ops = ops
+        return self
 
     def forward(self, t):
-        return self.body(F.elu(self.inorm_1(self.conv2d_1(t))))
+        x = self.conv2d_1(t)
+        if getattr(self, "ops", None) is not None:
+            return self.body(self.ops.inorm_elu(x, self.inorm_1, out=x))
+        return self.body(F.elu(self.inorm_1(x)))
 
     def body(self, x):
         """Everything after the prologue ELU(inorm_1(conv2d_1(t))) (which HeadPrologueOp fuses

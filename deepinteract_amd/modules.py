@@ -22,7 +22,7 @@ import torch.nn as nn
 from .config import GeoTConfig, NODE_COUNT_LIMIT, RESIDUE_COUNT_LIMIT
 from .engine import GeoTEngine, HeadPrologueOp, PairTensorOp
 from .graph import GraphBatch, ResidueGraph, batch as batch_graphs, unbatch
-from .head import ResNet2DInputWithOptAttention, contact_probs
+from .head import HeadNormOps, ResNet2DInputWithOptAttention, contact_probs
 
 
 def _identity_embedding_sd(sd, cfg: GeoTConfig):
@@ -82,7 +82,7 @@ class LitGINI(nn.Module):
                  num_gnn_attention_heads=4, knn=20, num_interact_layers=14, num_interact_hidden_channels=128,
                  num_classes=2, max_num_graph_nodes=NODE_COUNT_LIMIT, max_num_residues=RESIDUE_COUNT_LIMIT,
                  dtype="f32", head_dtype=torch.float32, precise_head=False, fuse_head_prologue=False,
-                 **kwargs):
+                 head_channels_last=False, head_hip_ops=True, **kwargs):
         super().__init__()
         self.cfg = GeoTConfig(num_node_input_feats=num_node_input_feats, num_gnn_layers=num_gnn_layers,
                               num_gnn_hidden_channels=num_gnn_hidden_channels,
@@ -98,6 +98,13 @@ class LitGINI(nn.Module):
         # fuse_head_prologue: ELU(inorm_1(conv2d_1(T))) straight from the node features on HIP
         # (di_head_prologue), never materialising the [2H, L1, L2] pair tensor T
         self.fuse_head_prologue = fuse_head_prologue
+        # head_dtype / head_channels_last: the dilated-ResNet head's parameters and activations in
+        # head_dtype (bf16: MIOpen bf16 convolutions, fp32 accumulation) and NHWC memory layout
+        # (SURVEY §8f-3); the fp32 NCHW default is the parity configuration
+        self.head_channels_last = head_channels_last
+        # head_hip_ops: the head's InstanceNorm+ELU and SE-gate+residual passes on HIP
+        # (head.HeadNormOps; NCHW only, so not with head_channels_last)
+        self.head_hip_ops = head_hip_ops and not head_channels_last
         self.prologue_op = None
         self.max_num_residues = max_num_residues
         self.interact_module = ResNet2DInputWithOptAttention(num_interact_layers, 2 * num_gnn_hidden_channels,
@@ -112,7 +119,12 @@ class LitGINI(nn.Module):
         self.engine = GeoTEngine(sd, self.dtype, self.cfg, device=dev)
         self.pair_op = PairTensorOp(dev)
         if self.fuse_head_prologue:
-            self.prologue_op = HeadPrologueOp.from_head(self.interact_module, dev)
+            self.prologue_op = HeadPrologueOp.from_head(self.interact_module, dev)  # from the fp32 weights
+        self.interact_module.to(dtype=self.head_dtype)
+        if self.head_channels_last:
+            self.interact_module.to(memory_format=torch.channels_last)
+        if self.head_hip_ops:
+            self.interact_module.use_hip_norm_ops(HeadNormOps(dev))
         return self
 
     @classmethod
@@ -134,7 +146,8 @@ class LitGINI(nn.Module):
         if strict and problems:
             raise RuntimeError(f"{checkpoint_path}: state dict does not match LitGINI ({len(problems)} problems): "
                                + "; ".join(problems[:8]))
-        opts = {k: kwargs[k] for k in ("dtype", "head_dtype", "precise_head", "fuse_head_prologue") if k in kwargs}
+        opts = {k: kwargs[k] for k in ("dtype", "head_dtype", "precise_head", "fuse_head_prologue",
+                                       "head_channels_last", "head_hip_ops") if k in kwargs}
         model = cls(num_node_input_feats=cfg.num_node_input_feats, num_gnn_layers=cfg.num_gnn_layers,
                     num_gnn_hidden_channels=cfg.num_gnn_hidden_channels,
                     num_gnn_attention_heads=cfg.num_gnn_attention_heads, knn=cfg.knn,
@@ -166,6 +179,8 @@ class LitGINI(nn.Module):
         """Head on an interaction tensor; prologue_done: the input is already
         ELU(inorm_1(conv2d_1(T))) (HeadPrologueOp)."""
         x = interact_tensor.to(self.head_dtype)
+        if self.head_channels_last:
+            x = x.contiguous(memory_format=torch.channels_last)
         fn = self.interact_module.body if prologue_done else self.interact_module
         if self.precise_head:
             with torch.backends.cudnn.flags(enabled=False):

@@ -18,6 +18,8 @@
  *   di_pair_tensor  construct_interact_tensor (pad=False)            deepinteract_utils.py:158-172
  *   di_head_prologue  ELU(inorm_1(conv2d_1(T))) of the head, T never materialised
  *                                                                    deepinteract_modules.py:1181-1184, 1228-1232
+ *   di_inorm_elu    ELU(InstanceNorm2d(x)) of the head's ResNet blocks deepinteract_modules.py:1016-1030,1075-1095
+ *   di_se_scale_add SEBlock gate + residual add                      deepinteract_modules.py:954-970, 1095
  *   di_knn_topk     dgl.knn_graph + topk(pairwise_squared_distance)  graph_utils.py:107-108
  *   di_geo_feats    GeometricProteinFeatures('full') + edge/node feature assembly
  *                                                                    protein_feature_utils.py:322-377,
@@ -132,6 +134,21 @@ int di_head_prologue(di_dtype dt, const di_pair_desc* descs /*device [B]*/, int3
                      const float* conv_w, const float* conv_b, const float* in_gamma, const float* in_beta,
                      float eps, float* work, void* out, void* stream);
 int64_t di_head_prologue_work_bytes(int32_t num_complexes, int32_t max_l1, int32_t max_l2, int32_t channels);
+
+/* ---- contact-head body (convolutions stay on MIOpen) --------------------- */
+/* y = ELU(InstanceNorm2d(x)) of one [channels, hw] NCHW image (batch 1): biased variance, eps,
+ * affine gamma/beta [channels] fp32; fp64 statistics. Replaces the `inorm_i` + `F.elu` pair of
+ * every inorm ResNet block (ResNet.forward, deepinteract_modules.py:1075-1095; the modules
+ * :1016-1030) and of the head prologue (:1231-1232). x, y: 16-B aligned, `dt` storage (y may
+ * alias x); work: di_inorm_work_bytes() bytes of device scratch. */
+int di_inorm_elu(di_dtype dt, const void* x, int32_t channels, int64_t hw, const float* gamma,
+                 const float* beta, float eps, void* work, void* y, void* stream);
+int64_t di_inorm_work_bytes(int32_t channels, int64_t hw);
+/* y = x * scale[c] + res: SEBlock's channel gate (deepinteract_modules.py:954-970) fused with the
+ * ResNet block's residual add (:1095); x * scale is rounded to `dt` before the add, as torch does.
+ * x, res, y: [channels, hw], 16-B aligned (y may alias x or res); scale [channels] fp32. */
+int di_se_scale_add(di_dtype dt, const void* x, const float* scale, const void* res, int32_t channels,
+                    int64_t hw, void* y, void* stream);
 
 /* ---- graph builder ----------------------------------------------------------------------- */
 /* Cα kNN per chain: idx_out [Nt,k] chain-local neighbour ids (ascending squared distance,
