@@ -48,7 +48,8 @@ _SIGS = {
     "di_head_prologue_work_bytes": ([_I, _I, _I, _I], ctypes.c_int64),
     "di_inorm_elu": ([_I, _P, _I, ctypes.c_int64, _P, _P, ctypes.c_float, _P, _P, _P], ctypes.c_int),
     "di_inorm_work_bytes": ([_I, ctypes.c_int64], ctypes.c_int64),
-    "di_se_scale_add": ([_I, _P, _P, _P, _I, ctypes.c_int64, _P, _P], ctypes.c_int),
+    "di_se_scale_add": ([_I, _P, _P, _P, _P, _I, ctypes.c_int64, _P, _P], ctypes.c_int),
+    "di_channel_mean": ([_I, _P, _I, ctypes.c_int64, _P, _P, _P, _P], ctypes.c_int),
     "di_knn_topk": ([_I, _P, _P, _I, _I, _P, _P, _P], ctypes.c_int),
     "di_geo_feats": ([ctypes.POINTER(DiGeoArgs), _P], ctypes.c_int),
     "di_build_nbr_ids": ([_I, _P, _P, _P, ctypes.c_uint64, _P, _P], ctypes.c_int),

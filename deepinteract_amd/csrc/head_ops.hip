@@ -11,8 +11,11 @@
 //      k_inorm_apply  grid (split, C): every block folds its channel's partials (biased variance,
 //                     as InstanceNorm) into mean and scale = gamma / sqrt(var + eps), then streams
 //                     y = ELU((x - mean) * scale + beta) (ELU(z) = z > 0 ? z : expm1(z)).
-//  * di_se_scale_add: y = x * s[c] + res — SEBlock's channel gate (:954-970) fused with the
-//    block's residual add (:1095): 3 plane passes instead of 5.
+//  * di_se_scale_add: y = (x + b[c]) * s[c] + res — the block's last conv bias, SEBlock's channel
+//    gate (:954-970) and the residual add (:1095): 3 plane passes instead of 7.
+//  * di_channel_mean: SEBlock's x.mean(dim=(2, 3)) (+ the deferred conv bias), one read pass.
+// The convs before an InstanceNorm run without their bias (a per-channel constant cancels in
+// the normalisation exactly), so the head does no separate bias-add passes.
 // fp32 accumulation everywhere, fp64 for the statistics; bf16 storage rounds once (RNE).
 #include <hip/hip_runtime.h>
 #include <math.h>
@@ -196,12 +199,13 @@ __global__ __launch_bounds__(HO_THREADS) void k_inorm_apply(const T* __restrict_
 
 template <typename T>
 __global__ __launch_bounds__(HO_THREADS) void k_se_scale_add(const T* __restrict__ x, const float* __restrict__ s,
+                                                             const float* __restrict__ bias,
                                                              const T* __restrict__ res, int64_t hw,
                                                              T* __restrict__ y) {
-#pragma clang fp contract(off)  // x * s and + res round separately, as torch's two kernels do
+#pragma clang fp contract(off)  // + bias, * s and + res round separately, as torch's kernels do
   using V = Vec<T>;
   const int c = blockIdx.y, split = gridDim.x;
-  const float g = s[c];
+  const float g = s[c], bc = bias ? bias[c] : 0.f;
   const Plane P(hw, V::N, c, split, blockIdx.x);
   for (int64_t i = P.lo + threadIdx.x; i < P.hi; i += HO_THREADS) {
     float a[V::N], r[V::N];
@@ -209,16 +213,27 @@ __global__ __launch_bounds__(HO_THREADS) void k_se_scale_add(const T* __restrict
     V::load(res + i * V::N, r);
     // torch rounds x * s to the storage type before the residual add; so does this
 #pragma unroll
-    for (int q = 0; q < V::N; ++q) a[q] = V::round(a[q] * g) + r[q];
+    for (int q = 0; q < V::N; ++q) a[q] = V::round(V::round(a[q] + bc) * g) + r[q];
     V::store(y + i * V::N, a);
   }
   if (blockIdx.x == split - 1) {
     const int64_t ns = P.nscalar(V::N);
     for (int64_t i = threadIdx.x; i < ns; i += HO_THREADS) {
       const int64_t e = P.scalar_at(i, V::N);
-      V::st1(y + e, V::round(V::ld1(x + e) * g) + V::ld1(res + e));
+      V::st1(y + e, V::round(V::round(V::ld1(x + e) + bc) * g) + V::ld1(res + e));
     }
   }
+}
+
+// mean[c] = sum of the channel's partials / hw (+ bias[c]): SEBlock's x.mean(dim=(2, 3)) of a
+// conv output whose bias is applied later (di_se_scale_add)
+__global__ void k_channel_mean(const double* __restrict__ part, int split, int channels, int64_t hw,
+                               const float* __restrict__ bias, float* __restrict__ mean) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= channels) return;
+  double a = 0.0;
+  for (int i = 0; i < split; ++i) a += part[((int64_t)c * split + i) * 2];
+  mean[c] = (float)(a / (double)hw + (bias ? (double)bias[c] : 0.0));
 }
 
 // blocks per channel: fill the chip (>= ~2048 blocks) without slices under 2 vectors per thread
@@ -263,18 +278,35 @@ extern "C" int di_inorm_elu(di_dtype dt, const void* x, int32_t channels, int64_
   return e == hipSuccess ? DI_OK : (int)e;
 }
 
-extern "C" int di_se_scale_add(di_dtype dt, const void* x, const float* scale, const void* res, int32_t channels,
-                               int64_t hw, void* y, void* stream) {
+extern "C" int di_channel_mean(di_dtype dt, const void* x, int32_t channels, int64_t hw, const float* bias,
+                               void* work, float* mean, void* stream) {
+  if (!x || !work || !mean || channels <= 0 || channels > 65535 || hw <= 0) return DI_EINVAL;
+  if ((dt != DI_F32 && dt != DI_BF16) || !aligned16(x)) return DI_EINVAL;
+  const int split = ho_split(channels, hw, dt == DI_BF16 ? 8 : 4);
+  const dim3 grid(split, channels);
+  hipStream_t s = (hipStream_t)stream;
+  double* part = reinterpret_cast<double*>(work);
+  if (dt == DI_BF16)
+    hipLaunchKernelGGL(k_inorm_stats<u16>, grid, dim3(HO_THREADS), 0, s, (const u16*)x, hw, part);
+  else
+    hipLaunchKernelGGL(k_inorm_stats<float>, grid, dim3(HO_THREADS), 0, s, (const float*)x, hw, part);
+  hipLaunchKernelGGL(k_channel_mean, dim3((channels + 63) / 64), dim3(64), 0, s, part, split, channels, hw, bias, mean);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? DI_OK : (int)e;
+}
+
+extern "C" int di_se_scale_add(di_dtype dt, const void* x, const float* scale, const float* bias, const void* res,
+                               int32_t channels, int64_t hw, void* y, void* stream) {
   if (!x || !scale || !res || !y || channels <= 0 || channels > 65535 || hw <= 0) return DI_EINVAL;
   if ((dt != DI_F32 && dt != DI_BF16) || !aligned16(x) || !aligned16(res) || !aligned16(y)) return DI_EINVAL;
   const int vec = dt == DI_BF16 ? 8 : 4;
   const dim3 grid(ho_split(channels, hw, vec), channels);
   hipStream_t s = (hipStream_t)stream;
   if (dt == DI_BF16)
-    hipLaunchKernelGGL(k_se_scale_add<u16>, grid, dim3(HO_THREADS), 0, s, (const u16*)x, scale, (const u16*)res,
-                       hw, (u16*)y);
+    hipLaunchKernelGGL(k_se_scale_add<u16>, grid, dim3(HO_THREADS), 0, s, (const u16*)x, scale, bias,
+                       (const u16*)res, hw, (u16*)y);
   else
-    hipLaunchKernelGGL(k_se_scale_add<float>, grid, dim3(HO_THREADS), 0, s, (const float*)x, scale,
+    hipLaunchKernelGGL(k_se_scale_add<float>, grid, dim3(HO_THREADS), 0, s, (const float*)x, scale, bias,
                        (const float*)res, hw, (float*)y);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? DI_OK : (int)e;

@@ -27,6 +27,23 @@ class HeadNormOps:
         self.lib = _lib.load()
         self.device = torch.device(device)
         self._work = None
+        self._f32 = {}  # fp32 copies of (bf16) per-channel parameters, made once per parameter
+
+    def f32(self, p):
+        """fp32 contiguous copy of a (possibly bf16) per-channel parameter, cached."""
+        if p is None:
+            return None
+        hit = self._f32.get(id(p))
+        # the entry holds p itself, so its id cannot be reused by another tensor while cached
+        if hit is None or hit[0] is not p or hit[1] != p._version:
+            hit = self._f32[id(p)] = (p, p._version, p.detach().float().contiguous())
+        return hit[2]
+
+    def work(self, C, hw, device):
+        nb = self.lib.di_inorm_work_bytes(C, hw)
+        if self._work is None or self._work.numel() * 8 < nb:
+            self._work = torch.empty((nb + 7) // 8, dtype=torch.float64, device=device)
+        return self._work
 
     def _dt(self, x):
         if x.dtype == torch.float32:
@@ -48,27 +65,40 @@ class HeadNormOps:
         self._check(x)
         C, hw = x.shape[1], x.shape[2] * x.shape[3]
         y = torch.empty_like(x) if out is None else out
-        nb = self.lib.di_inorm_work_bytes(C, hw)
-        if self._work is None or self._work.numel() * 8 < nb:
-            self._work = torch.empty((nb + 7) // 8, dtype=torch.float64, device=x.device)
-        g = norm.weight.detach().float().contiguous()
-        b = norm.bias.detach().float().contiguous()
+        w = self.work(C, hw, x.device)
+        g, b = self.f32(norm.weight), self.f32(norm.bias)
         self._lib.check(self.lib.di_inorm_elu(self._dt(x), ctypes.c_void_p(x.data_ptr()), C, hw,
                                               ctypes.c_void_p(g.data_ptr()), ctypes.c_void_p(b.data_ptr()),
-                                              ctypes.c_float(norm.eps), ctypes.c_void_p(self._work.data_ptr()),
+                                              ctypes.c_float(norm.eps), ctypes.c_void_p(w.data_ptr()),
                                               ctypes.c_void_p(y.data_ptr()), self._stream()), "di_inorm_elu")
         return y
 
-    def se_scale_add(self, x, scale, res, out=None):
-        """x * scale[None, :, None, None] + res; out may be x or res (in place)."""
+    def channel_mean(self, x, bias=None):
+        """x.mean(dim=(2, 3)) (+ bias) as fp32 [1, C]."""
+        self._check(x)
+        C, hw = x.shape[1], x.shape[2] * x.shape[3]
+        w = self.work(C, hw, x.device)
+        m = torch.empty(1, C, dtype=torch.float32, device=x.device)
+        b = self.f32(bias)
+        self._lib.check(self.lib.di_channel_mean(self._dt(x), ctypes.c_void_p(x.data_ptr()), C, hw,
+                                                 ctypes.c_void_p(0 if b is None else b.data_ptr()),
+                                                 ctypes.c_void_p(w.data_ptr()), ctypes.c_void_p(m.data_ptr()),
+                                                 self._stream()), "di_channel_mean")
+        return m
+
+    def se_scale_add(self, x, scale, res, out=None, bias=None):
+        """(x + bias[None, :, None, None]) * scale[None, :, None, None] + res; out may be x or res."""
         self._check(x)
         self._check(res)
         C, hw = x.shape[1], x.shape[2] * x.shape[3]
         s = scale.detach().reshape(-1).float().contiguous()
+        b = self.f32(bias)
         y = torch.empty_like(x) if out is None else out
         self._lib.check(self.lib.di_se_scale_add(self._dt(x), ctypes.c_void_p(x.data_ptr()),
-                                                 ctypes.c_void_p(s.data_ptr()), ctypes.c_void_p(res.data_ptr()),
-                                                 C, hw, ctypes.c_void_p(y.data_ptr()), self._stream()),
+                                                 ctypes.c_void_p(s.data_ptr()),
+                                                 ctypes.c_void_p(0 if b is None else b.data_ptr()),
+                                                 ctypes.c_void_p(res.data_ptr()), C, hw,
+                                                 ctypes.c_void_p(y.data_ptr()), self._stream()),
                         "di_se_scale_add")
         return y
 
@@ -80,7 +110,10 @@ class SEBlock(nn.Module):
         self.linear2 = nn.Linear(ch // ratio, ch)
 
     def gate(self, x):
-        s = x.mean(dim=(2, 3))
+        return self.gate_from_mean(x.mean(dim=(2, 3)))
+
+    def gate_from_mean(self, s):
+        s = s.to(self.linear1.weight.dtype)
         return torch.sigmoid(F.relu(self.linear2(F.relu(self.linear1(s)))))
 
     def forward(self, x):
@@ -118,21 +151,37 @@ class ResNet(nn.Module):
         if self.initial_projection:
             x = m[f"resnet_{self.module_name}_init_proj"](x)
         ops = self.ops
+        if ops is not None:
+            return self._forward_hip(x, ops)
         for r in self.blocks:
             res = x
             for i in (1, 2, 3):
-                if self.inorm and ops is not None:
+                if self.inorm:
+                    x = m[f"{r}_inorm_{i}"](x)
+                x = m[f"{r}_conv2d_{i}"](F.elu(x))
+            x = m[f"{r}_se_block"](x) + res
+        return x
+
+    def _forward_hip(self, x, ops):
+        """Same blocks with the norm / bias / SE passes on HIP (HeadNormOps). A conv that feeds an
+        InstanceNorm runs without its bias (a per-channel constant cancels in the normalisation);
+        the last conv's bias is applied inside the SE gate + residual pass, and the SE squeeze
+        (channel mean) adds it analytically."""
+        m = self._modules
+        for r in self.blocks:
+            res = x
+            for i in (1, 2, 3):
+                conv = m[f"{r}_conv2d_{i}"]
+                if self.inorm:
                     x = ops.inorm_elu(x, m[f"{r}_inorm_{i}"], out=None if i == 1 else x)
                 else:
-                    if self.inorm:
-                        x = m[f"{r}_inorm_{i}"](x)
                     x = F.elu(x)
-                x = m[f"{r}_conv2d_{i}"](x)
-            se = m[f"{r}_se_block"]
-            if ops is not None:
-                x = ops.se_scale_add(x, se.gate(x), res, out=x)
-            else:
-                x = se(x) + res
+                keep_bias = not self.inorm and i < 3
+                x = F.conv2d(x, conv.weight, conv.bias if keep_bias else None, conv.stride, conv.padding,
+                             conv.dilation)
+            conv3, se = m[f"{r}_conv2d_3"], m[f"{r}_se_block"]
+            gate = se.gate_from_mean(ops.channel_mean(x, conv3.bias))
+            x = ops.se_scale_add(x, gate, res, out=x, bias=conv3.bias)
         return x
 
 

@@ -19,7 +19,8 @@
  *   di_head_prologue  ELU(inorm_1(conv2d_1(T))) of the head, T never materialised
  *                                                                    deepinteract_modules.py:1181-1184, 1228-1232
  *   di_inorm_elu    ELU(InstanceNorm2d(x)) of the head's ResNet blocks deepinteract_modules.py:1016-1030,1075-1095
- *   di_se_scale_add SEBlock gate + residual add                      deepinteract_modules.py:954-970, 1095
+ *   di_se_scale_add conv bias + SEBlock gate + residual add          deepinteract_modules.py:954-970, 1095
+ *   di_channel_mean SEBlock squeeze (channel mean)                   deepinteract_modules.py:966
  *   di_knn_topk     dgl.knn_graph + topk(pairwise_squared_distance)  graph_utils.py:107-108
  *   di_geo_feats    GeometricProteinFeatures('full') + edge/node feature assembly
  *                                                                    protein_feature_utils.py:322-377,
@@ -144,11 +145,17 @@ int64_t di_head_prologue_work_bytes(int32_t num_complexes, int32_t max_l1, int32
 int di_inorm_elu(di_dtype dt, const void* x, int32_t channels, int64_t hw, const float* gamma,
                  const float* beta, float eps, void* work, void* y, void* stream);
 int64_t di_inorm_work_bytes(int32_t channels, int64_t hw);
-/* y = x * scale[c] + res: SEBlock's channel gate (deepinteract_modules.py:954-970) fused with the
- * ResNet block's residual add (:1095); x * scale is rounded to `dt` before the add, as torch does.
- * x, res, y: [channels, hw], 16-B aligned (y may alias x or res); scale [channels] fp32. */
-int di_se_scale_add(di_dtype dt, const void* x, const float* scale, const void* res, int32_t channels,
-                    int64_t hw, void* y, void* stream);
+/* y = (x + bias[c]) * scale[c] + res: the ResNet block's last conv bias (nullable), SEBlock's
+ * channel gate (deepinteract_modules.py:954-970) and the block's residual add (:1095); each step
+ * is rounded to `dt`, as torch's separate kernels do. x, res, y: [channels, hw], 16-B aligned (y
+ * may alias x or res); scale, bias [channels] fp32. */
+int di_se_scale_add(di_dtype dt, const void* x, const float* scale, const float* bias, const void* res,
+                    int32_t channels, int64_t hw, void* y, void* stream);
+/* mean[c] = mean over hw of x[c] (+ bias[c], nullable): SEBlock's x.mean(dim=(2, 3))
+ * (:966) of a conv output whose bias is deferred to di_se_scale_add. fp64 accumulation;
+ * work: di_inorm_work_bytes() bytes. */
+int di_channel_mean(di_dtype dt, const void* x, int32_t channels, int64_t hw, const float* bias, void* work,
+                    float* mean, void* stream);
 
 /* ---- graph builder ----------------------------------------------------------------------- */
 /* Cα kNN per chain: idx_out [Nt,k] chain-local neighbour ids (ascending squared distance,

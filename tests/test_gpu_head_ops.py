@@ -76,10 +76,27 @@ def test_se_scale_add_exact(ops, shape, dtype):
     ref = x * s[:, :, None, None] + res
     y = ops.se_scale_add(x, s, res)
     assert torch.equal(y, ref)
+    # with the deferred conv bias: torch's order is (x + b) -> * s -> + res, each rounded
+    b = torch.randn(C, generator=torch.Generator().manual_seed(8)).cuda()
+    xb = x + b.to(dtype)[None, :, None, None] if dtype == torch.bfloat16 else x + b[None, :, None, None]
+    ref_b = xb * s[:, :, None, None] + res
+    assert torch.equal(ops.se_scale_add(x, s, res, bias=b.to(dtype)), ref_b)
+
+
+@pytest.mark.parametrize("shape", SHAPES)
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_channel_mean(ops, shape, dtype):
+    C, H, W = shape
+    x = _x(C, H, W, 9, dtype)
+    b = torch.randn(C, generator=torch.Generator().manual_seed(10)).cuda()
+    ref = x.double().mean(dim=(2, 3)) + b.double()[None]
+    m = ops.channel_mean(x, b)
+    assert float((m.double() - ref).abs().max()) < 1e-6 * float(ref.abs().max()) + 1e-7
 
 
 def test_head_body_with_hip_ops_matches_torch_f32():
-    """The whole head (58 ResNet blocks) with the HIP passes vs torch's passes, fp32, 64x64."""
+    """The whole head (58 ResNet blocks) with the HIP passes (bias folding, SE fusion) vs torch's
+    passes, fp32, 64x64."""
     from deepinteract_amd.head import HeadNormOps, ResNet2DInputWithOptAttention
     from deepinteract_amd.weights import seeded_state_dict
     sd = seeded_state_dict(0)

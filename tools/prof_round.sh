@@ -17,4 +17,6 @@ P="--steps 1 --warmup 1 --no-cpu --complexes 64"
   "prof_write:120:cd /tmp && timeout -s KILL 110 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/prof_write -o run -- python $R/bench.py $P" \
   "sprof_stats:240:cd /tmp && rocprofv3 --kernel-trace --stats --output-format csv -d $O/sprof_stats -o run -- python $R/bench.py $S --overlap 0" \
   "sprof_fetch:120:cd /tmp && timeout -s KILL 110 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/sprof_fetch -o run -- python $R/bench.py $P --overlap 0" \
+  "head_bench:300:python tools/bench_head.py > $O/bench_head.json" \
+  "head_stats:300:cd /tmp && rocprofv3 --kernel-trace --stats --output-format csv -d $O/head_stats -o run -- python $R/tools/bench_head.py --only bf16_nchw_hipnorm --reps 2" \
   "sprof_write:120:cd /tmp && timeout -s KILL 110 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/sprof_write -o run -- python $R/bench.py $P --overlap 0"
