@@ -18,6 +18,7 @@ import re
 import zlib
 from collections import OrderedDict
 
+import numpy as np
 import torch
 
 from .config import GeoTConfig, NUM_RBF
@@ -191,6 +192,64 @@ def _draw(key: str, shape, kind: str, seed: int) -> torch.Tensor:
     else:
         raise ValueError(kind)
     return t.to(torch.float32)
+
+
+def glorot_orthogonal(tensor: torch.Tensor, scale: float, generator=None) -> torch.Tensor:
+    """deepinteract_utils.py:47-52: orthogonal_ then W *= sqrt(scale / ((fan_out + fan_in) * var(W)))."""
+    torch.nn.init.orthogonal_(tensor, generator=generator)
+    s = scale / ((tensor.size(-2) + tensor.size(-1)) * tensor.var())
+    tensor.mul_(s.sqrt())
+    return tensor
+
+
+def reference_init_state_dict(seed: int = 0, cfg: GeoTConfig = GeoTConfig(), with_head: bool = True):
+    """A LitGINI state dict initialised the way the reference's modules initialise themselves
+    (SURVEY.md §8a a14), from one seeded CPU generator:
+      * every GeoT linear weight: glorot_orthogonal(scale=2.0) (reset_parameters at
+        deepinteract_modules.py:55-74, 176-196, 336-371, 483-490, 652-667, 879-890, 1585-1589),
+        their biases zero-filled; BatchNorm at its defaults (1, 0, running 0 / 1);
+      * InitEdge's positional nn.Embedding: U(-sqrt(3), sqrt(3)) (:179);
+      * the head: PyTorch's default Conv2d / Linear init (U(+-1/sqrt(fan_in)) for weights and biases),
+        InstanceNorm affine at (1, 0), and phase2_conv.bias[1] = -7 (:1221-1226).
+    The values are not the reference's own random draws (torch's RNG stream over its module
+    construction order is not reproduced); the distributions and the deterministic parts are."""
+    g = torch.Generator(device="cpu")
+    g.manual_seed(seed)
+    sd = OrderedDict()
+    shared = {}
+    keys = geot_keys(cfg) + (head_keys(cfg) if with_head else [])
+    for key, shape, kind in keys:
+        canon = _canonical_key(key)
+        if canon in shared:  # the ResBlock's one BatchNorm, registered three times
+            sd[key] = shared[canon].clone()
+            continue
+        head = key.startswith("interact_module.")
+        if kind == "bn_nbt":
+            t = torch.tensor(0, dtype=torch.long)
+        elif kind in ("bn_w", "bn_var"):
+            t = torch.ones(shape)
+        elif kind in ("bn_b", "bn_mean"):
+            t = torch.zeros(shape)
+        elif kind == "emb":
+            t = torch.empty(shape).uniform_(-math.sqrt(3.0), math.sqrt(3.0), generator=g)
+        elif kind == "lin_w" and not head:
+            t = glorot_orthogonal(torch.empty(shape), 2.0, generator=g)
+        elif kind == "bias" and not head:
+            t = torch.zeros(shape)
+        elif kind in ("lin_w", "conv_w"):
+            fan_in = int(np.prod(shape[1:]))
+            b = 1.0 / math.sqrt(fan_in)
+            t = torch.empty(shape).uniform_(-b, b, generator=g)
+        elif kind in ("bias", "conv_b"):
+            w_shape = next(s for k, s, _ in keys if k == key[:-len("bias")] + "weight")
+            b = 1.0 / math.sqrt(int(np.prod(w_shape[1:])))
+            t = torch.empty(shape).uniform_(-b, b, generator=g)
+        else:
+            raise ValueError(kind)
+        if key == "interact_module.phase2_conv.bias":
+            t[1] = -7.0
+        sd[key] = shared[canon] = t.to(torch.float32) if t.is_floating_point() else t
+    return sd
 
 
 def seeded_state_dict(seed: int = 0, cfg: GeoTConfig = GeoTConfig(), with_head: bool = True):

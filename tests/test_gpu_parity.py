@@ -203,3 +203,26 @@ def test_end_to_end_logits_f32(sd, case):
     torch.cuda.synchronize()
     assert rel_max(logits[0].cpu().numpy(), z["logits"]) < F32_TOL
     assert rel_max(probs[0].cpu().numpy(), z["probs"]) < F32_TOL
+
+
+def test_geot_reference_init_weights():
+    """Weights drawn the reference's way (glorot_orthogonal, zero biases, default BatchNorm;
+    weights.reference_init_state_dict) through the HIP path vs the oracle, fp32."""
+    import oracle.geot_oracle as O
+    from deepinteract_amd.engine import GeoTEngine
+    from deepinteract_amd.weights import reference_init_state_dict
+    sd = reference_init_state_dict(1, with_head=False)
+    z = load_case("tiny")
+    gb = _batch(z)
+    h, e = GeoTEngine(sd, "f32").forward(gb)
+    torch.cuda.synchronize()
+    h, e = h.cpu().numpy(), e.cpu().numpy()
+    n1, e1 = gb.nodes_per_graph[0], gb.edges_per_graph[0]
+    for tag, hs, es in (("g1", h[:n1], e[:e1]), ("g2", h[n1:], e[e1:])):
+        it = chain_item(z, tag)
+        g = {"num_nodes": it["num_nodes"], "src": it["src"], "dst": it["dst"], "src_nbr": it["src_nbr"],
+             "dst_nbr": it["dst_nbr"], "node_f": it["node_f"].float(), "edge_f": it["edge_f"].float()}
+        with torch.no_grad():
+            hn, en = O.geot_forward(sd, g)
+        assert rel_max(hs, hn.numpy()) < F32_TOL
+        assert rel_max(es, en.numpy()) < F32_TOL
