@@ -399,7 +399,11 @@ __device__ __forceinline__ int xcd_tile(int b, int ntiles) {
 // across tiles (the last stage's DMA slot fetches stage 0 of the next tile) and the next tile's
 // inputs are prefetched under the current tile's last stages, so no tile pays a cold prologue.
 template <class DT, int MODE>
-__global__ __attribute__((amdgpu_flat_work_group_size(1, 512), amdgpu_waves_per_eu(2, 2), amdgpu_num_vgpr(120)))
+#ifndef DI_EDGE_NUM_VGPR
+#define DI_EDGE_NUM_VGPR 120
+#endif
+__global__ __attribute__((amdgpu_flat_work_group_size(1, 512), amdgpu_waves_per_eu(2, 2),
+                          amdgpu_num_vgpr(DI_EDGE_NUM_VGPR)))
 void k_edge_layer(EdgeArgs a) {
   constexpr bool FINAL = MODE == 1, CONF = MODE == 2;
   DI_GEOT_ENTRY();

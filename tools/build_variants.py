@@ -51,6 +51,8 @@ VARIANTS = {
     "prio1": ["DI_GEOT_PRIO=1"],
     "prio3": ["DI_GEOT_PRIO=3"],
     "persist_prio2": ["DI_EDGE_PERSIST=1", "DI_GEOT_PRIO=2"],
+    "vgpr128": ["DI_EDGE_NUM_VGPR=128"],
+    "vgpr124": ["DI_EDGE_NUM_VGPR=124"],
 }
 
 if __name__ == "__main__":
