@@ -58,6 +58,35 @@ def test_head_prologue_matches_oracle(dtype, sizes):
         assert rel_max(v.float().cpu().numpy(), ref.numpy()) < tol
 
 
+@pytest.mark.parametrize("C,H,sizes", [
+    (40, 64, [(70, 36), (4200, 12)]),   # channels % 16 != 0; 66 row tiles on one side (> one wave)
+    (13, 128, [(65, 128), (1, 8)]),     # fewer channels than one table block; single-row chain
+])
+def test_head_prologue_ragged_channels_and_many_tiles(C, H, sizes):
+    """The table kernels split rows into 64-row tiles and channels into groups of 16; the
+    per-channel statistics are merged from the tile summaries (fp32, <= 1e-4)."""
+    from deepinteract_amd.engine import HeadPrologueOp
+    from oracle import geot_oracle as O
+    torch.manual_seed(7)
+    sd = _head_params(8, C=C, H=H)
+    rows = sum(a + b for a, b in sizes)
+    h = torch.randn(rows, H) * 2
+    op = HeadPrologueOp(sd["interact_module.conv2d_1.weight"], sd["interact_module.conv2d_1.bias"],
+                        sd["interact_module.inorm_1.weight"], sd["interact_module.inorm_1.bias"], 1e-6, "cuda")
+    h1r, h2r, r = [], [], 0
+    for a, b in sizes:
+        h1r.append(r)
+        h2r.append(r + a)
+        r += a + b
+    _, views = op(h.cuda(), h1r, h2r, [a for a, _ in sizes], [b for _, b in sizes])
+    torch.cuda.synchronize()
+    for (a, b), s1, s2, v in zip(sizes, h1r, h2r, views):
+        with torch.no_grad():
+            ref = O.head_prologue(sd, O.pair_tensor(h[s1:s1 + a], h[s2:s2 + b]))
+        assert v.shape == ref.shape
+        assert rel_max(v.float().cpu().numpy(), ref.numpy()) < 1e-4
+
+
 def test_head_prologue_bf16_wide_range_channels_take_exact_exp():
     """Channels whose folded tables exceed |60| (gamma x 200) leave the e^a e^b product path for
     the exact exp path; results stay within the bf16 tolerance on every channel."""
