@@ -32,7 +32,15 @@
 namespace di {
 
 constexpr int PRO_THREADS = 256;
-constexpr int PRO_CG = 4;          // channels per table block
+#ifndef DI_PRO_TABLE_THREADS
+#define DI_PRO_TABLE_THREADS 512
+#endif
+constexpr int PRO_TTHREADS = DI_PRO_TABLE_THREADS;  // threads per table block (rows in flight)
+#ifndef DI_PRO_CG
+#define DI_PRO_CG 4
+#endif
+constexpr int PRO_CG = DI_PRO_CG;  // channels per table block (<= 4: one floatx4 of weights per k)
+static_assert(PRO_CG >= 1 && PRO_CG <= 4, "PRO_CG");
 constexpr int PRO_SEG = 128;       // 16-B chunks per row segment of the store stream (2 per lane)
 constexpr float PRO_EXP_SAFE = 60.f;
 
@@ -111,7 +119,7 @@ __device__ __forceinline__ void pro_dots(const T* __restrict__ h, int64_t h_row,
 }
 
 template <typename T>
-__global__ __launch_bounds__(PRO_THREADS) void k_prologue_tables(const di_pair_desc* __restrict__ descs, int hidden,
+__global__ __launch_bounds__(PRO_TTHREADS) void k_prologue_tables(const di_pair_desc* __restrict__ descs, int hidden,
                                                                  int channels, int max_l1, int max_l2, float eps,
                                                                  const T* __restrict__ h, const float* __restrict__ w,
                                                                  const float* __restrict__ bias,
@@ -119,7 +127,7 @@ __global__ __launch_bounds__(PRO_THREADS) void k_prologue_tables(const di_pair_d
                                                                  const float* __restrict__ beta,
                                                                  float* __restrict__ work) {
   __shared__ floatx4 wl[512];  // [2H][PRO_CG], hidden <= 256
-  __shared__ float red[(PRO_THREADS / 64) * PRO_CG];
+  __shared__ float red[(PRO_TTHREADS / 64) * PRO_CG];
   const int groups = (channels + PRO_CG - 1) / PRO_CG;
   const int c0 = (blockIdx.x % groups) * PRO_CG, cpx = blockIdx.x / groups;
   const int nc = channels - c0 < PRO_CG ? channels - c0 : PRO_CG;
@@ -392,10 +400,10 @@ extern "C" int di_head_prologue(di_dtype dt, const di_pair_desc* descs, int32_t 
   const int groups = (channels + PRO_CG - 1) / PRO_CG;
   const unsigned tgrid = (unsigned)num_complexes * (unsigned)groups;
   if (dt == DI_BF16)
-    hipLaunchKernelGGL(k_prologue_tables<u16>, dim3(tgrid), dim3(PRO_THREADS), 0, s, descs, hidden, channels, max_l1,
+    hipLaunchKernelGGL(k_prologue_tables<u16>, dim3(tgrid), dim3(PRO_TTHREADS), 0, s, descs, hidden, channels, max_l1,
                        max_l2, eps, (const u16*)h, conv_w, conv_b, in_gamma, in_beta, work);
   else
-    hipLaunchKernelGGL(k_prologue_tables<float>, dim3(tgrid), dim3(PRO_THREADS), 0, s, descs, hidden, channels,
+    hipLaunchKernelGGL(k_prologue_tables<float>, dim3(tgrid), dim3(PRO_TTHREADS), 0, s, descs, hidden, channels,
                        max_l1, max_l2, eps, (const float*)h, conv_w, conv_b, in_gamma, in_beta, work);
   if (aligned16) {
     const int rows = 64 * g_pro_waves;
