@@ -8,7 +8,9 @@ written to a rotating HBM buffer). The timed region starts with every complex's 
 (node [N,113], edge [E,28], ids) resident in HBM and ends with the outputs in HBM.
 
 Multi-GPU (torchrun): complexes are sharded, each rank owns its 1024; no collective in the timed
-region (weak scaling); value = total complexes / max-over-ranks time.
+region (weak scaling); value = total complexes / max-over-ranks time. After the timed region the
+C4 driver (distributed.predict_sharded) runs on real complexes and the contact-map all-gather is
+timed at the metric's size (supplementary record).
 
 Prints ONE JSON line on rank 0.
 """
@@ -54,6 +56,30 @@ def algorithmic_bytes_per_complex(n1, n2, k, s):
         e = n * k
         b += n * 113 * 4 + e * 28 * 4 + e * 4 + e * 2 * 2 * 4 + n * 128 * s + e * 128 * s
     return b + 256 * n1 * n2 * s
+
+
+def algorithmic_flops_per_complex(n1, n2, k, layers=2):
+    """2 * sum_chains [E*(129,024 + (L-1)*456,656 + 374,736)
+    + N*(113*128 + L*(3*128^2 + 128^2 + 2*128*256))] (77.9 GFLOP at C3)."""
+    f = 0
+    for n in (n1, n2):
+        e = n * k
+        f += e * (129_024 + (layers - 1) * 456_656 + 374_736) + n * (113 * H + layers * (3 * H * H + H * H + 2 * H * 2 * H))
+    return 2.0 * f
+
+
+def physical_cores():
+    """Physical cores (distinct (package, core) pairs) among the CPUs this process may run on."""
+    cpus = sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else list(range(os.cpu_count() or 1))
+    seen = set()
+    for c in cpus:
+        try:
+            base = f"/sys/devices/system/cpu/cpu{c}/topology/"
+            with open(base + "physical_package_id") as f1, open(base + "core_id") as f2:
+                seen.add((f1.read().strip(), f2.read().strip()))
+        except OSError:
+            seen.add(("?", str(c)))
+    return max(len(seen), 1), len(cpus)
 
 
 def kernel_units(kind, nodes, edges, l1l2):
@@ -107,8 +133,9 @@ def load_pmc_traffic(kernel):
         return None
 
 
-def cpu_baseline(n_res, k, sample, threads):
-    """Oracle (CPU restatement, DGL-style op-for-op, fp32) on C3-shaped complexes."""
+def cpu_baseline(n_res, k, sample, threads, warmup=3):
+    """Oracle (CPU restatement, DGL-style op-for-op, fp32, torch.inference_mode) on C3-shaped
+    complexes: `warmup` untimed complexes, then `sample` timed (SURVEY.md §8d protocol)."""
     from deepinteract_amd import synth
     from deepinteract_amd.weights import seeded_state_dict
     from oracle import geot_oracle as O
@@ -125,7 +152,8 @@ def cpu_baseline(n_res, k, sample, threads):
             t = O.pair_tensor(n1, n2)
         return t
 
-    one()  # warm-up
+    for _ in range(warmup):
+        one()
     t0 = time.perf_counter()
     for _ in range(sample):
         one()
@@ -158,12 +186,34 @@ def head_prologue_record(h1r, h2r, l1, l2, gb, eng, dev, tdt, reps=5):
             "bytes_per_launch": byts}
 
 
-def allgather_record(ws, complexes, n_res, dev, reps=3):
-    """Supplementary, outside the metric: the one RCCL all-gather of fp32 contact
-    maps ([L1, L2] per complex, every rank's complexes to every rank), timed after the metric."""
+def allgather_record(ws, rank, complexes, n_res, k, dev, reps=3):
+    """Supplementary, outside the metric, two parts:
+    1. the C4 driver end to end on REAL maps: distributed.predict_sharded over 2 synthetic
+       complexes per rank (device builder -> bf16 GeoT -> pair tensor -> bf16 head -> contact
+       probabilities) and its ONE RCCL all-gather; every rank then checks it holds every map;
+    2. that all-gather at the metric's size (`complexes` fp32 [L1, L2] maps per rank), the send
+       buffer filled with this rank's real maps (tiled), timed over `reps`."""
     import torch.distributed as dist
+    from deepinteract_amd import synth
+    from deepinteract_amd.distributed import gpu_forward, predict_sharded
+    from deepinteract_amd.modules import LitGINI
+    from deepinteract_amd.weights import seeded_state_dict
+    model = LitGINI(dtype="bf16", head_dtype=torch.bfloat16).to(dev).eval()
+    model.load_reference_state_dict(seeded_state_dict(0))
+    cx = [synth.synthetic_complex(50_000 + i, n_res, n_res) for i in range(2 * ws)]
+    barrier(ws)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    maps, plan = predict_sharded(cx, gpu_forward(model, k), micro_batch=2, dtype=torch.float32, device=dev)
+    torch.cuda.synchronize()
+    t_pred = max_over_ranks(ws, time.perf_counter() - t0)
+    sums = torch.stack([m.double().sum() for m in maps])
+    ref = sums.clone()
+    dist.broadcast(ref, 0)
+    consistent = bool(torch.equal(sums, ref)) and all(0.0 <= float(m.min()) and float(m.max()) <= 1.0 for m in maps)
     per_rank = complexes * n_res * n_res
-    send = torch.zeros(per_rank, dtype=torch.float32, device=dev)
+    local = torch.cat([maps[i].reshape(-1) for i in plan[rank]])
+    send = local.repeat((per_rank + local.numel() - 1) // local.numel())[:per_rank].contiguous()
     recv = torch.empty(per_rank * ws, dtype=torch.float32, device=dev)
     dist.all_gather_into_tensor(recv, send)
     torch.cuda.synchronize()
@@ -174,8 +224,11 @@ def allgather_record(ws, complexes, n_res, dev, reps=3):
     torch.cuda.synchronize()
     dt = max_over_ranks(ws, (time.perf_counter() - t0) / reps)
     del send, recv
-    return {"bytes_per_rank": per_rank * 4, "ms": round(dt * 1e3, 3),
-            "algbw_GBs": round(per_rank * 4 * (ws - 1) / dt / 1e9, 1), "collective": "all_gather_into_tensor (RCCL)"}
+    return {"predict_sharded": {"complexes": len(cx), "s": round(t_pred, 3), "maps_consistent_on_all_ranks": consistent,
+                                "what": "builder + bf16 GeoT + pair tensor + bf16 head + probs, one all-gather"},
+            "bytes_per_rank": per_rank * 4, "ms": round(dt * 1e3, 3),
+            "algbw_GBs": round(per_rank * 4 * (ws - 1) / dt / 1e9, 1),
+            "collective": "all_gather_into_tensor (RCCL), real contact maps tiled to the metric's size"}
 
 
 def main():
@@ -189,7 +242,7 @@ def main():
     ap.add_argument("--knn", type=int, default=20)
     ap.add_argument("--pool", type=int, default=16, help="distinct synthetic complexes replicated in HBM")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
-    ap.add_argument("--cpu-sample", type=int, default=16)
+    ap.add_argument("--cpu-sample", type=int, default=20)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-prologue", action="store_true", help="skip the supplementary fused-head-prologue line")
     ap.add_argument("--pair-cus", type=int, default=0,
@@ -211,7 +264,12 @@ def main():
     ap.add_argument("--layers", type=int, default=None, help="GeoT layers (default 2; c5: 4)")
     ap.add_argument("--node-limit", type=int, default=None,
                     help="max_num_graph_nodes of the synthetic model (default 2304; c5: 4096)")
+    ap.add_argument("--lib", default=None, help="tuning: a launch-shape variant of the HIP library "
+                                                 "(deepinteract_amd.build.build_variant)")
     args = ap.parse_args()
+    if args.lib:
+        from deepinteract_amd import _lib
+        _lib.load_variant(args.lib)
     if args.config == "c5":
         # BASELINE.json configs[4]: 2x4000 residues, k=30, 4 GeoT layers. The reference's
         # nn.Embedding(max_num_graph_nodes=2304) cannot index 4000 residues, so the synthetic model is
@@ -236,7 +294,7 @@ def main():
     from deepinteract_amd import synth
     from deepinteract_amd.builder import build_graph_batch
     from deepinteract_amd.engine import GeoTEngine, PairTensorOp
-    from deepinteract_amd.graph import concat_batches
+    from deepinteract_amd.graph import select_graphs
     from deepinteract_amd.weights import seeded_state_dict
 
     n_res, k, M = args.residues, args.knn, args.micro_batch
@@ -265,13 +323,17 @@ def main():
     t_synth = time.perf_counter() - tb
     torch.cuda.synchronize()
     tb = time.perf_counter()
-    pool_gb = [build_graph_batch([a, b], k=k, seed=c + 1, device=dev, node_count_limit=args.node_limit)
-               for c, (a, b) in enumerate(pool)]
+    # the whole pool in one builder call (one launch per stage); neighbour ids as the reference
+    # draws them after torch.manual_seed(s) per chain (bit-exact mode)
+    pool_gb = build_graph_batch([ch for pair in pool for ch in pair], k=k, device=dev,
+                                node_count_limit=args.node_limit,
+                                nbr_seeds=[2 * (1000 * rank + c) + s + 1 for c in range(P) for s in (0, 1)])
     torch.cuda.synchronize()
     t_build = time.perf_counter() - tb
     # resident batch: complexes -> micro-batches (copies of pool complexes, distinct HBM buffers)
     n_mb = args.complexes // M
-    mbs = [concat_batches([pool_gb[(m * M + j) % P] for j in range(M)]) for m in range(n_mb)]
+    mbs = [select_graphs(pool_gb, [2 * ((m * M + j) % P) + s for j in range(M) for s in (0, 1)])
+           for m in range(n_mb)]
     del pool_gb
     gb0 = mbs[0]
     h1r = [gb0.node_off[2 * j] for j in range(M)]
@@ -344,7 +406,7 @@ def main():
 
     # ---- supplementary (outside the metric): fused head prologue, contact-map all-gather ----
     prologue = head_prologue_record(h1r, h2r, l1, l2, mbs[-1], eng, dev, tdt) if not args.no_prologue else None
-    gather = allgather_record(ws, args.complexes, n_res, dev) if ws > 1 else None
+    gather = allgather_record(ws, rank, args.complexes, n_res, k, dev) if ws > 1 and args.config == "c3" else None
     value = total / elapsed
 
     # ---- per-kernel timing (HIP events on the launch stream, inside the timed region) -------
@@ -376,6 +438,8 @@ def main():
     roof["traffic"] = traffic
     bytes_c = algorithmic_bytes_per_complex(n_res, n_res, k, esz)
     hbm_frac = bytes_c * value / ws / (HBM_PEAK_GBS * 1e9)
+    flops_c = algorithmic_flops_per_complex(n_res, n_res, k, args.layers)
+    mfma_frac = flops_c * value / ws / (MFMA_PEAK_TFLOPS[args.dtype] * 1e12)
 
     out = {
         "metric": METRIC if args.config == "c3" else METRIC_C5, "value": round(value, 2), "unit": "complexes/s", "n_gpus": ws,
@@ -395,20 +459,27 @@ def main():
                    + f"; pair kernel {args.pair_kernel}"
                    + (f", pace {args.pair_pace}" if args.pair_pace else "")},
         "hbm_frac_of_peak": round(hbm_frac, 4),
+        "mfma_frac_of_peak": round(mfma_frac, 4),
+        "algorithmic_per_complex": {"bytes": bytes_c, "flops": flops_c,
+                                    "mfma_peak_tflops": MFMA_PEAK_TFLOPS[args.dtype], "hbm_peak_gbs": HBM_PEAK_GBS},
         "roofline": roof,
         "kernels": {n: {kk: round(v, 3) if isinstance(v, float) else v for kk, v in r.items()} for n, r in kern.items()},
-        "builder": {"complexes": P, "build_s": round(t_build, 4), "synth_host_s": round(t_synth, 3)},
+        "builder": {"complexes": P, "build_s": round(t_build, 4), "ms_per_complex": round(t_build / P * 1e3, 3),
+                    "synth_host_s": round(t_synth, 3),
+                    "what": "one builder call for the pool: kNN, features, topology, torch-seeded neighbour ids"},
     }
     if prologue is not None:
         out["head_prologue"] = prologue
     if gather is not None:
         out["contact_map_allgather"] = gather
     if rank == 0 and ws == 1 and not args.no_cpu:
-        threads = min(16, os.cpu_count() or 1)
+        threads, logical = physical_cores()
         cps, dt = cpu_baseline(n_res, k, args.cpu_sample, threads)
         out["cpu_baseline"] = {"value": round(cps, 4), "unit": "complexes/s", "cores": threads, "kind": "port",
-                               "sample": f"{args.cpu_sample} C3 complexes (2x{n_res} res, k={k}) after 1 warm-up, "
-                                         f"oracle fp32 GeoT both chains + pair tensor, {dt:.1f}s"}
+                               "sample": f"{args.cpu_sample} C3 complexes (2x{n_res} res, k={k}) after 3 warm-ups, "
+                                         f"oracle fp32 (DGL-style op-for-op) GeoT both chains + pair tensor, "
+                                         f"torch.inference_mode, {threads} threads = physical cores of the "
+                                         f"{logical} logical CPUs this process may use, {dt:.1f}s"}
     if rank == 0:
         print(json.dumps(out), flush=True)
     if ws > 1:

@@ -53,6 +53,8 @@ _SIGS = {
     "di_knn_topk": ([_I, _P, _P, _I, _I, _P, _P, _P], ctypes.c_int),
     "di_geo_feats": ([ctypes.POINTER(DiGeoArgs), _P], ctypes.c_int),
     "di_build_nbr_ids": ([_I, _P, _P, _P, ctypes.c_uint64, _P, _P], ctypes.c_int),
+    "di_build_nbr_ids_torch": ([_I, _P, _I, _P, _P, _P, _P, _P], ctypes.c_int),
+    "di_knn_graph": ([_I, _P, _I, _P, _I, _P, _P, _P, _P, _P], ctypes.c_int),
     "di_conformation": ([ctypes.POINTER(DiGraph), _I, _P, _P, _P, _P, _P, _P, _P], ctypes.c_int),
     "di_gemm_bias_act": ([_I, _I, _I, _I, _P, _I, _P, _P, _I, _P, _I, _P, _I, _P], ctypes.c_int),
     "di_geo_attention": ([ctypes.POINTER(DiGraph), _I, _P, _P, _P, _P, _P, _P], ctypes.c_int),
@@ -65,33 +67,44 @@ def library_path() -> str:
     return _build.LIB
 
 
+def _bind(path: str):
+    lib = ctypes.CDLL(path)
+    for name, (argtypes, restype) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.argtypes = argtypes
+        fn.restype = restype
+    if lib.di_abi_version() != 1:
+        raise RuntimeError("deepinteract_amd ABI version mismatch")
+    return lib
+
+
 def load(build_if_missing: bool = True):
-    """Load (building first if needed) the HIP library; raises if it is unavailable."""
+    """Load (building first if needed) the in-tree HIP library; raises if it is unavailable."""
     global _lib
     if _lib is not None:
         return _lib
     # torch ships its own libamdhip64.so.7: load it first so this library binds to the SAME HIP
     # runtime (same SONAME) instead of pulling /opt/rocm's copy into the process.
     import torch  # noqa: F401
-    path = os.environ.get("DI_LIB")  # a tuning variant built by build.build_variant()
-    if path:
-        if not os.path.exists(path):
-            raise RuntimeError(f"DI_LIB={path} does not exist")
-    elif not os.path.exists(_build.LIB) or (build_if_missing and not _build.up_to_date()):
+    if not os.path.exists(_build.LIB) or (build_if_missing and not _build.up_to_date()):
         if not build_if_missing:
             raise RuntimeError(f"deepinteract_amd HIP library missing: {_build.LIB}")
         _build.build()
-    lib = ctypes.CDLL(path or _build.LIB)
-    for name, (argtypes, restype) in _SIGS.items():
-        if path and not hasattr(lib, name):  # an older tuning variant (DI_LIB) may lack newer entry points
-            continue
-        fn = getattr(lib, name)
-        fn.argtypes = argtypes
-        fn.restype = restype
-    if lib.di_abi_version() != 1:
-        raise RuntimeError("deepinteract_amd ABI version mismatch")
-    _lib = lib
-    return lib
+    _lib = _bind(_build.LIB)
+    return _lib
+
+
+def load_variant(path: str):
+    """Tuning only (bench.py --lib): bind a launch-shape variant of the library built by
+    build.build_variant() instead of the in-tree one. Must run before any other load()."""
+    global _lib
+    if _lib is not None:
+        raise RuntimeError("the HIP library is already loaded")
+    import torch  # noqa: F401
+    if not os.path.exists(path):
+        raise RuntimeError(f"variant library {path} does not exist")
+    _lib = _bind(path)
+    return _lib
 
 
 def check(rc: int, what: str):

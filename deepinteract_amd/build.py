@@ -41,7 +41,7 @@ def up_to_date() -> bool:
 def build(force: bool = False, verbose: bool = True, defines=(), out: str | None = None) -> str:
     """Build the library. ``defines``/``out`` build a tuning variant (extra -D defines, or raw
     compiler flags when an entry starts with '-') into its
-    own directory, loaded with DI_LIB=<path> (kernel experiments compared in one GPU session)."""
+    own directory, loaded with bench.py --lib <path> (launch-shape knobs compared in one GPU session)."""
     lib_path = out or LIB
     if not force and not defines and out is None and up_to_date():
         return LIB

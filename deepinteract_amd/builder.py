@@ -1,12 +1,17 @@
-"""On-device residue-graph builder (host sequencing of di_knn_topk / di_geo_feats /
-di_build_nbr_ids). Replaces convert_df_to_dgl_graph's tensor work
+"""On-device residue-graph builder (host sequencing of di_knn_topk / di_knn_graph /
+di_geo_feats / di_build_nbr_ids[_torch]). Replaces convert_df_to_dgl_graph's tensor work
 (deepinteract_utils.py:386-555): Cα kNN (graph_utils.py:107-108), geometric features
 (protein_feature_utils.py:322-377 + :494-530) and neighbour-edge ids (:534-553).
 
 Input chains are dicts of backbone [N,4,3], amide_norm [N,3], dips [N,106] (see synth.py).
-Neighbour-edge ids are drawn on the device from a counter-based RNG (seeded, reproducible);
-the reference's torch.randperm stream cannot be reproduced on the GPU, so parity for the ids
-is structural (tests/test_gpu_parity.py::test_nbr_ids_structure).
+One call builds every chain of a batch with one launch per stage (one host->device copy of the
+inputs, no host synchronisation, no ATen glue between the kernels).
+
+Neighbour-edge ids, two modes:
+* ``nbr_seeds`` given (one int per chain): bit-exact with the reference — chain c's ids are the
+  ones convert_df_to_dgl_graph draws right after ``torch.manual_seed(nbr_seeds[c])``
+  (mt19937 + Fisher-Yates restated on the device, di_build_nbr_ids_torch);
+* otherwise a counter-based RNG keyed by (seed, global edge id): same distribution, cheaper.
 """
 from __future__ import annotations
 
@@ -36,48 +41,86 @@ def _node_off(sizes, device):
 
 def knn(cas, k=KNN, device="cuda"):
     """cas: list of [N_g,3] Cα coordinate tensors -> (idx [Nt,k] int32 chain-local, d2 [Nt,k] f32)."""
-    lib = _lib.load()
     sizes = [int(c.shape[0]) for c in cas]
+    ca = torch.cat([torch.as_tensor(c, dtype=torch.float32) for c in cas]).to(device).contiguous()
+    return _knn(ca, sizes, _node_off(sizes, device), k)
+
+
+def _knn(ca, sizes, off, k):
+    lib = _lib.load()
     if min(sizes) < k:
         raise ValueError(f"a chain has fewer than k={k} residues")  # dgl.knn_graph raises too
-    ca = torch.cat([torch.as_tensor(c, dtype=torch.float32) for c in cas]).to(device).contiguous()
-    off = _node_off(sizes, device)
     nt = ca.shape[0]
-    idx = torch.empty(nt, k, dtype=torch.int32, device=device)
-    d2 = torch.empty(nt, k, dtype=torch.float32, device=device)
+    idx = torch.empty(nt, k, dtype=torch.int32, device=ca.device)
+    d2 = torch.empty(nt, k, dtype=torch.float32, device=ca.device)
     _lib.check(lib.di_knn_topk(len(sizes), _p(off), _p(ca), k, max(sizes), _p(idx), _p(d2), _stream()),
                "di_knn_topk")
     return idx, d2
 
 
 def build_graph_batch(chains, k=KNN, nb=GEO_NBRHD_SIZE, seed=0, device="cuda", return_aux=False,
-                      node_count_limit=NODE_COUNT_LIMIT):
-    """Build the kernels' GraphBatch for a list of chains entirely on the device."""
+                      node_count_limit=NODE_COUNT_LIMIT, nbr_seeds=None):
+    """Build the kernels' GraphBatch for a list of chains entirely on the device.
+
+    nbr_seeds: optional per-chain torch seeds (reference-exact neighbour ids, see module doc)."""
     if nb != 2:
         raise NotImplementedError("geo_nbrhd_size=2 (the reference's setting, lit_model_predict.py:156)")
+    from .engine import gpu_device
+    device = gpu_device(device)
     lib = _lib.load()
     sizes = [int(np.asarray(c["backbone"]).shape[0]) for c in chains]
-    cat = lambda key, shape: torch.cat([torch.as_tensor(np.asarray(c[key]), dtype=torch.float32).reshape(shape)  # noqa: E731
-                                        for c in chains]).to(device).contiguous()
-    bb = cat("backbone", (-1, 4, 3))
-    am = cat("amide_norm", (-1, 3))
-    dips = cat("dips", (-1, 106))
-    nt = bb.shape[0]
-    idx, d2 = knn([bb[o:o + n, 1, :] for o, n in zip(np.cumsum([0] + sizes[:-1]), sizes)], k, device)
-    off = _node_off(sizes, device)
+    for n in sizes:
+        if n > node_count_limit:
+            raise IndexError(f"chain of {n} residues exceeds NODE_COUNT_LIMIT={node_count_limit}")
+    if nbr_seeds is not None and len(nbr_seeds) != len(sizes):
+        raise ValueError(f"{len(nbr_seeds)} neighbour seeds for {len(sizes)} chains")
+    nt, G = int(sum(sizes)), len(sizes)
+    # one packed host buffer -> one copy: [backbone 12 | amide 3 | dips 106] per residue
+    host = np.empty((nt, 121), dtype=np.float32)
+    o = 0
+    for c, n in zip(chains, sizes):
+        host[o:o + n, :12] = np.asarray(c["backbone"], dtype=np.float32).reshape(n, 12)
+        host[o:o + n, 12:15] = np.asarray(c["amide_norm"], dtype=np.float32).reshape(n, 3)
+        host[o:o + n, 15:] = np.asarray(c["dips"], dtype=np.float32).reshape(n, 106)
+        o += n
+    offs = np.zeros(G + 1, dtype=np.int64)
+    offs[1:] = np.cumsum(sizes)
+    n_off = (G + 2) // 2 * 2  # int32 offsets padded to 8 bytes, then the uint64 seeds
+    off_i32 = np.zeros(n_off, dtype=np.int32)
+    off_i32[:G + 1] = offs
+    meta = np.concatenate([off_i32.view(np.uint8),
+                           np.asarray(nbr_seeds if nbr_seeds is not None else [], dtype=np.uint64).view(np.uint8)])
+    d_in = torch.from_numpy(host).to(device, non_blocking=False)
+    d_meta = torch.from_numpy(meta).to(device)
+    off = d_meta[:4 * (G + 1)].view(torch.int32)
+    bb = d_in[:, :12].contiguous().view(nt, 4, 3)
+    am = d_in[:, 12:15].contiguous()
+    dips = d_in[:, 15:].contiguous()
+    ca = bb[:, 1, :].contiguous()
+    idx, d2 = _knn(ca, sizes, off, k)
     node_f = torch.empty(nt, 113, dtype=torch.float32, device=device)
     edge_f = torch.empty(nt * k, 28, dtype=torch.float32, device=device)
-    stats = torch.empty(len(sizes), 4, dtype=torch.float32, device=device)
-    args = _lib.DiGeoArgs(len(sizes), k, max(sizes), off.data_ptr(), bb.data_ptr(), am.data_ptr(), dips.data_ptr(),
+    stats = torch.empty(G, 4, dtype=torch.float32, device=device)
+    args = _lib.DiGeoArgs(G, k, max(sizes), off.data_ptr(), bb.data_ptr(), am.data_ptr(), dips.data_ptr(),
                           idx.data_ptr(), d2.data_ptr(), node_f.data_ptr(), edge_f.data_ptr(), stats.data_ptr())
     _lib.check(lib.di_geo_feats(ctypes.byref(args), _stream()), "di_geo_feats")
-    node_base = torch.repeat_interleave(off[:-1], torch.as_tensor(sizes, device=device))
-    src = (idx + node_base[:, None]).reshape(-1).contiguous()
-    dst = torch.arange(nt, dtype=torch.int32, device=device).repeat_interleave(k).contiguous()
+    src = torch.empty(nt * k, dtype=torch.int32, device=device)
+    dst = torch.empty(nt * k, dtype=torch.int32, device=device)
+    in_ptr = torch.empty(nt + 1, dtype=torch.int32, device=device)
+    node_pos = torch.empty(nt, dtype=torch.int32, device=device)
+    _lib.check(lib.di_knn_graph(G, _p(off), k, _p(idx), nt, _p(src), _p(dst), _p(in_ptr), _p(node_pos), _stream()),
+               "di_knn_graph")
     nbr = torch.empty(nt * k, 4, dtype=torch.int32, device=device)
-    gb = GraphBatch(src, dst, nbr, node_f, edge_f, sizes, [n * k for n in sizes], node_count_limit=node_count_limit)
-    _lib.check(lib.di_build_nbr_ids(gb.num_edges, _p(gb.src), _p(gb.dst), _p(gb.in_ptr), ctypes.c_uint64(seed),
-                                    _p(nbr), _stream()), "di_build_nbr_ids")
+    if nbr_seeds is not None:
+        seeds = d_meta[4 * n_off:]
+        _lib.check(lib.di_build_nbr_ids_torch(G, _p(off), k, _p(seeds), _p(src), _p(dst), _p(nbr), _stream()),
+                   "di_build_nbr_ids_torch")
+    else:
+        _lib.check(lib.di_build_nbr_ids(nt * k, _p(src), _p(dst), _p(in_ptr), ctypes.c_uint64(seed), _p(nbr),
+                                        _stream()), "di_build_nbr_ids")
+    gb = GraphBatch(src, dst, nbr, node_f, edge_f, sizes, [n * k for n in sizes], node_count_limit=node_count_limit,
+                    in_ptr=in_ptr, node_pos=node_pos)
+    gb._keep = (d_in, d_meta)  # inputs referenced by in-flight launches
     if return_aux:
         return gb, {"knn_idx": idx, "knn_d2": d2}
     return gb

@@ -88,11 +88,6 @@ __device__ __forceinline__ float expf_(float x) {
 // exact path keeps the IEEE division (~10 ops) for fp32 parity.
 template <bool FAST>
 __device__ __forceinline__ float silu(float x) {
-#if defined(DI_X_NOSILU)  // timing experiment only
-  if constexpr (FAST) return x;
-#elif defined(DI_X_HALFSILU)  // timing experiment only: one transcendental
-  if constexpr (FAST) return x * __expf(-x);
-#endif
   if constexpr (FAST) return x * __builtin_amdgcn_rcpf(1.0f + __expf(-x));
   else return x / (1.0f + expf(-x));
 }
@@ -325,11 +320,7 @@ __device__ __forceinline__ void mma(Act<NBO>& out, const Op<BF16T, NS>& op, cons
     for (int s = 0; s < NS; ++s) {
 #pragma unroll
       for (int bo = 0; bo < NBO; ++bo) {
-#ifdef DI_X_NOLDSA  // timing experiment only: no LDS operand reads
-        const bf16x8 af = op.f[(s + bo) % NS];
-#else
         const bf16x8 af = *reinterpret_cast<const bf16x8*>(w + (bo * NS + s) * BLK + lane * 8);
-#endif
         out.v[bo] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, op.f[s], out.v[bo], 0, 0, 0);
       }
       if constexpr (DI_MMA_ORDER == 0)
@@ -381,6 +372,13 @@ __device__ __forceinline__ void linear(Act<NBO>& out, const Act<2 * NS>& a, cons
 }
 
 // ------------------------------------------------------------------ weight staging
+// Completion of this wave's LDS-DMA pieces. buffer_load ... lds writes LDS asynchronously and is
+// tracked by vmcnt only; a workgroup barrier does not wait for it, and hipcc does not reliably emit
+// s_waitcnt vmcnt(0) in front of __syncthreads() (measured: C3 edge layers read stale weight
+// stages under load). Every barrier that publishes a DMA'd stage to the other waves is preceded
+// by this explicit wait (MI355X_MICROARCH.md, "Two waves per SIMD" item 7).
+__device__ __forceinline__ void lds_dma_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
 // Copy `nblk` packed blocks (512 elements each) from global memory to LDS with LDS-DMA
 // (global_load_lds_dwordx4: 1 KiB per wave-instruction, lane-linear destination = the packed
 // order). Issued by all NW waves of the block; completion is awaited by the next barrier.
@@ -392,9 +390,6 @@ __device__ __forceinline__ void dma_blocks(T* lds, const T* g, int nblk) {
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int loff = (threadIdx.x & 63) * 16;
   const int nkib = nblk * BLK * (int)sizeof(T) / 1024;
-#ifdef DI_X_NODMA  // timing experiment only: weights are never loaded
-  if (nkib > 0) return;
-#endif
   const __amdgpu_buffer_rsrc_t r = buf_rsrc(g);
   for (int i = wave; i < nkib; i += NW)
     __builtin_amdgcn_raw_ptr_buffer_load_lds(
@@ -461,14 +456,14 @@ struct WPipe {
     if constexpr (DBUF) {
       if constexpr (DI_DMA_PUMP > 0)
         while (dp.pi < dp.pk) dp.pump();  // pieces the stage's MFMAs did not carry
-#ifndef DI_X_NOBAR  // timing experiment only: results are wrong without the barrier
+      lds_dma_wait();
       __syncthreads();
-#endif
       cur ^= 1;
     } else {
       __syncthreads();
       dma_blocks<NW>(slot_w(0), pend, pend_n);
       if (pendv) dma_vec<NW>(slot_v(0), pendv, pendv_n / 128);
+      lds_dma_wait();
       __syncthreads();
     }
     return slot_w(cur);
@@ -511,16 +506,15 @@ struct RingPipe {
     }
   }
   __device__ __forceinline__ const T* next() {
+    lds_dma_wait();
     __syncthreads();
     cur = nxt(cur);
     return slot_w(cur);
   }
   __device__ __forceinline__ void mid() const {
-#ifndef DI_X_NOMID
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-#endif
   }
   __device__ __forceinline__ const T* w() const { return slot_w(cur); }
   __device__ __forceinline__ const float* v() const { return slot_v(cur); }
@@ -531,6 +525,7 @@ template <typename T>
 __device__ __forceinline__ void stage(T* lds, const T* g, int nblk) {
   __syncthreads();
   dma_blocks<WAVES>(lds, g, nblk);
+  lds_dma_wait();
   __syncthreads();
 }
 

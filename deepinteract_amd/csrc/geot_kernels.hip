@@ -425,13 +425,7 @@ void k_edge_layer(EdgeArgs a) {
   DmaPump* PP = pipe.pump_ptr();
   EdgeStages<DT, MODE> st{pipe, W, a.wvec, 0, false};
   pipe.issue(W + EL_S0 * BLK, EL_SIZE[0]);
-#ifdef DI_X_STAGGER
-  if (blockIdx.x & 1) __builtin_amdgcn_s_sleep(DI_X_STAGGER);
-#endif
   if (G::PP && (threadIdx.x >> 8)) pipe.mid();  // group 1 runs half a stage behind group 0
-#ifdef DI_X_PRIO
-  if (G::PP && (threadIdx.x >> 8)) __builtin_amdgcn_s_setprio(DI_X_PRIO);
-#endif
   EdgeIn<DT> in;
   {
     bool v0;

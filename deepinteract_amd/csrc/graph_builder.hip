@@ -454,9 +454,187 @@ __global__ __launch_bounds__(256) void k_nbr_ids(int Et, const int* __restrict__
   }
 }
 
+// ------------------------------------------------------------------ torch-seeded neighbour ids
+// Bit-exact restatement of the reference's draw (deepinteract_utils.py:539-546): with the torch
+// CPU generator seeded by torch.manual_seed(seed) just before convert_df_to_dgl_graph, the loop
+// calls torch.randperm(k) once per edge for the src side (E calls), then once per edge for the
+// dst side (E calls). torch's CPU randperm (ATen randperm_cpu) is Fisher-Yates over mt19937:
+//   r = 0..k-1; for i in 0..k-2: z = mt() % (k - i); swap(r[i], r[i + z])
+// so every call consumes k-1 consecutive 32-bit mt19937 outputs and only the first two (the two
+// entries kept, geo_nbrhd_size = 2, :545-546) matter:
+//   pi[0] = z0 = u0 % k;   pi[1] = (1 + z1 == z0) ? 0 : 1 + z1,  z1 = u1 % (k - 1).
+// The [DGL-ASSUMPTION] in-edge order (in_edges(v) = edge ids v*k .. v*k+k-1) makes the kept edge
+// id node*k + pi (global ids: every chain has uniform in-degree k, so its edge offset is k times
+// its node offset). mt19937 (MT19937RNGEngine.h: init_with_uint32, standard twist/tempering) is
+// serial per chain: one workgroup per chain generates the stream 624 words at a time, the twist in
+// three data-parallel phases ([0,227) reads only old words, [227,454) reads the words phase 1
+// wrote, [454,624) those of phase 2 and word 0).
+constexpr int MT_N = 624, MT_M = 397;
+constexpr uint32_t MT_A = 0x9908b0dfu, MT_UP = 0x80000000u, MT_LO = 0x7fffffffu;
+
+__device__ __forceinline__ uint32_t mt_next(uint32_t cur, uint32_t nxt, uint32_t far) {
+  const uint32_t y = (cur & MT_UP) | (nxt & MT_LO);
+  return far ^ (y >> 1) ^ ((y & 1u) ? MT_A : 0u);
+}
+
+__global__ __launch_bounds__(256) void k_nbr_ids_torch(const int* __restrict__ node_off, int k,
+                                                       const uint64_t* __restrict__ seeds,
+                                                       const int* __restrict__ src, const int* __restrict__ dst,
+                                                       int* __restrict__ nbr) {
+  __shared__ uint32_t st[MT_N];
+  __shared__ uint32_t out[MT_N];
+  __shared__ uint32_t prev_last;
+  const int g = blockIdx.x, tid = threadIdx.x;
+  const int n0 = node_off[g], n = node_off[g + 1] - n0;
+  const int64_t E = (int64_t)n * k, e0 = (int64_t)n0 * k;
+  const int64_t total = 2 * E * (k - 1);  // draws of the 2E randperm(k) calls
+  if (tid == 0) {                          // init_with_uint32(seed)
+    uint32_t s = (uint32_t)(seeds[g] & 0xffffffffull);
+    st[0] = s;
+    for (int i = 1; i < MT_N; ++i) {
+      s = 1812433253u * (s ^ (s >> 30)) + (uint32_t)i;
+      st[i] = s;
+    }
+    prev_last = 0u;
+  }
+  __syncthreads();
+  for (int64_t base = 0; base < total; base += MT_N) {
+    // twist, phase 1: i in [0, 227) from old words only
+    uint32_t v[3];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const int i = tid + 256 * q;
+      if (i < MT_N - MT_M) v[q] = mt_next(st[i], st[i + 1], st[i + MT_M]);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const int i = tid + 256 * q;
+      if (i < MT_N - MT_M) st[i] = v[q];
+    }
+    __syncthreads();
+    // phase 2: i in [227, 454): far word i-227 is new (phase 1); i+1 <= 454 is still old
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const int i = MT_N - MT_M + tid + 256 * q;
+      if (i < 2 * (MT_N - MT_M)) v[q] = mt_next(st[i], st[i + 1], st[i - (MT_N - MT_M)]);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const int i = MT_N - MT_M + tid + 256 * q;
+      if (i < 2 * (MT_N - MT_M)) st[i] = v[q];
+    }
+    __syncthreads();
+    // phase 3: i in [454, 624): far word i-227 from phase 2; word 623 wraps to the new word 0
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const int i = 2 * (MT_N - MT_M) + tid + 256 * q;
+      if (i < MT_N) v[q] = mt_next(st[i], st[i + 1 < MT_N ? i + 1 : 0], st[i - (MT_N - MT_M)]);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const int i = 2 * (MT_N - MT_M) + tid + 256 * q;
+      if (i < MT_N) st[i] = v[q];
+    }
+    __syncthreads();
+    // tempering
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const int i = tid + 256 * q;
+      if (i < MT_N) {
+        uint32_t y = st[i];
+        y ^= y >> 11;
+        y ^= (y << 7) & 0x9d2c5680u;
+        y ^= (y << 15) & 0xefc60000u;
+        y ^= y >> 18;
+        out[i] = y;
+      }
+    }
+    __syncthreads();
+    // the two kept draws of every randperm call that touches this block of the stream
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const int i = tid + 256 * q;
+      const int64_t t = base + i;
+      if (i < MT_N && t < total) {
+        const int64_t c = t / (k - 1);
+        const int j = (int)(t - c * (k - 1));
+        if (j < 2) {
+          const int side = c >= E;
+          const int64_t e = e0 + (side ? c - E : c);
+          const int node = side ? dst[e] : src[e];
+          int p;
+          if (j == 0) {
+            p = (int)(out[i] % (uint32_t)k);
+          } else {
+            const uint32_t u0 = i > 0 ? out[i - 1] : prev_last;
+            const int z0 = (int)(u0 % (uint32_t)k), z1 = (int)(out[i] % (uint32_t)(k - 1));
+            p = (1 + z1 == z0) ? 0 : 1 + z1;
+          }
+          nbr[e * 4 + 2 * side + j] = node * k + p;
+        }
+      }
+    }
+    __syncthreads();
+    if (tid == 0) prev_last = out[MT_N - 1];
+    // (the next block's first barrier orders this write before any read of prev_last)
+  }
+}
+
+// ------------------------------------------------------------------ kNN graph topology
+// [DGL-ASSUMPTION, DGL 0.6 knn_graph] edge e = v*k + r of chain g: src = idx[v, r] (chain-local)
+// + node_off[g], dst = v; in-edges of v are v*k .. v*k+k-1 (CSR row pointer v*k); node_pos = the
+// node's index inside its chain (InitEdge positional row). One thread per node.
+__global__ __launch_bounds__(256) void k_knn_graph(int num_graphs, const int* __restrict__ node_off, int k,
+                                                   const int* __restrict__ idx, int Nt, int* __restrict__ src,
+                                                   int* __restrict__ dst, int* __restrict__ in_ptr,
+                                                   int* __restrict__ node_pos) {
+  const int v = blockIdx.x * 256 + threadIdx.x;
+  if (v > Nt) return;
+  in_ptr[v] = v * k;
+  if (v == Nt) return;
+  int lo = 0, hi = num_graphs - 1;  // last g with node_off[g] <= v
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (node_off[mid] <= v) lo = mid;
+    else hi = mid - 1;
+  }
+  const int n0 = node_off[lo];
+  node_pos[v] = v - n0;
+  for (int r = 0; r < k; ++r) {
+    const int64_t e = (int64_t)v * k + r;
+    src[e] = idx[e] + n0;
+    dst[e] = v;
+  }
+}
+
 }  // namespace di
 
 using namespace di;
+
+extern "C" int di_knn_graph(int32_t num_graphs, const int32_t* node_off, int32_t k, const int32_t* knn_idx,
+                            int32_t num_nodes, int32_t* src_out, int32_t* dst_out, int32_t* in_ptr_out,
+                            int32_t* node_pos_out, void* stream) {
+  if (num_graphs <= 0 || !node_off || k <= 0 || !knn_idx || num_nodes <= 0 || !src_out || !dst_out ||
+      !in_ptr_out || !node_pos_out || (int64_t)num_nodes * k > INT32_MAX)
+    return DI_EINVAL;
+  hipLaunchKernelGGL(k_knn_graph, dim3(num_nodes / 256 + 1), dim3(256), 0, (hipStream_t)stream, num_graphs,
+                     node_off, k, knn_idx, num_nodes, src_out, dst_out, in_ptr_out, node_pos_out);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? DI_OK : (int)e;
+}
+
+extern "C" int di_build_nbr_ids_torch(int32_t num_graphs, const int32_t* node_off, int32_t k, const uint64_t* seeds,
+                                      const int32_t* src, const int32_t* dst, int32_t* nbr_out, void* stream) {
+  if (num_graphs <= 0 || num_graphs > 65535 || !node_off || k < 3 || !seeds || !src || !dst || !nbr_out)
+    return DI_EINVAL;
+  hipLaunchKernelGGL(k_nbr_ids_torch, dim3(num_graphs), dim3(256), 0, (hipStream_t)stream, node_off, k, seeds, src,
+                     dst, nbr_out);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? DI_OK : (int)e;
+}
 
 extern "C" int di_knn_topk(int32_t num_graphs, const int32_t* node_off, const float* ca, int32_t k,
                            int32_t max_nodes, int32_t* idx_out, float* d2_out, void* stream) {

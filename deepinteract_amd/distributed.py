@@ -3,49 +3,77 @@
 SURVEY.md §8e: complexes are independent (eval-mode BatchNorm, replicated weights), so the
 forward shards by complex with no exchange; the only collective is ONE all-gather of the
 contact maps after the head (the reference has no multi-GPU inference; its predict path is
-single-node DP, lit_model_predict_docker.py:183).
+single-node DP, lit_model_predict_docker.py:183, producing per-complex maps as
+lit_model_predict.py:236-239 does).
 
-* ``shard`` — size-balanced contiguous-by-rank assignment (longest-processing-time greedy on
-  L1*L2 + edges, so varlen complexes spread evenly); every rank computes the same plan.
+* ``shard`` — contiguous shards: rank r owns complexes [b_r, b_{r+1}), the boundaries chosen so
+  every rank's summed cost (L1*L2 pair work + (L1+L2)*k edge work) is as even as a contiguous
+  split allows; every rank computes the same plan from the sizes alone.
+* ``local_order`` — a rank's complexes in size-sorted order, so micro-batches group similar
+  sizes (varlen work balanced inside each launch).
 * ``all_gather_maps`` — packs each rank's [L1,L2] maps into one flat buffer (padded to the
   largest rank's element count) and issues a single ``all_gather_into_tensor``; on xGMI one big
-  collective beats many small ones (7 point-to-point links per GPU).
+  collective beats many small ones (7 point-to-point links per GPU). dtype and device are
+  arguments every rank passes identically, so a rank that owns no complex still sends a
+  buffer of the agreed type.
+* ``predict_sharded`` — the C4 driver: shard -> micro-batched forward (graph build, GeoT,
+  pair tensor / head prologue, head, contact probabilities) -> all_gather_maps.
 """
 from __future__ import annotations
 
-from typing import Sequence
+from typing import Callable, Sequence
 
 import torch
 import torch.distributed as dist
 
 
-def shard(sizes: Sequence[tuple], world: int):
-    """sizes: (L1, L2) per complex -> list (per rank) of complex indices, cost-balanced."""
-    cost = [l1 * l2 + 20 * (l1 + l2) for l1, l2 in sizes]
-    order = sorted(range(len(sizes)), key=lambda i: (-cost[i], i))
-    load = [0] * world
-    plan = [[] for _ in range(world)]
-    for i in order:
-        r = min(range(world), key=lambda q: (load[q], q))
-        plan[r].append(i)
-        load[r] += cost[i]
-    return [sorted(p) for p in plan]
+def complex_cost(l1: int, l2: int, k: int = 20) -> int:
+    return l1 * l2 + k * (l1 + l2)
 
 
-def all_gather_maps(local_maps: Sequence[torch.Tensor], plan, sizes, group=None):
-    """Gather every rank's contact maps; returns the maps of ALL complexes in global order."""
+def shard(sizes: Sequence[tuple], world: int, k: int = 20):
+    """sizes: (L1, L2) per complex -> per rank, the contiguous list of its complex indices.
+
+    Boundary b_r is the first index whose cost prefix reaches r/world of the total, so each
+    shard's cost is within one complex of the even share."""
+    n = len(sizes)
+    cost = [complex_cost(a, b, k) for a, b in sizes]
+    total = float(sum(cost))
+    bounds, acc, i = [0], 0.0, 0
+    for r in range(1, world):
+        target = total * r / world
+        while i < n and acc + cost[i] / 2.0 <= target:
+            acc += cost[i]
+            i += 1
+        bounds.append(i)
+    bounds.append(n)
+    return [list(range(bounds[r], bounds[r + 1])) for r in range(world)]
+
+
+def local_order(sizes: Sequence[tuple], indices: Sequence[int]):
+    """A rank's complexes, largest first (stable), for size-grouped micro-batches."""
+    return sorted(indices, key=lambda i: (-(sizes[i][0] * sizes[i][1]), i))
+
+
+def all_gather_maps(local_maps: Sequence[torch.Tensor], plan, sizes, dtype: torch.dtype,
+                    device, group=None):
+    """Gather every rank's contact maps; returns the maps of ALL complexes in global order.
+
+    local_maps: this rank's maps in the order of plan[rank]; dtype / device: the wire format,
+    identical on every rank (RCCL needs matching dtypes and sizes on all ranks)."""
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
+    if len(plan) != world:
+        raise ValueError(f"plan has {len(plan)} shards for a world of {world}")
     counts = [sum(sizes[i][0] * sizes[i][1] for i in p) for p in plan]
     width = max(max(counts), 1)
-    ref = local_maps[0] if len(local_maps) else None
-    dtype = ref.dtype if ref is not None else torch.float32
-    device = ref.device if ref is not None else (torch.device("cuda") if dist.get_backend(group) == "nccl"
-                                                  else torch.device("cpu"))
     send = torch.zeros(width, dtype=dtype, device=device)
+    if len(local_maps) != len(plan[rank]):
+        raise ValueError(f"rank {rank}: {len(local_maps)} maps for {len(plan[rank])} planned complexes")
     if len(local_maps):
-        flat = torch.cat([m.reshape(-1) for m in local_maps])
-        assert flat.numel() == counts[rank], (flat.numel(), counts[rank])
+        flat = torch.cat([m.reshape(-1).to(device=device, dtype=dtype) for m in local_maps])
+        if flat.numel() != counts[rank]:
+            raise ValueError(f"rank {rank}: maps hold {flat.numel()} elements, plan says {counts[rank]}")
         send[:flat.numel()] = flat
     recv = torch.empty(world * width, dtype=dtype, device=device)
     dist.all_gather_into_tensor(recv, send, group=group)
@@ -57,3 +85,50 @@ def all_gather_maps(local_maps: Sequence[torch.Tensor], plan, sizes, group=None)
             out[i] = recv[off:off + l1 * l2].view(l1, l2)
             off += l1 * l2
     return out
+
+
+def gpu_forward(model, k: int = 20, seed: int = 0):
+    """The per-micro-batch forward of ``predict_sharded`` on the HIP path: on-device graph build
+    (deepinteract_amd.builder) -> LitGINI.predict_batch -> contact probabilities. Complex i's
+    chains draw their neighbour-edge ids as torch.manual_seed(seed + 2i + s) would (s = 0, 1), so
+    the maps do not depend on how the complexes are sharded or micro-batched."""
+    from .builder import build_graph_batch
+
+    def fn(complexes, ids):
+        chains = [c for pair in complexes for c in pair]
+        dev = model.engine.device
+        gb = build_graph_batch(chains, k=k, device=dev, node_count_limit=model.cfg.node_count_limit,
+                               nbr_seeds=[seed + 2 * i + s for i in ids for s in (0, 1)])
+        with torch.no_grad():
+            _, probs = model.predict_batch(gb, [(2 * j, 2 * j + 1) for j in range(len(complexes))])
+        return probs
+
+    return fn
+
+
+def predict_sharded(complexes: Sequence, forward: Callable, micro_batch: int = 8, dtype=torch.float32,
+                    device=None, group=None):
+    """C4 driver: every rank runs ``forward`` over its contiguous shard of
+    ``complexes`` in size-sorted micro-batches, then ONE all-gather collects every complex's
+    contact map on every rank.
+
+    complexes: per complex a (chain1, chain2) pair of builder inputs (dicts with backbone
+    [N,4,3], amide_norm [N,3], dips [N,106]); forward(batch, ids) -> list of [L1, L2] maps for
+    the complexes ``batch`` (global indices ``ids``). Returns the maps of all complexes in
+    global order (views of one gathered buffer) and this rank's plan."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    sizes = [(int(len(c[0]["backbone"])), int(len(c[1]["backbone"]))) for c in complexes]
+    plan = shard(sizes, world)
+    mine = local_order(sizes, plan[rank])
+    maps = {}
+    for s in range(0, len(mine), micro_batch):
+        ids = mine[s:s + micro_batch]
+        for i, m in zip(ids, forward([complexes[i] for i in ids], ids)):
+            if tuple(m.shape) != sizes[i]:
+                raise ValueError(f"complex {i}: map {tuple(m.shape)} != {sizes[i]}")
+            maps[i] = m
+    if device is None:
+        device = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" \
+            else torch.device("cpu")
+    return all_gather_maps([maps[i] for i in plan[rank]], plan, sizes, dtype, device, group), plan

@@ -36,6 +36,24 @@ def _stream():
     return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 
 
+def gpu_device(device) -> torch.device:
+    """The ROCm device the HIP kernels run on; anything else (e.g. 'cpu') raises: the kernels
+    dereference device pointers, so host tensors must never reach them (no CPU fallback)."""
+    if not torch.cuda.is_available():
+        raise RuntimeError("deepinteract_amd HIP kernels need a ROCm GPU (no CPU fallback)")
+    dev = torch.device(device)
+    if dev.type != "cuda":
+        raise RuntimeError(f"deepinteract_amd HIP kernels run on a ROCm GPU, not on {dev}")
+    return torch.device("cuda", torch.cuda.current_device() if dev.index is None else dev.index)
+
+
+def check_on(device: torch.device, what: str, *tensors):
+    """Every tensor handed to a kernel must live on the kernel's device."""
+    for t in tensors:
+        if t is not None and t.device != device:
+            raise ValueError(f"{what}: tensor on {t.device}, the kernels run on {device}")
+
+
 class _Ticker:
     """Records (start, end) event pairs around consecutive launches on the current stream."""
 
@@ -56,11 +74,11 @@ class GeoTEngine:
     """Holds packed device weights; runs the GeoT forward for a GraphBatch."""
 
     def __init__(self, state_dict, dtype: str = "f32", cfg: GeoTConfig = GeoTConfig(), device="cuda"):
-        if not torch.cuda.is_available():
-            raise RuntimeError("deepinteract_amd GeoT kernels need a ROCm GPU (no CPU fallback)")
+        if cfg.num_gnn_hidden_channels != 128 or cfg.num_gnn_attention_heads != 4:
+            raise NotImplementedError("the GeoT kernels are specialised for 128 hidden channels, 4 heads")
+        self.device = gpu_device(device)
         self.lib = _lib.load()
         self.dtype, self.cfg = dtype, cfg
-        self.device = torch.device(device)
         self.packed = PackedGeoT(state_dict, dtype, cfg, self.device)
         self._check_blob_sizes()
         self._ws = {}
@@ -81,19 +99,33 @@ class GeoTEngine:
 
     def workspace(self, num_nodes: int, num_edges: int, slot: int = 0):
         """Per-slot activation buffers (two slots let a consumer of slot s's outputs, e.g. the
-        pair-tensor kernel on another stream, run while the next batch computes in slot 1-s)."""
-        key = (num_nodes, num_edges)
-        if slot not in self._ws or self._ws[slot][0] != key:
+        pair-tensor kernel on another stream, run while the next batch computes in slot 1-s).
+
+        Slots only grow: a batch no larger than the slot's capacity gets views of the same
+        memory. Before a slot's buffers are replaced the device is drained, because a consumer
+        on another stream may still be reading them and the caching allocator would otherwise
+        hand that memory to the next launch."""
+        cap = self._ws.get(slot)
+        if cap is None or cap[0][0] < num_nodes or cap[0][1] < num_edges:
+            if cap is not None:
+                torch.cuda.synchronize(self.device)
+            cn = max(num_nodes, cap[0][0] if cap else 0)
+            ce = max(num_edges, cap[0][1] if cap else 0)
             dt, dev, H = _TORCH_DT[self.dtype], self.device, self.cfg.num_gnn_hidden_channels
-            self._ws[slot] = (key, {
-                "h": [torch.empty(num_nodes, H, dtype=dt, device=dev) for _ in range(2)],
-                "qkv": [torch.empty(num_nodes, 3 * H, dtype=dt, device=dev) for _ in range(2)],
-                "f": [torch.empty(num_edges, H, dtype=dt, device=dev) for _ in range(2)],
-                "fn": [torch.empty(num_edges, H, dtype=dt, device=dev) for _ in range(2)],
-                "alpha": torch.empty(num_edges, 4, dtype=torch.float32, device=dev),
-                "hT": torch.empty(H, num_nodes, dtype=dt, device=dev),
+            self._ws[slot] = cap = ((cn, ce), {
+                "h": [torch.empty(cn, H, dtype=dt, device=dev) for _ in range(2)],
+                "qkv": [torch.empty(cn, 3 * H, dtype=dt, device=dev) for _ in range(2)],
+                "f": [torch.empty(ce, H, dtype=dt, device=dev) for _ in range(2)],
+                "fn": [torch.empty(ce, H, dtype=dt, device=dev) for _ in range(2)],
+                "alpha": torch.empty(ce, 4, dtype=torch.float32, device=dev),
+                "hT": torch.empty(H * cn, dtype=dt, device=dev),
             })
-        return self._ws[slot][1]
+        b, H = cap[1], self.cfg.num_gnn_hidden_channels
+        return {
+            "h": [t[:num_nodes] for t in b["h"]], "qkv": [t[:num_nodes] for t in b["qkv"]],
+            "f": [t[:num_edges] for t in b["f"]], "fn": [t[:num_edges] for t in b["fn"]],
+            "alpha": b["alpha"][:num_edges], "hT": b["hT"][:H * num_nodes].view(H, num_nodes),
+        }
 
     def forward(self, gb: GraphBatch, clone: bool = True, events=None, slot: int = 0, after_init=None):
         """-> (node feats [Nt,128], edge feats [Et,128]) in the engine dtype.
@@ -103,6 +135,8 @@ class GeoTEngine:
         after_init: optional torch.cuda.Event recorded right after the InitEdge launch (lets a
         concurrent HBM-bound consumer start once the memory-heavy prologue has passed)."""
         lib, p, dt = self.lib, self.packed, _DI_DT[self.dtype]
+        check_on(self.device, "GeoTEngine.forward", gb.src, gb.dst, gb.nbr, gb.node_f, gb.edge_f,
+                 gb.node_pos, gb.in_ptr)
         if max(gb.nodes_per_graph) > p.pos_src.shape[0]:
             # InitEdge gathers positional rows node_pos < max_num_graph_nodes (nn.Embedding, :153, :210)
             raise IndexError(f"chain of {max(gb.nodes_per_graph)} residues exceeds this model's "
@@ -159,8 +193,8 @@ class PairTensorOp:
         """blocks / waves_per_block / kernel ("rows" | "vector"): launch shape and kernel of the
         16-B-aligned path (di_pair_config; 0 / None keep the library's current setting); pace:
         store-rate pacing, s_sleep(1) per row / vector trip (di_pair_pace; None keeps it)."""
+        self.device = gpu_device(device)
         self.lib = _lib.load()
-        self.device = torch.device(device)
         self._desc_cache = {}
         k = self.KERNELS[kernel] if kernel else 0
         if (blocks or waves_per_block or k) and hasattr(self.lib, "di_pair_config"):
@@ -189,6 +223,7 @@ class PairTensorOp:
         dt = _lib.DI_BF16 if h.dtype == torch.bfloat16 else _lib.DI_F32
         if h.dtype not in (torch.float32, torch.bfloat16):
             raise TypeError(h.dtype)
+        check_on(self.device, "PairTensorOp", h, hT, out)
         d, offs, total = self.descs(h1_rows, h2_rows, l1s, l2s, hidden)
         if out is None:
             out = torch.empty(total, dtype=h.dtype, device=h.device)
@@ -218,8 +253,8 @@ class HeadPrologueOp:
     head body's input, [1, C, L1, L2] per complex, in the dtype of h."""
 
     def __init__(self, conv_w, conv_b, in_gamma, in_beta, eps=1e-6, device="cuda"):
+        self.device = gpu_device(device)
         self.lib = _lib.load()
-        self.device = torch.device(device)
         f = lambda t: t.detach().to(self.device, torch.float32).contiguous()  # noqa: E731
         self.w = f(conv_w).reshape(conv_w.shape[0], -1)  # [C, 2H(,1,1)] -> [C, 2H]
         self.b, self.g, self.beta = f(conv_b), f(in_gamma), f(in_beta)
@@ -237,6 +272,7 @@ class HeadPrologueOp:
         hidden, C = h.shape[1], self.channels
         if h.dtype not in (torch.float32, torch.bfloat16):
             raise TypeError(h.dtype)
+        check_on(self.device, "HeadPrologueOp", h, out)
         if self.w.shape[1] != 2 * hidden:
             raise ValueError(f"conv2d_1 expects {self.w.shape[1]} input channels, h gives 2x{hidden}")
         dt = _lib.DI_BF16 if h.dtype == torch.bfloat16 else _lib.DI_F32

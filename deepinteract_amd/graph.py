@@ -122,7 +122,9 @@ class GraphBatch:
     """
 
     def __init__(self, src, dst, nbr, node_f, edge_f, nodes_per_graph, edges_per_graph,
-                 node_count_limit=NODE_COUNT_LIMIT):
+                 node_count_limit=NODE_COUNT_LIMIT, in_ptr=None, node_pos=None):
+        """in_ptr / node_pos: precomputed by the device builder (di_knn_graph); when given, the
+        destination-major order is guaranteed by construction and not re-checked on the host."""
         self.src, self.dst, self.nbr = src, dst, nbr
         self.node_f, self.edge_f = node_f, edge_f
         self.nodes_per_graph = [int(x) for x in nodes_per_graph]
@@ -137,13 +139,18 @@ class GraphBatch:
             if n > self.node_count_limit:
                 # the reference's nn.Embedding(max_num_graph_nodes) raises IndexError (:153, :210)
                 raise IndexError(f"chain of {n} residues exceeds NODE_COUNT_LIMIT={self.node_count_limit}")
-        self.node_pos = torch.cat([torch.arange(n, dtype=torch.int32, device=dev)
-                                   for n in self.nodes_per_graph])
-        if self.num_edges and bool((self.dst[1:] < self.dst[:-1]).any()):
-            raise ValueError("edges must be destination-major (sorted by dst), as dgl.knn_graph emits them")
-        counts = torch.bincount(self.dst.long(), minlength=self.num_nodes)
-        self.in_ptr = torch.zeros(self.num_nodes + 1, dtype=torch.int32, device=dev)
-        self.in_ptr[1:] = torch.cumsum(counts, 0).to(torch.int32)
+        if (in_ptr is None) != (node_pos is None):
+            raise ValueError("in_ptr and node_pos come together")
+        if in_ptr is not None:
+            self.in_ptr, self.node_pos = in_ptr, node_pos
+        else:
+            self.node_pos = torch.cat([torch.arange(n, dtype=torch.int32, device=dev)
+                                       for n in self.nodes_per_graph])
+            if self.num_edges and bool((self.dst[1:] < self.dst[:-1]).any()):
+                raise ValueError("edges must be destination-major (sorted by dst), as dgl.knn_graph emits them")
+            counts = torch.bincount(self.dst.long(), minlength=self.num_nodes)
+            self.in_ptr = torch.zeros(self.num_nodes + 1, dtype=torch.int32, device=dev)
+            self.in_ptr[1:] = torch.cumsum(counts, 0).to(torch.int32)
         self.node_off = [0]
         self.edge_off = [0]
         for n, e in zip(self.nodes_per_graph, self.edges_per_graph):
@@ -201,8 +208,8 @@ class GraphBatch:
 
 
 def concat_batches(batches: Sequence[GraphBatch]) -> GraphBatch:
-    """Device-side concatenation of GraphBatches (ids re-offset; new buffers)."""
-    srcs, dsts, nbrs, nfs, efs, nn, ne = [], [], [], [], [], [], []
+    """Device-side concatenation of GraphBatches (ids re-offset; new buffers; no host sync)."""
+    srcs, dsts, nbrs, nfs, efs, ptrs, poss, nn, ne = [], [], [], [], [], [], [], [], []
     noff = eoff = 0
     for b in batches:
         srcs.append(b.src + noff)
@@ -210,10 +217,26 @@ def concat_batches(batches: Sequence[GraphBatch]) -> GraphBatch:
         nbrs.append(b.nbr + eoff)
         nfs.append(b.node_f)
         efs.append(b.edge_f)
+        ptrs.append(b.in_ptr[:-1] + eoff)
+        poss.append(b.node_pos)
         nn += b.nodes_per_graph
         ne += b.edges_per_graph
         noff += b.num_nodes
         eoff += b.num_edges
+    ptrs.append(torch.full((1,), eoff, dtype=torch.int32, device=batches[0].src.device))
     return GraphBatch(torch.cat(srcs).contiguous(), torch.cat(dsts).contiguous(), torch.cat(nbrs).contiguous(),
                       torch.cat(nfs).contiguous(), torch.cat(efs).contiguous(), nn, ne,
-                      node_count_limit=max(b.node_count_limit for b in batches))
+                      node_count_limit=max(b.node_count_limit for b in batches),
+                      in_ptr=torch.cat(ptrs).contiguous(), node_pos=torch.cat(poss).contiguous())
+
+
+def select_graphs(gb: GraphBatch, indices: Sequence[int]) -> GraphBatch:
+    """A new GraphBatch of the chains ``indices`` of ``gb`` (in that order), ids re-offset."""
+    parts = []
+    for g in indices:
+        n0, n1 = gb.node_off[g], gb.node_off[g + 1]
+        e0, e1 = gb.edge_off[g], gb.edge_off[g + 1]
+        parts.append(GraphBatch(gb.src[e0:e1] - n0, gb.dst[e0:e1] - n0, gb.nbr[e0:e1] - e0, gb.node_f[n0:n1],
+                                gb.edge_f[e0:e1], [n1 - n0], [e1 - e0], node_count_limit=gb.node_count_limit,
+                                in_ptr=gb.in_ptr[n0:n1 + 1] - e0, node_pos=gb.node_pos[n0:n1]))
+    return concat_batches(parts)

@@ -20,7 +20,7 @@ import torch
 import torch.nn as nn
 
 from .config import GeoTConfig, NODE_COUNT_LIMIT, RESIDUE_COUNT_LIMIT
-from .engine import GeoTEngine, HeadPrologueOp, PairTensorOp
+from .engine import GeoTEngine, HeadPrologueOp, PairTensorOp, gpu_device
 from .graph import GraphBatch, ResidueGraph, batch as batch_graphs, unbatch
 from .head import HeadNormOps, ResNet2DInputWithOptAttention, contact_probs
 
@@ -84,9 +84,16 @@ class LitGINI(nn.Module):
                  dtype="f32", head_dtype=torch.float32, precise_head=False, fuse_head_prologue=False,
                  head_channels_last=False, head_hip_ops=True, **kwargs):
         super().__init__()
+        if num_gnn_hidden_channels != 128 or num_gnn_attention_heads != 4:
+            # Q/K/V are Linear(H, H) whatever the head count, so a checkpoint trained with another
+            # head count would load and silently compute 4-head attention
+            raise NotImplementedError("the GeoT kernels are specialised for 128 hidden channels, 4 heads")
+        if not 0 < max_num_graph_nodes <= 4096:
+            raise NotImplementedError("max_num_graph_nodes above 4096 (the on-device kNN's row limit)")
         self.cfg = GeoTConfig(num_node_input_feats=num_node_input_feats, num_gnn_layers=num_gnn_layers,
                               num_gnn_hidden_channels=num_gnn_hidden_channels,
                               num_gnn_attention_heads=num_gnn_attention_heads, knn=knn,
+                              node_count_limit=max_num_graph_nodes,
                               num_interact_layers=num_interact_layers,
                               num_interact_hidden_channels=num_interact_hidden_channels, num_classes=num_classes)
         self.dtype = dtype
@@ -105,27 +112,50 @@ class LitGINI(nn.Module):
         # head_hip_ops: the head's InstanceNorm+ELU and SE-gate+residual passes on HIP
         # (head.HeadNormOps; NCHW only, so not with head_channels_last)
         self.head_hip_ops = head_hip_ops and not head_channels_last
-        self.prologue_op = None
         self.max_num_residues = max_num_residues
         self.interact_module = ResNet2DInputWithOptAttention(num_interact_layers, 2 * num_gnn_hidden_channels,
                                                              num_interact_hidden_channels, num_classes)
-        self.engine = None
-        self.pair_op = None
+        self._geot_sd = None     # GeoT part of the reference state dict (host copy)
+        self._prologue_w = None  # fp32 host copies of conv2d_1 / inorm_1 (fused head prologue)
+        self._dev_ops = None     # (device, GeoTEngine, PairTensorOp, HeadPrologueOp | None)
 
     def load_reference_state_dict(self, sd):
+        """Reference-keyed LitGINI state dict. The head loads into this nn.Module; the GeoT
+        weights are kept on the host and packed for the GPU the model lives on at first use
+        (so ``load`` on the CPU followed by ``.cuda()``, as lit_model_predict.py:214 does, works)."""
         head = {k[len("interact_module."):]: v for k, v in sd.items() if k.startswith("interact_module.")}
         self.interact_module.load_state_dict(head)
-        dev = next(self.interact_module.parameters()).device
-        self.engine = GeoTEngine(sd, self.dtype, self.cfg, device=dev)
-        self.pair_op = PairTensorOp(dev)
-        if self.fuse_head_prologue:
-            self.prologue_op = HeadPrologueOp.from_head(self.interact_module, dev)  # from the fp32 weights
+        self._geot_sd = {k: v.detach().to("cpu", copy=True) for k, v in sd.items()
+                         if not k.startswith("interact_module.")}
+        m = self.interact_module
+        self._prologue_w = tuple(t.detach().to("cpu", torch.float32, copy=True) for t in
+                                 (m.conv2d_1.weight, m.conv2d_1.bias, m.inorm_1.weight, m.inorm_1.bias))
+        self._prologue_eps = m.inorm_1.eps
         self.interact_module.to(dtype=self.head_dtype)
         if self.head_channels_last:
             self.interact_module.to(memory_format=torch.channels_last)
-        if self.head_hip_ops:
-            self.interact_module.use_hip_norm_ops(HeadNormOps(dev))
+        self._dev_ops = None
         return self
+
+    def _ops(self):
+        """(GeoTEngine, PairTensorOp, HeadPrologueOp | None) on the device of the model's
+        parameters, (re)built when the model has moved. A model on the CPU raises: the kernels
+        take device pointers only (no CPU fallback)."""
+        if self._geot_sd is None:
+            raise RuntimeError("load_reference_state_dict() / load_from_checkpoint() first")
+        dev = gpu_device(next(self.interact_module.parameters()).device)
+        if self._dev_ops is None or self._dev_ops[0] != dev:
+            self._dev_ops = None
+            eng = GeoTEngine(self._geot_sd, self.dtype, self.cfg, device=dev)
+            pair = PairTensorOp(dev)
+            pro = HeadPrologueOp(*self._prologue_w, self._prologue_eps, dev) if self.fuse_head_prologue else None
+            self.interact_module.use_hip_norm_ops(HeadNormOps(dev) if self.head_hip_ops else None)
+            self._dev_ops = (dev, eng, pair, pro)
+        return self._dev_ops[1:]
+
+    @property
+    def engine(self):
+        return self._ops()[0]
 
     @classmethod
     def load_from_checkpoint(cls, checkpoint_path, map_location=None, strict=True, safe_globals=None, **kwargs):
@@ -170,8 +200,9 @@ class LitGINI(nn.Module):
         """node_in_embedding + GeoT for a (batched) graph; returns per-graph node features and
         writes ndata['f'] / edata['f'] like the reference (:1660-1679)."""
         graphs = _graph_list(graph)
-        gb = GraphBatch.from_graphs(graphs, device=self.engine.device, node_count_limit=self.cfg.node_count_limit)
-        h, e = self.engine.forward(gb)
+        eng = self.engine
+        gb = GraphBatch.from_graphs(graphs, device=eng.device, node_count_limit=self.cfg.node_count_limit)
+        h, e = eng.forward(gb)
         graph.ndata["f"], graph.edata["f"] = h, e
         return [h[a:b] for a, b in zip(gb.node_off[:-1], gb.node_off[1:])]
 
@@ -207,17 +238,18 @@ class LitGINI(nn.Module):
 
     # --- batched entry ------------------------------------------------------------------
     def _forward_batch(self, gb: GraphBatch, pairs):
-        h, e = self.engine.forward(gb)
+        eng, pair_op, prologue_op = self._ops()
+        h, e = eng.forward(gb)
         off = gb.node_off
         h1r = [off[a] for a, _ in pairs]
         h2r = [off[b] for _, b in pairs]
         l1 = [gb.nodes_per_graph[a] for a, _ in pairs]
         l2 = [gb.nodes_per_graph[b] for _, b in pairs]
-        if self.prologue_op is not None:
-            _, views = self.prologue_op(h, h1r, h2r, l1, l2)
+        if prologue_op is not None:
+            _, views = prologue_op(h, h1r, h2r, l1, l2)
             logits = [self.interact_forward(v, prologue_done=True) for v in views]
         else:
-            _, views = self.pair_op(h, h1r, h2r, l1, l2, hT=self.engine.last_hT)
+            _, views = pair_op(h, h1r, h2r, l1, l2, hT=eng.last_hT)
             logits = [self.interact_forward(v) for v in views]
         return logits, h, e
 

@@ -307,6 +307,9 @@ def infer_config(sd, **overrides) -> GeoTConfig:
               num_gnn_layers=len(layers) or GeoTConfig().num_gnn_layers)
     if chunks:
         kw["num_interact_layers"] = max(chunks) + 1
+    pos = sd.get("gnn_module.0.init_edge_module.node_embedding.weight")
+    if pos is not None:  # nn.Embedding(max_num_graph_nodes, H) (deepinteract_modules.py:153)
+        kw["node_count_limit"] = int(pos.shape[0])
     for k in ("num_gnn_attention_heads", "knn", "num_interact_hidden_channels", "num_classes",
               "num_node_input_feats", "num_gnn_layers", "num_gnn_hidden_channels", "num_interact_layers"):
         if k in overrides:

@@ -22,10 +22,12 @@
  *   di_se_scale_add conv bias + SEBlock gate + residual add          deepinteract_modules.py:954-970, 1095
  *   di_channel_mean SEBlock squeeze (channel mean)                   deepinteract_modules.py:966
  *   di_knn_topk     dgl.knn_graph + topk(pairwise_squared_distance)  graph_utils.py:107-108
+ *   di_knn_graph    knn_graph's edge list / in-edge CSR (src, dst)   graph_utils.py:107, deepinteract_utils.py:442-443
  *   di_geo_feats    GeometricProteinFeatures('full') + edge/node feature assembly
  *                                                                    protein_feature_utils.py:322-377,
  *                                                                    deepinteract_utils.py:474-530
  *   di_build_nbr_ids  per-edge neighbour-edge ids                    deepinteract_utils.py:534-553
+ *   di_build_nbr_ids_torch  the same, bit-exact with torch.randperm  deepinteract_utils.py:539-546
  *
  * Module-at-a-time entry points (deepinteract_amd/layers.py; same math as the fused kernels):
  *   di_conformation   ConformationModule.forward                      deepinteract_modules.py:373-455
@@ -163,6 +165,13 @@ int di_channel_mean(di_dtype dt, const void* x, int32_t channels, int64_t hw, co
 int di_knn_topk(int32_t num_graphs, const int32_t* node_off, const float* ca /*[Nt,3]*/, int32_t k,
                 int32_t max_nodes, int32_t* idx_out, float* d2_out, void* stream);
 
+/* kNN graph topology of every chain from di_knn_topk's idx ([DGL-ASSUMPTION] DGL 0.6 knn_graph
+ * edge order, graph_utils.py:107): edge e = v*k + r has src = idx[v,r] + node_off[g] and dst = v
+ * (global ids); in_ptr_out [Nt+1] = v*k; node_pos_out [Nt] = v - node_off[g]. */
+int di_knn_graph(int32_t num_graphs, const int32_t* node_off, int32_t k, const int32_t* knn_idx,
+                 int32_t num_nodes, int32_t* src_out, int32_t* dst_out, int32_t* in_ptr_out,
+                 int32_t* node_pos_out, void* stream);
+
 typedef struct {
   int32_t num_graphs, k, max_nodes;
   const int32_t* node_off;   /* [G+1] */
@@ -181,6 +190,14 @@ int di_geo_feats(const di_geo_args* args, void* stream);
  * (seed, e); nbr_out [Et,4] global edge ids in the di_graph.nbr layout. */
 int di_build_nbr_ids(int32_t num_edges, const int32_t* src, const int32_t* dst, const int32_t* in_ptr,
                      uint64_t seed, int32_t* nbr_out, void* stream);
+
+/* neighbour-edge ids bit-exact with the reference's torch.randperm draws
+ * (deepinteract_utils.py:539-546): chain g's ids are those convert_df_to_dgl_graph produces right
+ * after torch.manual_seed(seeds[g]) (torch CPU generator = mt19937; randperm = Fisher-Yates, E src
+ * calls then E dst calls). kNN graphs only (uniform in-degree k, dst-major edges, k >= 3).
+ * node_off [G+1], seeds [G] (device); src/dst [Et] global node ids; nbr_out [Et,4] global ids. */
+int di_build_nbr_ids_torch(int32_t num_graphs, const int32_t* node_off, int32_t k, const uint64_t* seeds,
+                           const int32_t* src, const int32_t* dst, int32_t* nbr_out, void* stream);
 
 /* ---- module-at-a-time API ---------------------------------------------------------------- */
 /* ConformationModule alone (kind-6 blob): conf_out [Et,128] = F + SiLU(final_linear(...)), from the

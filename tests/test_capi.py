@@ -56,3 +56,44 @@ def test_ctypes_struct_layouts():
     assert ctypes.sizeof(_lib.DiGraph) == 8 + 5 * 8
     assert ctypes.sizeof(_lib.DiPairDesc) == 32
     assert ctypes.sizeof(_lib.DiGeoArgs) == 16 + 8 * 9
+
+
+def _declared_arg_counts():
+    """function name -> number of parameters, parsed from include/deepinteract_amd.h."""
+    src = open(os.path.join(ROOT, "include", "deepinteract_amd.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    out = {}
+    for m in re.finditer(r"\b(?:int|int64_t)\s+(di_[a-z0-9_]+)\s*\(([^)]*)\)\s*;", src):
+        args = m.group(2).strip()
+        out[m.group(1)] = 0 if args in ("", "void") else len(args.split(","))
+    return out
+
+
+def test_ctypes_signatures_match_header():
+    """Every entry point the header declares is bound in _lib._SIGS with the header's argument
+    count (a stale ctypes signature would pass garbage through the boundary)."""
+    decl = _declared_arg_counts()
+    assert set(decl) == set(declared_symbols())
+    assert set(decl) == set(_lib._SIGS), set(decl) ^ set(_lib._SIGS)
+    for name, n in decl.items():
+        assert len(_lib._SIGS[name][0]) == n, (name, len(_lib._SIGS[name][0]), n)
+
+
+def test_integration_stub_matches_header():
+    """INTEGRATION.md's raw-C (ctypes) stub passes as many arguments as the header declares."""
+    text = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    decl = _declared_arg_counts()
+    calls = re.findall(r"\blib\.(di_[a-z0-9_]+)\(", text)
+    assert calls, "INTEGRATION.md has no ctypes stub calls"
+    for m in re.finditer(r"\blib\.(di_[a-z0-9_]+)\(", text):
+        depth, i = 1, m.end()
+        while depth:
+            depth += {"(": 1, ")": -1}.get(text[i], 0)
+            i += 1
+        body = text[m.end():i - 1]
+        # count top-level commas
+        n, d = (1 if body.strip() else 0), 0
+        for ch in body:
+            d += {"(": 1, "[": 1, ")": -1, "]": -1}.get(ch, 0)
+            n += ch == "," and d == 0
+        assert n == decl[m.group(1)], (m.group(1), n, decl[m.group(1)])

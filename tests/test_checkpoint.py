@@ -63,3 +63,40 @@ def test_checkpoint_needing_other_globals_is_refused(tmp_path):
         read_checkpoint(p)
     sd, _ = read_checkpoint(p, safe_globals=[argparse.Namespace])  # explicitly allowed by the caller
     assert "node_in_embedding.weight" in sd
+
+
+def test_node_count_limit_inferred_from_positional_table():
+    from deepinteract_amd.config import GeoTConfig
+    sd = seeded_state_dict(0, GeoTConfig(node_count_limit=4096), with_head=False)
+    assert infer_config(sd).node_count_limit == 4096
+    assert infer_config(seeded_state_dict(0, with_head=False)).node_count_limit == 2304
+
+
+def test_litgini_rejects_unsupported_heads_and_width():
+    from deepinteract_amd.modules import LitGINI
+    with pytest.raises(NotImplementedError):
+        LitGINI(num_gnn_attention_heads=8)
+    with pytest.raises(NotImplementedError):
+        LitGINI(num_gnn_hidden_channels=64)
+
+
+def test_litgini_passes_max_num_graph_nodes_to_config():
+    from deepinteract_amd.modules import LitGINI
+    assert LitGINI(max_num_graph_nodes=4096).cfg.node_count_limit == 4096
+    assert LitGINI().cfg.node_count_limit == 2304
+
+
+def test_load_on_cpu_does_not_touch_the_gpu_and_refuses_cpu_compute(tmp_path):
+    """load_from_checkpoint without map_location (lit_model_predict.py:214) builds on the CPU; the
+    GeoT weights are packed for the GPU only at first use, and a CPU-resident model raises
+    rather than handing host pointers to a kernel."""
+    from deepinteract_amd.graph import ResidueGraph
+    from deepinteract_amd.modules import LitGINI
+    sd = seeded_state_dict(0)
+    p = os.path.join(tmp_path, "m.ckpt")
+    _write_ckpt(p, sd)
+    m = LitGINI.load_from_checkpoint(p).freeze()
+    assert next(m.parameters()).device.type == "cpu"
+    g = ResidueGraph(torch.zeros(40, dtype=torch.long), torch.arange(2).repeat_interleave(20), 2)
+    with pytest.raises(RuntimeError):
+        m.gnn_forward(g)

@@ -1,26 +1,42 @@
-"""World-size-2 gloo tests of the complex-sharded path (CPU): sharding plan and the single
-all-gather of contact maps."""
+"""World-size-2 gloo tests of the complex-sharded path (CPU): the contiguous sharding plan, the
+single all-gather of contact maps (incl. a rank that owns no complex, bf16 maps) and the
+composed C4 driver ``predict_sharded`` with a CPU stand-in for the GPU forward."""
 import os
 import socket
 
+import numpy as np
 import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from deepinteract_amd.distributed import all_gather_maps, shard
+from deepinteract_amd.distributed import all_gather_maps, complex_cost, local_order, predict_sharded, shard
 
 
-def test_shard_balanced_and_complete():
+def test_shard_contiguous_balanced_and_complete():
     sizes = [(1000, 1000)] * 7 + [(145, 145), (256, 256), (2000, 300)]
-    for world in (1, 2, 4, 8):
+    for world in (1, 2, 4, 8, 16):
         plan = shard(sizes, world)
-        flat = sorted(i for p in plan for i in p)
-        assert flat == list(range(len(sizes)))
+        assert len(plan) == world
+        flat = [i for p in plan for i in p]
+        assert flat == list(range(len(sizes)))          # contiguous, in order, complete
         if world <= 7:
             assert all(len(p) >= 1 for p in plan)
     plan = shard([(100, 100)] * 16, 4)
     assert [len(p) for p in plan] == [4, 4, 4, 4]
+    # cost balance: every shard within one (largest) complex of the even share
+    rng = np.random.default_rng(0)
+    sizes = [(int(a), int(b)) for a, b in rng.integers(50, 1500, size=(200, 2))]
+    cost = [complex_cost(a, b) for a, b in sizes]
+    for world in (2, 3, 8):
+        plan = shard(sizes, world)
+        loads = [sum(cost[i] for i in p) for p in plan]
+        assert max(loads) - sum(cost) / world <= max(cost)
+
+
+def test_local_order_size_sorted():
+    sizes = [(10, 10), (30, 30), (20, 20), (30, 30)]
+    assert local_order(sizes, [0, 1, 2, 3]) == [1, 3, 2, 0]
 
 
 def _free_port():
@@ -31,33 +47,87 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, sizes, q):
+def _map_of(i, l1, l2, dtype=torch.float32):
+    return (torch.full((l1, l2), float(i)) + torch.arange(l2).float() / 1000).to(dtype)
+
+
+def _worker_gather(rank, world, port, sizes, dtype, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         plan = shard(sizes, world)
-        maps = [torch.full((l1, l2), float(i)) + torch.arange(l2).float() / 1000
-                for i, (l1, l2) in enumerate(sizes) if i in plan[rank]]
-        maps = [maps[j] for j in range(len(maps))]
-        got = all_gather_maps(maps, plan, sizes)
-        ok = all(torch.equal(got[i], torch.full(sizes[i], float(i)) + torch.arange(sizes[i][1]).float() / 1000)
+        maps = [_map_of(i, *sizes[i], dtype) for i in plan[rank]]
+        got = all_gather_maps(maps, plan, sizes, dtype=dtype, device="cpu")
+        ok = all(got[i].dtype == dtype and torch.equal(got[i], _map_of(i, *sizes[i], dtype))
                  for i in range(len(sizes)))
         q.put((rank, ok))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2])
-def test_all_gather_contact_maps_gloo(world):
-    sizes = [(7, 5), (3, 9), (12, 12), (1, 4), (6, 6)]
+def _spawn(target, world, *args):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, sizes, q)) for r in range(world)]
+    procs = [ctx.Process(target=target, args=(r, world, port, *args, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = [q.get(timeout=120) for _ in procs]
+    res = [q.get(timeout=180) for _ in procs]
     for p in procs:
         p.join(timeout=60)
+    return res
+
+
+@pytest.mark.parametrize("sizes,dtype", [
+    ([(7, 5), (3, 9), (12, 12), (1, 4), (6, 6)], torch.float32),
+    ([(9, 4)], torch.bfloat16),            # world > complexes: rank 1 owns nothing, still sends bf16
+])
+def test_all_gather_contact_maps_gloo(sizes, dtype):
+    res = _spawn(_worker_gather, 2, sizes, dtype)
     assert all(ok for _, ok in res), res
+
+
+def _chain(n, seed):
+    rng = np.random.default_rng(seed)
+    return {"backbone": rng.normal(size=(n, 4, 3)).astype(np.float32),
+            "amide_norm": rng.normal(size=(n, 3)).astype(np.float32),
+            "dips": rng.random((n, 106)).astype(np.float32)}
+
+
+def _complexes():
+    lens = [(30, 22), (25, 25), (40, 21), (21, 33), (28, 30)]
+    return [(_chain(a, 2 * i), _chain(b, 2 * i + 1)) for i, (a, b) in enumerate(lens)]
+
+
+def _cpu_forward(batch, ids):
+    """Stand-in for the GPU forward: a deterministic per-complex map from the chains' coordinates
+    (independent of which rank or micro-batch computes it)."""
+    out = []
+    for c1, c2 in batch:
+        a = torch.as_tensor(c1["backbone"][:, 1, :])
+        b = torch.as_tensor(c2["backbone"][:, 1, :])
+        out.append(torch.sigmoid(-torch.cdist(a, b)))
+    return out
+
+
+def _worker_predict(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        cx = _complexes()
+        maps, plan = predict_sharded(cx, _cpu_forward, micro_batch=2)
+        ref = _cpu_forward(cx, list(range(len(cx))))
+        ok = len(maps) == len(cx) and all(torch.equal(m, r) for m, r in zip(maps, ref))
+        q.put((rank, ok, [len(p) for p in plan]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_predict_sharded_gloo():
+    """The composed C4 driver: contiguous shard -> size-sorted micro-batches -> forward -> one
+    all-gather; every rank ends with every complex's map, equal to a single-process run."""
+    res = _spawn(_worker_predict, 2)
+    assert all(ok for _, ok, _ in res), res
+    assert sum(res[0][2]) == len(_complexes())

@@ -1,0 +1,106 @@
+"""C3 parity on the benchmark's own path (BASELINE configs[2]; bench.py step()): synthetic 2x1000
+heterodimers built on the device (kNN, features, torch-seeded neighbour ids), micro-batches of 8
+complexes concatenated as the bench does, bf16 GeoT in two workspace slots on stream A, the
+'vector' pair-tensor kernel reading hT on stream B, cross-stream events between them, three
+micro-batches so slot 0 is reused after its pair tensor has drained.
+
+Checked against the oracle (fp32 CPU restatement of the reference, pinned to the reference's own
+modules by test_oracle_golden.py) on the same device-built graphs:
+* GeoT node / edge outputs of sampled complexes: bf16 bound BF16_GEOT_TOL (max-abs error / max-abs
+  reference), the stated looser bound of north_star for bf16;
+* the pair tensor: bit-exact copies of the GPU's own node features (full 512 MB tensors), and
+  sampled entries vs the oracle's pair tensor within the same bf16 bound.
+"""
+import numpy as np
+import pytest
+import torch
+
+from gpu_common import rel_max
+
+pytestmark = pytest.mark.gpu
+
+# the bf16 bound of the small cases (test_gpu_parity.BF16_TOL); measured C3 errors: DESIGN.md §2
+BF16_GEOT_TOL = 5e-2
+M, N_RES, K, N_MB = 8, 1000, 20, 3
+
+
+def _oracle_graph(gb, g):
+    n0, n1 = gb.node_off[g], gb.node_off[g + 1]
+    e0, e1 = gb.edge_off[g], gb.edge_off[g + 1]
+    nbr = gb.nbr[e0:e1].long().cpu() - e0
+    return {"num_nodes": n1 - n0, "src": gb.src[e0:e1].long().cpu() - n0, "dst": gb.dst[e0:e1].long().cpu() - n0,
+            "src_nbr": nbr[:, :2], "dst_nbr": nbr[:, 2:], "node_f": gb.node_f[n0:n1].cpu(),
+            "edge_f": gb.edge_f[e0:e1].cpu()}
+
+
+def test_c3_bench_path_bf16_two_slots_two_streams():
+    from deepinteract_amd import synth
+    from deepinteract_amd.builder import build_graph_batch
+    from deepinteract_amd.engine import GeoTEngine, PairTensorOp
+    from deepinteract_amd.graph import select_graphs
+    from deepinteract_amd.weights import seeded_state_dict
+    from oracle import geot_oracle as O
+
+    sd = seeded_state_dict(0, with_head=False)
+    eng = GeoTEngine(sd, "bf16")
+    n_cx = M * N_MB
+    chains = [c for j in range(n_cx) for c in synth.synthetic_complex(700 + j, N_RES, N_RES)]
+    pool = build_graph_batch(chains, k=K, nbr_seeds=list(range(1, 2 * n_cx + 1)))
+    mbs = [select_graphs(pool, range(2 * M * m, 2 * M * (m + 1))) for m in range(N_MB)]
+    gb0 = mbs[0]
+    h1r = [gb0.node_off[2 * j] for j in range(M)]
+    h2r = [gb0.node_off[2 * j + 1] for j in range(M)]
+    l1 = l2 = [N_RES] * M
+    pair = PairTensorOp(kernel="vector")
+    try:
+        s_geot = torch.cuda.current_stream()
+        s_pair = torch.cuda.Stream()
+        done, keep = [None, None], []
+        for m, gb in enumerate(mbs):
+            slot = m & 1
+            with torch.cuda.stream(s_geot):
+                if done[slot] is not None:
+                    s_geot.wait_event(done[slot])
+                h, e = eng.forward(gb, clone=False, slot=slot)
+                hT = eng.last_hT
+                ready = torch.cuda.Event()
+                ready.record(s_geot)
+            with torch.cuda.stream(s_pair):
+                s_pair.wait_event(ready)
+                out, views = pair(h, h1r, h2r, l1, l2, hT=hT)
+                hc, ec = h.clone(), e.clone()   # snapshot of this slot before it is reused
+                ev = torch.cuda.Event()
+                ev.record(s_pair)
+                done[slot] = ev
+            keep.append((hc, ec, views))
+        torch.cuda.synchronize()
+    finally:
+        PairTensorOp(kernel="rows")  # process-wide launch knob back to its default
+
+    errs = {}
+    for m, j in ((0, 0), (0, 5), (2, 3)):
+        hc, ec, views = keep[m]
+        gb = mbs[m]
+        ref = []
+        for g in (2 * j, 2 * j + 1):
+            with torch.no_grad():
+                n_ref, e_ref = O.geot_forward(sd, _oracle_graph(gb, g))
+            n0, n1 = gb.node_off[g], gb.node_off[g + 1]
+            e0, e1 = gb.edge_off[g], gb.edge_off[g + 1]
+            errs[f"mb{m}_c{j}_g{g % 2}_node"] = rel_max(hc[n0:n1].float().cpu().numpy(), n_ref.numpy())
+            errs[f"mb{m}_c{j}_g{g % 2}_edge"] = rel_max(ec[e0:e1].float().cpu().numpy(), e_ref.numpy())
+            ref.append(n_ref)
+        # pair tensor: bit-exact copy of the GPU's node features (the whole tensor) ...
+        a, b = hc[h1r[j]:h1r[j] + N_RES], hc[h2r[j]:h2r[j] + N_RES]
+        t = views[j]
+        assert t.shape == (1, 256, N_RES, N_RES) and t.dtype == torch.bfloat16
+        assert torch.equal(t[0, :128], a.t().unsqueeze(2).expand(128, N_RES, N_RES))
+        assert torch.equal(t[0, 128:], b.t().unsqueeze(1).expand(128, N_RES, N_RES))
+        # ... and sampled entries against the oracle's pair tensor
+        rng = np.random.default_rng(m * 100 + j)
+        idx = np.stack([rng.integers(0, 256, 4096), rng.integers(0, N_RES, 4096), rng.integers(0, N_RES, 4096)], 1)
+        pt = O.pair_tensor(ref[0], ref[1])[0].numpy()
+        got = t[0][torch.as_tensor(idx[:, 0]), torch.as_tensor(idx[:, 1]), torch.as_tensor(idx[:, 2])]
+        errs[f"mb{m}_c{j}_pair"] = rel_max(got.float().cpu().numpy(), pt[idx[:, 0], idx[:, 1], idx[:, 2]])
+    print("C3 bf16 errors (max-abs / max-abs ref):", {k: f"{v:.3e}" for k, v in errs.items()})
+    assert max(errs.values()) < BF16_GEOT_TOL, errs

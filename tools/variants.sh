@@ -7,6 +7,6 @@ cd "$R"
 ARGS="${BENCH_ARGS:---no-cpu --overlap 0 --complexes 256 --steps 2 --warmup 1}"
 specs=()
 for n in "$@"; do
-  specs+=("var${TAG}_$n:300:DI_LIB=$R/deepinteract_amd/lib/variants/$n/libdeepinteract_amd.so python bench.py $ARGS > gpurun_out/var${TAG}_$n.json")
+  specs+=("var${TAG}_$n:300:python bench.py --lib $R/deepinteract_amd/lib/variants/$n/libdeepinteract_amd.so $ARGS > gpurun_out/var${TAG}_$n.json")
 done
 "$R/tools/gpu_run.sh" "${specs[@]}"
