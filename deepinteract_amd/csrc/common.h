@@ -520,6 +520,104 @@ struct RingPipe {
   __device__ __forceinline__ const float* v() const { return slot_v(cur); }
 };
 
+// Decoupled weight ring for one 8-wave block per CU (128 rows per weight pass): NSLOT = 4 LDS
+// slots, every stage's pieces split over all 8 waves, and NO workgroup barrier per stage. Stage i
+// lives in slot i % 4; per slot one monotone LDS counter FULL counts the waves whose pieces of the
+// slot's current stage have landed (generation g = i / 4 is complete at 8 (g + 1)). A wave
+// entering stage i:
+//   1. drains its own vector memory (s_waitcnt vmcnt(0): its pieces of stage i+1, issued when it
+//      entered stage i-1, have landed) and its LDS reads (lgkmcnt(0): nothing of stage i-1 is read
+//      later), then adds 1 to FULL[(i+1) % 4];
+//   2. waits (s_sleep poll) until FULL[i % 4] is complete, i.e. every wave has entered stage i-1;
+//   3. issues its share of stage i+2 into slot (i+2) % 4 = the slot of stage i-2, which every wave
+//      finished before entering stage i-1 (step 2), so no further check is needed.
+// So a weight piece has two stages of compute to land, and a wave can run up to one stage ahead of
+// the slowest wave of its block (the two waves of a SIMD drift out of phase instead of meeting at
+// a barrier 25 times per tile). Call order: init(); issue(0); issue(1); then per stage i:
+// enter(i); if (i + 2 < total) issue(i + 2, ...); compute with w(i) / v(i).
+template <typename T, int CAP, int VCAP, int NW_ = 8>
+struct FullRing {
+  static constexpr int NW = NW_, NSLOT = 4;
+  static constexpr int SLOT_BYTES = CAP * BLK * (int)sizeof(T) + VCAP * 4;
+  static constexpr int LDS_BYTES = NSLOT * SLOT_BYTES + 16;  // + 4 FULL counters
+  char* base;
+  uint32_t* full;
+  int wave;
+  __device__ explicit FullRing(void* lds)
+      : base(reinterpret_cast<char*>(lds)),
+        full(reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(lds) + NSLOT * SLOT_BYTES)) {
+    wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  }
+  __device__ __forceinline__ void init() {
+    if (threadIdx.x < NSLOT) full[threadIdx.x] = 0u;
+    __syncthreads();
+  }
+  __device__ __forceinline__ T* slot_w(int i) const { return reinterpret_cast<T*>(base + (i & 3) * SLOT_BYTES); }
+  __device__ __forceinline__ float* slot_v(int i) const {
+    return reinterpret_cast<float*>(base + (i & 3) * SLOT_BYTES + CAP * BLK * (int)sizeof(T));
+  }
+  // this wave's share of stage i: 1-KiB pieces wave, wave + 8, ...; the 512-B bias vector by the
+  // wave whose turn it is (i % 8), as one half-wave piece
+  __device__ __forceinline__ void issue(int i, const T* g, int nblk, const float* gv) {
+    const int loff = (threadIdx.x & 63) * 16;
+    const int nkib = nblk * BLK * (int)sizeof(T) / 1024;
+    const __amdgpu_buffer_rsrc_t r = buf_rsrc(g);
+    char* dst = reinterpret_cast<char*>(slot_w(i));
+    for (int p = wave; p < nkib; p += NW)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)(dst + p * 1024), 16,
+                                               loff, p * 1024, 0, 0);
+    if (gv != nullptr && wave == i % NW && (threadIdx.x & 63) < 32)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(buf_rsrc(gv),
+                                               (__attribute__((address_space(3))) void*)slot_v(i), 16,
+                                               (threadIdx.x & 63) * 16, 0, 0, 0);
+  }
+  // pumped form (DI_DMA_PUMP > 0): defer() records this wave's pieces of stage i, mma() issues
+  // one of them every DI_DMA_PUMP MFMAs (so the CU's LDS-DMA path is not flooded by 8 waves
+  // issuing a whole stage at once), flush() issues what the stage's MFMAs did not carry
+  DmaPump dp;
+  __device__ __forceinline__ DmaPump* pump_ptr() { return DI_DMA_PUMP > 0 ? &dp : nullptr; }
+  __device__ __forceinline__ void defer(int i, const T* g, int nblk, const float* gv) {
+    dp.src = reinterpret_cast<const char*>(g);
+    dp.dst = reinterpret_cast<char*>(slot_w(i));
+    dp.pi = wave;
+    dp.pk = nblk * BLK * (int)sizeof(T) / 1024;
+    dp.step = NW;
+    if (gv != nullptr && wave == i % NW && (threadIdx.x & 63) < 32)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(buf_rsrc(gv),
+                                               (__attribute__((address_space(3))) void*)slot_v(i), 16,
+                                               (threadIdx.x & 63) * 16, 0, 0, 0);
+  }
+  __device__ __forceinline__ void flush() {
+    while (dp.pi < dp.pk) dp.pump();
+  }
+  __device__ __forceinline__ void signal(int i) {  // my pieces of stage i have landed
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    if ((threadIdx.x & 63) == 0)
+      __hip_atomic_fetch_add(full + (i & 3), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+  __device__ __forceinline__ void wait(int i) {  // every wave's pieces of stage i have landed
+    const uint32_t target = (uint32_t)NW * (uint32_t)((i >> 2) + 1);
+    while (__builtin_amdgcn_readfirstlane(
+               __hip_atomic_load(full + (i & 3), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) < target)
+      __builtin_amdgcn_s_sleep(1);
+    asm volatile("" ::: "memory");
+  }
+  // prologue: stages 0 and 1 issued by every wave; signal both, wait for stage 0
+  __device__ __forceinline__ void start() {
+    signal(0);
+    signal(1);
+    wait(0);
+  }
+  // entering stage i >= 1: signal stage i+1 (own pieces issued at stage i-1), wait stage i
+  __device__ __forceinline__ void enter(int i, bool has_next) {
+    if (has_next) signal(i + 1);
+    else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    wait(i);
+  }
+  __device__ __forceinline__ const T* w(int i) const { return slot_w(i); }
+  __device__ __forceinline__ const float* v(int i) const { return slot_v(i); }
+};
+
 // Single synchronous stage (kept for simple kernels).
 template <typename T>
 __device__ __forceinline__ void stage(T* lds, const T* g, int nblk) {

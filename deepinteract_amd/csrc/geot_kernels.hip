@@ -289,61 +289,115 @@ __constant__ int EL_VEC[25] = {-1, ELV_OM, -1,
 constexpr int EL_NSTAGE_CONF = 18, EL_NSTAGE_FINAL = 19, EL_NSTAGE = 25;
 constexpr int EL_CAP = 36;
 
-// bf16: 8-wave ping-pong blocks (RingPipe, one block per CU, 128 rows per weight pass);
+// bf16 (the benchmark path): two independent 4-wave blocks per CU, each double-buffering its
+// weight stages (WPipe). DI_EDGE_RING=1 instead runs one 8-wave block per CU (128 rows per weight
+// pass, half the LDS-DMA bytes per CU) on the decoupled 4-slot FullRing (common.h: no per-stage
+// barrier, two stages of DMA lead). Measured (C3 micro-batch, serial, rocprof-consistent HIP
+// events): ring 518-533 us vs 501-504 us for the two 4-wave blocks, ring + pumped pieces
+// (DI_DMA_PUMP 2/4/8) 523-556 us: the two waves of a SIMD from two independent blocks keep more
+// phase diversity than the halved weight stream buys.
 // fp32 parity path: 4-wave blocks with synchronous stages (WPipe).
-#ifndef DI_EDGE_PP
-#define DI_EDGE_PP 0  // measured: 8-wave ping-pong 631 us vs 498 us for two 4-wave blocks per CU (C3 edge layer)
+#ifndef DI_EDGE_RING
+#define DI_EDGE_RING 0
+#endif
+#ifndef DI_RING_PRIO
+#define DI_RING_PRIO 0
+#endif
+#ifndef DI_RING_STAGGER
+#define DI_RING_STAGGER 0  // x 512 clocks of start delay for waves 4-7
 #endif
 template <class DT>
 struct EdgeGeo {
-  static constexpr bool PP = DT::kBF16 && DI_EDGE_PP;
-  static constexpr int NW = PP ? 8 : Geo<DT>::NW;
+  static constexpr bool RING = DT::kBF16 && DI_EDGE_RING;
+  static constexpr int NW = RING ? 8 : Geo<DT>::NW;
   static constexpr int THREADS = 64 * NW;
   static constexpr int ROWS = ROWS_PER_WAVE * NW;
 };
 template <class DT>
-using EdgePipe = std::conditional_t<EdgeGeo<DT>::PP, RingPipe<typename DT::T, EL_CAP, 128>,
+using EdgePipe = std::conditional_t<EdgeGeo<DT>::RING, FullRing<typename DT::T, EL_CAP, 128>,
                                     WPipe<typename DT::T, Geo<DT>::NW, Geo<DT>::DBUF, EL_CAP, 128>>;
 template <class DT>
 constexpr int edge_lds_bytes() {
-  return (EdgeGeo<DT>::PP ? 3 : (Geo<DT>::DBUF ? 2 : 1)) * EdgePipe<DT>::SLOT_BYTES;
+  if constexpr (EdgeGeo<DT>::RING) return EdgePipe<DT>::LDS_BYTES;
+  else return (Geo<DT>::DBUF ? 2 : 1) * EdgePipe<DT>::SLOT_BYTES;
 }
 
 // MODE: 0 intermediate layer, 1 final layer, 2 conformation module alone (di_conformation)
+template <int MODE>
+constexpr int edge_nstage() { return MODE == 2 ? EL_NSTAGE_CONF : (MODE == 1 ? EL_NSTAGE_FINAL : EL_NSTAGE); }
+
+// The weight-stage sequence of a block's tiles: next() makes the next stage current (its weights
+// w(), its bias vector v()) and keeps the DMA stream ahead of it (ring: two stages, barrier pipe:
+// one); the sequence runs on across the block's tiles (stage 0 of tile t+1 follows the last stage
+// of tile t).
 template <class DT, int MODE>
 struct EdgeStages {
   using T = typename DT::T;
+  static constexpr int NS = edge_nstage<MODE>();
   EdgePipe<DT>& pipe;
   const T* W;
   const float* V;
-  int i;      // stage whose DMA is pending / current
-  bool more;  // another tile follows: the last stage wraps to stage 0 of the next tile
-  // wait for stage i (already issued), start stage i+1; pipe.w()/pipe.v() = stage i
-  __device__ const T* next() {
-    const T* w = pipe.next();
-    const int n = MODE == 2 ? EL_NSTAGE_CONF : (MODE == 1 ? EL_NSTAGE_FINAL : EL_NSTAGE);
-    const int ni = i + 1 < n ? i + 1 : (more ? 0 : -1);
-    if (ni >= 0) {
-      const int vo = EL_VEC[ni];
-      pipe.issue(W + EL_ORDER[ni] * BLK, EL_SIZE[ni], vo >= 0 ? V + vo : nullptr, 128);
+  int gi;     // global index of the next stage to make current
+  int total;  // stages this block runs (tiles x NS)
+  const float* vcur;
+  __device__ void issue(int i, bool pumped = false) {
+    const int s = i % NS;
+    const int vo = EL_VEC[s];
+    if constexpr (EdgeGeo<DT>::RING) {
+      if (pumped) pipe.defer(i, W + EL_ORDER[s] * BLK, EL_SIZE[s], vo >= 0 ? V + vo : nullptr);
+      else pipe.issue(i, W + EL_ORDER[s] * BLK, EL_SIZE[s], vo >= 0 ? V + vo : nullptr);
+    } else {
+      pipe.issue(W + EL_ORDER[s] * BLK, EL_SIZE[s], vo >= 0 ? V + vo : nullptr, 128);
     }
-    ++i;
-    return w;
   }
+  // weight-piece pump handed to the MFMA loops (nullptr: pieces were issued in one burst)
+  __device__ DmaPump* pp() {
+    if constexpr (EdgeGeo<DT>::RING) return pipe.pump_ptr();
+    else return nullptr;
+  }
+  __device__ void begin() {  // before the first next()
+    if constexpr (EdgeGeo<DT>::RING) {
+      pipe.init();
+      issue(0);
+      if (total > 1) issue(1);
+    } else {
+      issue(0);
+    }
+  }
+  __device__ const T* next() {
+    const int i = gi++;
+    if constexpr (EdgeGeo<DT>::RING) {
+      if (i == 0) {
+        pipe.signal(0);
+        if (total > 1) pipe.signal(1);
+        pipe.wait(0);
+      } else {
+        if constexpr (DI_DMA_PUMP > 0) pipe.flush();  // pieces of stage i+1 the last stage did not carry
+        pipe.enter(i, i + 1 < total);
+      }
+      if (i + 2 < total) issue(i + 2, DI_DMA_PUMP > 0);
+      vcur = pipe.v(i);
+      return pipe.w(i);
+    } else {
+      const T* w = pipe.next();
+      if (i + 1 < total) issue(i + 1);
+      vcur = pipe.v();
+      return w;
+    }
+  }
+  __device__ const float* v() const { return vcur; }
 };
 
 template <class DT, int MODE>
 __device__ __forceinline__ void res_block(Act<8>& x, EdgeStages<DT, MODE>& st, int lane, int g) {
   constexpr bool FAST = DT::kBF16;
-  DmaPump* PP = st.pipe.pump_ptr();
   Act<8> y = x;
 #pragma unroll 1
   for (int l = 0; l < 3; ++l) {
     const typename DT::T* w = st.next();
     Act<8> t;
-    init_vec_lds(t, st.pipe.v(), g);
-    linear<DT, 8, 4>(t, y, w, lane, PP);
-    st.pipe.mid();
+    init_vec_lds(t, st.v(), g);
+    linear<DT, 8, 4>(t, y, w, lane, st.pp());
     silu2_<8, FAST>(t);  // log2 units: folded into the next linear / the residual fma
     y = t;
   }
@@ -420,12 +474,19 @@ void k_edge_layer(EdgeArgs a) {
   // first tile: XCD-aware when every block owns one tile; persistent grids stride by gridDim.x
   const int first = (int)gridDim.x >= ntiles ? xcd_tile(blockIdx.x, ntiles) : (int)blockIdx.x;
   if (first >= ntiles) return;  // padding block of the XCD-aware grid (uniform, before any DMA)
+  const int my_tiles = (ntiles - first + (int)gridDim.x - 1) / (int)gridDim.x;
 
   EdgePipe<DT> pipe(lds);
-  DmaPump* PP = pipe.pump_ptr();
-  EdgeStages<DT, MODE> st{pipe, W, a.wvec, 0, false};
-  pipe.issue(W + EL_S0 * BLK, EL_SIZE[0]);
-  if (G::PP && (threadIdx.x >> 8)) pipe.mid();  // group 1 runs half a stage behind group 0
+  EdgeStages<DT, MODE> st{pipe, W, a.wvec, 0, my_tiles * EdgeStages<DT, MODE>::NS, nullptr};
+  st.begin();
+  if constexpr (G::RING) {
+    // the younger half (waves 4-7) of the block: static priority and/or a start delay, so the two
+    // waves of a SIMD run out of phase (MI355X_MICROARCH.md "Two waves per SIMD", items 4 and 9)
+    const bool young = __builtin_amdgcn_readfirstlane(threadIdx.x) >= 256;
+    if (DI_RING_PRIO && young) __builtin_amdgcn_s_setprio(1);
+    if (DI_RING_STAGGER > 0 && young)
+      for (int t = 0; t < DI_RING_STAGGER; ++t) __builtin_amdgcn_s_sleep(8);
+  }
   EdgeIn<DT> in;
   {
     bool v0;
@@ -441,8 +502,6 @@ void k_edge_layer(EdgeArgs a) {
     const bool more = tile + (int)gridDim.x < ntiles;
     bool vn;
     const int en = tile_edge<DT>(more ? tile + gridDim.x : tile, a.Et, vn);
-    st.i = 0;
-    st.more = more;
     const T* f_row = reinterpret_cast<const T*>(a.f_in) + (int64_t)e * HID;
 
     const int4 nb = in.nb;
@@ -457,12 +516,12 @@ void k_edge_layer(EdgeArgs a) {
     {
       Act<4> t1;
       zero(gate);
-      mma<4, 1>(gate, gop, w + 8 * BLK, lane, PP);
+      mma<4, 1>(gate, gop, w + 8 * BLK, lane, st.pp());
       zero(t1);
-      mma<4, 1>(t1, gop, w + 12 * BLK, lane, PP);
+      mma<4, 1>(t1, gop, w + 12 * BLK, lane, st.pp());
       mul_(gate, t1);
       zero(t1);
-      mma<4, 1>(t1, gop, w + 16 * BLK, lane, PP);
+      mma<4, 1>(t1, gop, w + 16 * BLK, lane, st.pp());
       mul_(gate, t1);
     }
     Act<4> s;
@@ -481,43 +540,39 @@ void k_edge_layer(EdgeArgs a) {
       asm volatile("" ::: "memory");
       Act<8> dg;
       zero(dg);
-      mma<8, 1>(dg, gop, w, lane, PP);
+      mma<8, 1>(dg, gop, w, lane, st.pp());
 #pragma unroll
       for (int b = 0; b < 8; ++b)
 #pragma unroll
         for (int q = 0; q < 4; ++q) x.v[b][q] *= dg.v[b][q];  // gathered rows are silu(nbr_linear(F))
       Act<4> y;
       zero(y);
-      linear<DT, 4, 4>(y, x, w + 20 * BLK, lane, PP);  // downward_proj
+      linear<DT, 4, 4>(y, x, w + 20 * BLK, lane, st.pp());  // downward_proj
 #pragma unroll
       for (int b = 0; b < 4; ++b)
 #pragma unroll
         for (int q = 0; q < 4; ++q) s.v[b][q] += silu2<FAST>(y.v[b][q]) * gate.v[b][q];
-      if (j == 1) pipe.mid();
     }
     Act<8> x;
     w = st.next();  // stage 1: upward_proj (+ orig_msg_linear bias)
     zero(x);
-    linear<DT, 8, 2>(x, s, w, lane, PP);
-    pipe.mid();
+    linear<DT, 8, 2>(x, s, w, lane, st.pp());
     silu2_<8, FAST>(x);
     {
       Act<8> bo;
-      init_vec_lds(bo, pipe.v(), g);
+      init_vec_lds(bo, st.v(), g);
 #pragma unroll
       for (int b = 0; b < 8; ++b) x.v[b] = silu2_unit<FAST>() * x.v[b] + bo.v[b];
     }
     w = st.next();  // stage 2: orig_msg_linear(res) + nbr
-    mma<8, 4>(x, fr.operand(f_row, g), w, lane, PP);
-    pipe.mid();
+    mma<8, 4>(x, fr.operand(f_row, g), w, lane, st.pp());
     res_block<DT, MODE>(x, st, lane, g);
     res_block<DT, MODE>(x, st, lane, g);
     {
       w = st.next();  // res_connect_linear
       Act<8> y;
-      init_vec_lds(y, pipe.v(), g);
-      linear<DT, 8, 4>(y, x, w, lane, PP);
-      pipe.mid();
+      init_vec_lds(y, st.v(), g);
+      linear<DT, 8, 4>(y, x, w, lane, st.pp());
       silu2_<8, FAST>(y);
       fr.act(x, f_row, g);
       add_scaled_(x, y, silu2_unit<FAST>());
@@ -529,14 +584,12 @@ void k_edge_layer(EdgeArgs a) {
       if ((FINAL || CONF) && more) in.load_ids(a, en);
       Act<8> fg;
       zero(fg);
-      mma<8, 1>(fg, gop, w, lane, PP);
+      mma<8, 1>(fg, gop, w, lane, st.pp());
       mul_(x, fg);
-      pipe.mid();
       w = st.next();  // final_linear
       Act<8> y;
-      init_vec_lds(y, pipe.v(), g);
-      linear<DT, 8, 4>(y, x, w, lane, PP);
-      pipe.mid();
+      init_vec_lds(y, st.v(), g);
+      linear<DT, 8, 4>(y, x, w, lane, st.pp());
       silu2_<8, FAST>(y);
       fr.act(x, f_row, g);
       add_scaled_(x, y, silu2_unit<FAST>());  // conformation output
@@ -555,9 +608,8 @@ void k_edge_layer(EdgeArgs a) {
     if (FINAL && more) in.load_rest(a, en, g);  // F of this tile is dead from here on
     if (!FINAL && more) in.load_ids(a, en);
     Act<8> p;
-    init_vec_lds(p, pipe.v(), g);
-    linear<DT, 8, 4>(p, x, w, lane, PP);
-    pipe.mid();
+    init_vec_lds(p, st.v(), g);
+    linear<DT, 8, 4>(p, x, w, lane, st.pp());
     {
       Act<8> kq, qd;
       kr.to_act(kq);
@@ -581,9 +633,8 @@ void k_edge_layer(EdgeArgs a) {
       // ---- edge output: e = in + O_e(e_out); e = e + FFN(BN2e(e)) (:697-724)
       w = st.next();  // O_edge_feats
       Act<8> e1;
-      init_vec_lds(e1, pipe.v(), g);
-      linear<DT, 8, 4>(e1, p, w, lane, PP);
-      pipe.mid();
+      init_vec_lds(e1, st.v(), g);
+      linear<DT, 8, 4>(e1, p, w, lane, st.pp());
       {
         Act<8> fa;
         fr.act(fa, f_row, g);
@@ -596,26 +647,22 @@ void k_edge_layer(EdgeArgs a) {
         w = st.next();  // edge_feats_MLP.0 (BN2e folded), hidden half
         if (half == 0 && more) in.load_rest(a, en, g);  // F of this tile is dead from here on
         Act<8> t;
-        init_vec_lds(t, pipe.v(), g);
-        linear<DT, 8, 4>(t, e1, w, lane, PP);
-        pipe.mid();
-        silu2_<8, FAST>(t);
+        init_vec_lds(t, st.v(), g);
+        linear<DT, 8, 4>(t, e1, w, lane, st.pp());
+          silu2_<8, FAST>(t);
         w = st.next();  // edge_feats_MLP.3, input half
-        linear<DT, 8, 4>(o, t, w, lane, PP);
-        pipe.mid();
-      }
+        linear<DT, 8, 4>(o, t, w, lane, st.pp());
+        }
       add_(e1, o);
       if (valid) store_row(e1, reinterpret_cast<T*>(a.f_out) + (int64_t)e * HID, g);
       w = st.next();  // next layer's silu(nbr_linear(.))
       Act<8> fn;
-      init_vec_lds(fn, pipe.v(), g);
-      linear<DT, 8, 4>(fn, e1, w, lane, PP);
-      pipe.mid();
+      init_vec_lds(fn, st.v(), g);
+      linear<DT, 8, 4>(fn, e1, w, lane, st.pp());
       silu_<8, FAST>(fn);
       if (valid) store_row(fn, reinterpret_cast<T*>(a.fn_out) + (int64_t)e * HID, g);
     }
   }
-  if (G::PP && !(threadIdx.x >> 8)) pipe.mid();  // matches group 1's leading mid()
 }
 
 // ================================================================ fused node layer
@@ -640,9 +687,35 @@ __global__ __launch_bounds__(THREADS, 2) void k_node_layer(NodeArgs a) {
   Act<8> wv;
   zero(wv);
   floatx4 z = {0.f, 0.f, 0.f, 0.f};
+  // In-edges in groups of UNR: the group's source ids, alphas and V[src] rows are all in flight
+  // before the first product (one latency per group instead of two dependent ones per edge); the
+  // products are still added one edge at a time in edge order (the reference's summation order).
+  constexpr int UNR = DT::kBF16 ? 4 : 2;
   const int e0 = a.in_ptr[v], e1 = a.in_ptr[v + 1];
+  int e = e0;
 #pragma unroll 1
-  for (int e = e0; e < e1; ++e) {
+  for (; e + UNR <= e1; e += UNR) {
+    int sid[UNR];
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) sid[u] = a.src[e + u];
+    floatx4 al[UNR];
+    RawRow<T> vr[UNR];
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      al[u] = ld4(a.alpha + (int64_t)(e + u) * 4);
+      vr[u].load(qkv + (int64_t)sid[u] * 3 * HID + 2 * HID, g);
+    }
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      Act<8> vv;
+      vr[u].to_act(vv);
+#pragma unroll
+      for (int b = 0; b < 8; ++b) wv.v[b] += al[u][b >> 1] * vv.v[b];
+      z += al[u];
+    }
+  }
+#pragma unroll 1
+  for (; e < e1; ++e) {
     const floatx4 al = ld4(a.alpha + (int64_t)e * 4);
     Act<8> vv;
     load_row(vv, qkv + (int64_t)a.src[e] * 3 * HID + 2 * HID, g);
@@ -791,8 +864,10 @@ extern "C" int di_edge_layer(const di_graph* g, di_dtype dt, int final_layer, co
 #define DI_EDGE_PERSIST 0
 #endif
     const int tiles = grid_rows(a.Et, EdgeGeo<BF16T>::ROWS);
-    const int resident = DI_EDGE_PERSIST ? (EdgeGeo<BF16T>::PP ? 1 : 2) * num_cus() : xcd_grid(tiles);
-    dim3 grid(DI_EDGE_PERSIST && tiles > resident ? resident : xcd_grid(tiles)), block(EdgeGeo<BF16T>::THREADS);
+    // ring: one 8-wave block per CU, persistent over the tiles; barrier pipe: 2 blocks per CU
+    const int resident = (EdgeGeo<BF16T>::RING ? 1 : 2) * num_cus();
+    const bool persist = EdgeGeo<BF16T>::RING || DI_EDGE_PERSIST;
+    dim3 grid(persist && tiles > resident ? resident : xcd_grid(tiles)), block(EdgeGeo<BF16T>::THREADS);
     if (final_layer) hipLaunchKernelGGL((k_edge_layer<BF16T, 1>), grid, block, 0, s, a);
     else hipLaunchKernelGGL((k_edge_layer<BF16T, 0>), grid, block, 0, s, a);
   } else {

@@ -22,9 +22,10 @@ from gpu_common import chain_arrays, chain_item, load_case, rel_max
 
 pytestmark = pytest.mark.gpu
 F32_TOL = 1e-4
-# bf16 GeoT (fp32 head) vs the fp32 reference: measured values in DESIGN.md §2
-BF16_LOGIT_TOL = 5e-2
-BF16_PROB_ABS = 5e-2
+# bf16 GeoT (fp32 head) vs the fp32 reference, measured on MI355X: logits <= 1.32e-2
+# relative (max-abs error / max-abs reference), contact probabilities <= 1.0e-2 absolute; bounds ~2x
+BF16_LOGIT_TOL = 3e-2
+BF16_PROB_ABS = 2e-2
 
 
 @pytest.fixture(scope="module")

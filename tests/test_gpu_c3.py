@@ -19,8 +19,9 @@ from gpu_common import rel_max
 
 pytestmark = pytest.mark.gpu
 
-# the bf16 bound of the small cases (test_gpu_parity.BF16_TOL); measured C3 errors: DESIGN.md §2
-BF16_GEOT_TOL = 5e-2
+# measured on MI355X: node <= 6.8e-3, edge <= 4.9e-3, pair samples <= 7.0e-3 of the
+# max-abs reference; stated bound ~2x the largest measured value
+BF16_GEOT_TOL = 1.5e-2
 M, N_RES, K, N_MB = 8, 1000, 20, 3
 
 
