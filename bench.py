@@ -480,6 +480,13 @@ def main():
                                          f"oracle fp32 (DGL-style op-for-op) GeoT both chains + pair tensor, "
                                          f"torch.inference_mode, {threads} threads = physical cores of the "
                                          f"{logical} logical CPUs this process may use, {dt:.1f}s"}
+        omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+        if 0 < omp < threads:
+            # the host's per-job CPU share (OMP_NUM_THREADS) on a shared box: more threads than the
+            # share can be slower; reported beside the protocol's number, not instead of it
+            cps2, dt2 = cpu_baseline(n_res, k, 5, omp, warmup=1)
+            out["cpu_baseline"]["at_job_cpu_share"] = {"threads": omp, "value": round(cps2, 4),
+                                                       "sample": f"5 complexes after 1 warm-up, {dt2:.1f}s"}
     if rank == 0:
         print(json.dumps(out), flush=True)
     if ws > 1:

@@ -39,6 +39,25 @@ def _node_off(sizes, device):
     return torch.as_tensor(off, device=device)
 
 
+_stage = {"buf": None, "event": None}
+
+
+def _pinned(words):
+    """Reusable pinned host staging buffer of at least `words` 4-byte words (float32 view)."""
+    st = _stage
+    if st["event"] is not None:
+        st["event"].synchronize()  # the previous copy out of the buffer has finished
+    if st["buf"] is None or st["buf"].numel() < words:
+        st["buf"] = torch.empty(max(words, 1 << 20), dtype=torch.float32, pin_memory=True)
+    return st["buf"]
+
+
+def _keep_until_copied(buf):
+    ev = torch.cuda.Event()
+    ev.record()
+    _stage["event"] = ev
+
+
 def knn(cas, k=KNN, device="cuda"):
     """cas: list of [N_g,3] Cα coordinate tensors -> (idx [Nt,k] int32 chain-local, d2 [Nt,k] f32)."""
     sizes = [int(c.shape[0]) for c in cas]
@@ -75,27 +94,32 @@ def build_graph_batch(chains, k=KNN, nb=GEO_NBRHD_SIZE, seed=0, device="cuda", r
     if nbr_seeds is not None and len(nbr_seeds) != len(sizes):
         raise ValueError(f"{len(nbr_seeds)} neighbour seeds for {len(sizes)} chains")
     nt, G = int(sum(sizes)), len(sizes)
-    # one packed host buffer -> one copy: [backbone 12 | amide 3 | dips 106] per residue
-    host = np.empty((nt, 121), dtype=np.float32)
-    o = 0
-    for c, n in zip(chains, sizes):
-        host[o:o + n, :12] = np.asarray(c["backbone"], dtype=np.float32).reshape(n, 12)
-        host[o:o + n, 12:15] = np.asarray(c["amide_norm"], dtype=np.float32).reshape(n, 3)
-        host[o:o + n, 15:] = np.asarray(c["dips"], dtype=np.float32).reshape(n, 106)
-        o += n
+    # one host buffer -> one copy: [backbone nt x 12 | amide nt x 3 | dips nt x 106 | node offsets |
+    # seeds], every field contiguous (memcpy-speed packing), staged in reusable pinned memory
     offs = np.zeros(G + 1, dtype=np.int64)
     offs[1:] = np.cumsum(sizes)
     n_off = (G + 2) // 2 * 2  # int32 offsets padded to 8 bytes, then the uint64 seeds
-    off_i32 = np.zeros(n_off, dtype=np.int32)
-    off_i32[:G + 1] = offs
-    meta = np.concatenate([off_i32.view(np.uint8),
-                           np.asarray(nbr_seeds if nbr_seeds is not None else [], dtype=np.uint64).view(np.uint8)])
-    d_in = torch.from_numpy(host).to(device, non_blocking=False)
-    d_meta = torch.from_numpy(meta).to(device)
-    off = d_meta[:4 * (G + 1)].view(torch.int32)
-    bb = d_in[:, :12].contiguous().view(nt, 4, 3)
-    am = d_in[:, 12:15].contiguous()
-    dips = d_in[:, 15:].contiguous()
+    n_meta = n_off + 2 * (len(nbr_seeds) if nbr_seeds is not None else 0)  # in 4-byte words
+    m0 = (nt * 121 + 1) // 2 * 2  # metadata 8-byte aligned (uint64 seeds)
+    words = m0 + n_meta
+    stage = _pinned(words)
+    hf = stage.numpy()
+    np.concatenate([np.asarray(c["backbone"], dtype=np.float32).reshape(-1) for c in chains], out=hf[:nt * 12])
+    np.concatenate([np.asarray(c["amide_norm"], dtype=np.float32).reshape(-1) for c in chains],
+                   out=hf[nt * 12:nt * 15])
+    np.concatenate([np.asarray(c["dips"], dtype=np.float32).reshape(-1) for c in chains], out=hf[nt * 15:nt * 121])
+    hm = hf[m0:words].view(np.int32)
+    hm[:n_off] = 0
+    hm[:G + 1] = offs
+    if nbr_seeds is not None:
+        hm[n_off:].view(np.uint64)[:] = np.asarray(nbr_seeds, dtype=np.uint64)
+    d_all = stage[:words].to(device, non_blocking=True)
+    _keep_until_copied(stage)
+    bb = d_all[:nt * 12].view(nt, 4, 3)
+    am = d_all[nt * 12:nt * 15].view(nt, 3)
+    dips = d_all[nt * 15:nt * 121].view(nt, 106)
+    d_meta = d_all[m0:words].view(torch.int32)
+    off = d_meta[:G + 1]
     ca = bb[:, 1, :].contiguous()
     idx, d2 = _knn(ca, sizes, off, k)
     node_f = torch.empty(nt, 113, dtype=torch.float32, device=device)
@@ -112,7 +136,7 @@ def build_graph_batch(chains, k=KNN, nb=GEO_NBRHD_SIZE, seed=0, device="cuda", r
                "di_knn_graph")
     nbr = torch.empty(nt * k, 4, dtype=torch.int32, device=device)
     if nbr_seeds is not None:
-        seeds = d_meta[4 * n_off:]
+        seeds = d_meta[n_off:]
         _lib.check(lib.di_build_nbr_ids_torch(G, _p(off), k, _p(seeds), _p(src), _p(dst), _p(nbr), _stream()),
                    "di_build_nbr_ids_torch")
     else:
@@ -120,7 +144,7 @@ def build_graph_batch(chains, k=KNN, nb=GEO_NBRHD_SIZE, seed=0, device="cuda", r
                                         _stream()), "di_build_nbr_ids")
     gb = GraphBatch(src, dst, nbr, node_f, edge_f, sizes, [n * k for n in sizes], node_count_limit=node_count_limit,
                     in_ptr=in_ptr, node_pos=node_pos)
-    gb._keep = (d_in, d_meta)  # inputs referenced by in-flight launches
+    gb._keep = (d_all,)  # inputs referenced by in-flight launches
     if return_aux:
         return gb, {"knn_idx": idx, "knn_d2": d2}
     return gb

@@ -201,7 +201,7 @@ void k_init_edge(InitArgs a) {
   const T* W = reinterpret_cast<const T*>(a.wmat);
   WPipe<T, G::NW, G::DBUF, CAP> pipe(lds);
   DmaPump* PP = pipe.pump_ptr();
-  pipe.issue(W + IE_T0 * BLK, 40);
+  pipe.issue(W + IE_T0 * BLK, 8);  // stage 0: the collapsed edge-message map (8 blocks)
 
   Act<2> geo;
   load_edge_geo(geo, a.edge_f + (int64_t)e * NFEAT_E, g);
@@ -212,15 +212,22 @@ void k_init_edge(InitArgs a) {
   Act<8> acc;
   load_row(acc, a.pos_src + (int64_t)a.node_pos[a.src[e]] * HID, g);
   add_row(acc, a.pos_dst + (int64_t)a.node_pos[a.dst[e]] * HID, g);
+  {
+    // t = 0: edge_messages_linear_0 and its combined_linear_0 slice, collapsed on the host into one
+    // [128, 2] map of the message columns (no activation between them, :237-241)
+    const T* w = pipe.next();
+    pipe.issue(W + (IE_T0 + 40) * BLK, 40);
+    mma<8, 1>(acc, gop, w, lane, PP);
+  }
 #pragma unroll 1
-  for (int t = 0; t < 5; ++t) {
+  for (int t = 1; t < 5; ++t) {
     const T* w = pipe.next();
     if (t < 4) pipe.issue(W + (IE_T0 + 40 * (t + 1)) * BLK, 40);
     else pipe.issue(W + IE_GEO1 * BLK, 40);
     Act<8> y;
     zero(y);
     mma<8, 1>(y, gop, w, lane, PP);
-    if (t > 0) silu2_<8, FAST>(y);
+    silu2_<8, FAST>(y);
     linear<DT, 8, 4>(acc, y, w + 8 * BLK, lane, PP);
   }
   silu2_<8, FAST>(acc);  // combined_edge_logits (log2 units: feeds the gate product -> linear)

@@ -13,7 +13,8 @@ constexpr int EM_EMB = 0, EM_Q = 32, EM_K = 64, EM_V = 96, EM_NBLK = 128;
 constexpr int EMV_Q = 0, EMV_K = 128, EMV_V = 256, EMV_N = 384;
 
 // ---- kind 1: InitEdgeModule ----------------------------------------------------------------
-// for t in {edge_messages, dist, dir, orient, amide}: geo0_t [8 blk] then c0_t [32 blk]
+// for t in {edge_messages, dist, dir, orient, amide}: geo0_t [8 blk] then c0_t [32 blk]; t = 0 holds
+// only the collapsed combined_linear_0 . edge_messages_linear_0 map [8 blk] (blocks 8..39 zero)
 constexpr int IE_T0 = 0;      // + 40*t
 constexpr int IE_GEO1 = 200;  // 5 x [8 blk]
 constexpr int IE_C1 = 240;    // combined_linear_1 (28 -> 32 rows) [2 x 4]

@@ -198,10 +198,18 @@ def init_blob(sd, dtype, p="gnn_module.0.init_edge_module",
     sc = _l2e(dtype)  # log2-unit SiLU: geometric projections, combined logits and gates (silu2)
     wc0 = _np(sd[f"{p}.combined_linear_0.weight"])  # [128, 896]
     for t, kind in enumerate(GEO_ORDER):
-        # t > 0: silu2(sc * W_t0 g) = sc * silu(W_t0 g), consumed by wc0 (x 1/sc), accumulated into
-        # sc * acc (x sc): net 1. t = 0 (no SiLU): the wc0 slice carries the sc.
-        bb.put(40 * t, _geo_rows(_np(sd[f"{p}.{kind}_linear_0.weight"]), kind) * (sc if t > 0 else 1.0))
-        bb.put(40 * t + 8, wc0[:, 256 + 128 * t: 384 + 128 * t] * (1.0 if t > 0 else sc))
+        w0 = _np(sd[f"{p}.{kind}_linear_0.weight"])
+        if t == 0:
+            # edge_messages_linear_0 has no activation before combined_linear_0 (:237-241), so its
+            # slice of combined_linear_0 collapses with it into ONE [128, 2] map of the two message
+            # columns (pos_enc, weight): 8 blocks / 8 MFMAs instead of 40; blocks 8..39 stay zero
+            bb.put(0, _geo_rows(wc0[:, 256:384] @ w0, kind) * sc)
+            bb.put(8, np.zeros((128, 128)))  # unused (layout kept)
+        else:
+            # silu2(sc * W_t0 g) = sc * silu(W_t0 g), consumed by wc0 (x 1/sc), accumulated into
+            # sc * acc (x sc): net 1
+            bb.put(40 * t, _geo_rows(w0, kind) * sc)
+            bb.put(40 * t + 8, wc0[:, 256 + 128 * t: 384 + 128 * t])
         bb.put(200 + 8 * t, _geo_rows(_np(sd[f"{p}.{kind}_linear_1.weight"]), kind) * sc)  # gs' = sc * gs
     # silu2(sc * acc) * (sc * gs) = sc^2 * (silu(acc) * gs)
     bb.put(240, pad2(_np(sd[f"{p}.combined_linear_1.weight"]), 32, 128) / (sc * sc))

@@ -60,10 +60,9 @@ class Emu:
         pos = np.arange(N)  # per-chain graph
         acc = p.pos_src.numpy()[pos[src]] + p.pos_dst.numpy()[pos[dst]]
         s2 = self.s2
-        for t in range(5):
-            y = G @ self.M(ib, 40 * t, 128, 32).T
-            if t > 0:
-                y = s2(y)
+        acc = acc + G @ self.M(ib, 0, 128, 32).T  # t = 0: collapsed edge-message map
+        for t in range(1, 5):
+            y = s2(G @ self.M(ib, 40 * t, 128, 32).T)
             acc = acc + y @ self.M(ib, 40 * t + 8, 128, 128).T
         c = s2(acc)
         gs = sum((G @ self.M(ib, 200 + 8 * t, 128, 32).T) if t == 0 else s2(G @ self.M(ib, 200 + 8 * t, 128, 32).T)
