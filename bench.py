@@ -321,15 +321,19 @@ def main():
         ch1, ch2 = synth.synthetic_complex(1000 * rank + c, n_res, n_res)
         pool.append((ch1, ch2))
     t_synth = time.perf_counter() - tb
-    torch.cuda.synchronize()
-    tb = time.perf_counter()
     # the whole pool in one builder call (one launch per stage); neighbour ids as the reference
-    # draws them after torch.manual_seed(s) per chain (bit-exact mode)
-    pool_gb = build_graph_batch([ch for pair in pool for ch in pair], k=k, device=dev,
-                                node_count_limit=args.node_limit,
-                                nbr_seeds=[2 * (1000 * rank + c) + s + 1 for c in range(P) for s in (0, 1)])
-    torch.cuda.synchronize()
-    t_build = time.perf_counter() - tb
+    # draws them after torch.manual_seed(s) per chain (bit-exact mode). Timed twice: the first
+    # (cold) call also pays module loading and the pinned staging allocation.
+    t_builds = []
+    for _ in range(2):
+        torch.cuda.synchronize()
+        tb = time.perf_counter()
+        pool_gb = build_graph_batch([ch for pair in pool for ch in pair], k=k, device=dev,
+                                    node_count_limit=args.node_limit,
+                                    nbr_seeds=[2 * (1000 * rank + c) + s + 1 for c in range(P) for s in (0, 1)])
+        torch.cuda.synchronize()
+        t_builds.append(time.perf_counter() - tb)
+    t_build = t_builds[1]
     # resident batch: complexes -> micro-batches (copies of pool complexes, distinct HBM buffers)
     n_mb = args.complexes // M
     mbs = [select_graphs(pool_gb, [2 * ((m * M + j) % P) + s for j in range(M) for s in (0, 1)])
@@ -465,6 +469,7 @@ def main():
         "roofline": roof,
         "kernels": {n: {kk: round(v, 3) if isinstance(v, float) else v for kk, v in r.items()} for n, r in kern.items()},
         "builder": {"complexes": P, "build_s": round(t_build, 4), "ms_per_complex": round(t_build / P * 1e3, 3),
+                    "cold_build_s": round(t_builds[0], 4),
                     "synth_host_s": round(t_synth, 3),
                     "what": "one builder call for the pool: kNN, features, topology, torch-seeded neighbour ids"},
     }

@@ -53,7 +53,7 @@ _SIGS = {
     "di_knn_topk": ([_I, _P, _P, _I, _I, _P, _P, _P], ctypes.c_int),
     "di_geo_feats": ([ctypes.POINTER(DiGeoArgs), _P], ctypes.c_int),
     "di_build_nbr_ids": ([_I, _P, _P, _P, ctypes.c_uint64, _P, _P], ctypes.c_int),
-    "di_build_nbr_ids_torch": ([_I, _P, _I, _P, _P, _P, _P, _P], ctypes.c_int),
+    "di_build_nbr_ids_torch": ([_I, _P, _I, _P, _I, _P, _P, _P, _P], ctypes.c_int),
     "di_knn_graph": ([_I, _P, _I, _P, _I, _P, _P, _P, _P, _P], ctypes.c_int),
     "di_conformation": ([ctypes.POINTER(DiGraph), _I, _P, _P, _P, _P, _P, _P, _P], ctypes.c_int),
     "di_gemm_bias_act": ([_I, _I, _I, _I, _P, _I, _P, _P, _I, _P, _I, _P, _I, _P], ctypes.c_int),

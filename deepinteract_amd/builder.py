@@ -137,7 +137,7 @@ def build_graph_batch(chains, k=KNN, nb=GEO_NBRHD_SIZE, seed=0, device="cuda", r
     nbr = torch.empty(nt * k, 4, dtype=torch.int32, device=device)
     if nbr_seeds is not None:
         seeds = d_meta[n_off:]
-        _lib.check(lib.di_build_nbr_ids_torch(G, _p(off), k, _p(seeds), _p(src), _p(dst), _p(nbr), _stream()),
+        _lib.check(lib.di_build_nbr_ids_torch(G, _p(off), k, _p(seeds), nt, _p(src), _p(dst), _p(nbr), _stream()),
                    "di_build_nbr_ids_torch")
     else:
         _lib.check(lib.di_build_nbr_ids(nt * k, _p(src), _p(dst), _p(in_ptr), ctypes.c_uint64(seed), _p(nbr),

@@ -288,6 +288,10 @@ __device__ __forceinline__ void unpack_op(Act<2 * NS>& a, const Op<BF16T, NS>& o
 // after every DI_DMA_PUMP MFMAs (0: the stage's pieces are issued in one burst at stage start),
 // so the issue cost of the weight stream hides between this wave's MFMAs. Measured (C3 edge
 // layer, bf16): burst 503 us, pump every 1/2/4 MFMAs 576/575/559 us (extra spills) -> off.
+// LDS weight fragments kept in flight ahead of their MFMA (0: compiler schedule)
+#ifndef DI_MMA_LEAD
+#define DI_MMA_LEAD 0
+#endif
 #ifndef DI_DMA_PUMP
 #define DI_DMA_PUMP 0
 #endif
@@ -341,6 +345,18 @@ __device__ __forceinline__ void mma(Act<NBO>& out, const Op<BF16T, NS>& op, cons
           if (pp && ((b0 / G) * NS + s) % (DI_DMA_PUMP < G ? 1 : DI_DMA_PUMP / G) == 0) pp->pump();
       }
       if constexpr (DI_MMA_ORDER == 1) __builtin_amdgcn_sched_barrier(0);
+    }
+    if constexpr (DI_MMA_LEAD > 0) {
+      // keep LEAD weight fragments in flight ahead of the MFMA that consumes them: LEAD ds_reads,
+      // then alternate one MFMA / one ds_read, then the last LEAD MFMAs
+      constexpr int N = NBO * NS, L = N < DI_MMA_LEAD ? N : DI_MMA_LEAD;
+      __builtin_amdgcn_sched_group_barrier(0x100, L, 0);
+#pragma unroll
+      for (int i = 0; i < N - L; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, L, 0);
     }
   }
 }

@@ -386,6 +386,12 @@ struct EdgeStages {
       vcur = pipe.v(i);
       return pipe.w(i);
     } else {
+#ifdef DI_NODMA  // diagnostic only: after two stages, no weight stream (stale weights, wrong results)
+      if (i >= 2) {
+        vcur = pipe.slot_v(i & 1);
+        return pipe.slot_w(i & 1);
+      }
+#endif
       const T* w = pipe.next();
       if (i + 1 < total) issue(i + 1);
       vcur = pipe.v();

@@ -221,20 +221,21 @@ __device__ __forceinline__ float knn_dist(const float* ca, int n0, int j, float 
   return (ni + nj) - 2.f * dot3(x0, x1, x2, y0, y1, y2);
 }
 
+// LDS sized to the batch's largest chain (stride S = max_nodes rounded up to 64 per wave): at
+// 1000-node chains 24 KiB per block, so six blocks (24 waves) share a CU instead of one.
 __global__ __launch_bounds__(64 * KNN_WAVES) void k_knn(const int* __restrict__ node_off,
-                                                          const float* __restrict__ ca, int k,
+                                                          const float* __restrict__ ca, int k, int S,
                                                           int* __restrict__ idx_out, float* __restrict__ d2_out) {
-  __shared__ float dist[KNN_WAVES][KNN_MAX_N];
-  __shared__ uint16_t sidx[KNN_WAVES][KNN_MAX_N];
+  extern __shared__ __attribute__((aligned(16))) char knn_lds[];
   const int gph = blockIdx.y;
   const int n0 = node_off[gph], n = node_off[gph + 1] - n0;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int i = blockIdx.x * KNN_WAVES + wave;
-  if (i >= n) return;  // wave-uniform; no block barrier below
+  if (i >= n || n > S) return;  // wave-uniform; no block barrier below (n > S: max_nodes too small)
   const float* xi = ca + (int64_t)(n0 + i) * 3;
   const float x0 = xi[0], x1 = xi[1], x2 = xi[2];
   const float ni = sq3(x0, x1, x2);
-  float* d = dist[wave];
+  float* d = reinterpret_cast<float*>(knn_lds) + wave * S;
   for (int j = lane; j < n; j += 64) d[j] = knn_dist(ca, n0, j, x0, x1, x2, ni);
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -275,7 +276,7 @@ __global__ __launch_bounds__(64 * KNN_WAVES) void k_knn(const int* __restrict__ 
   }
   if (!tie) return;  // wave-uniform (every lane reduced the same values)
   // exact-tie row: replay torch's CPU selection on the full row
-  uint16_t* ix = sidx[wave];
+  uint16_t* ix = reinterpret_cast<uint16_t*>(knn_lds + (size_t)KNN_WAVES * S * 4) + wave * S;
   for (int j = lane; j < n; j += 64) {
     d[j] = knn_dist(ca, n0, j, x0, x1, x2, ni);
     ix[j] = (uint16_t)j;
@@ -477,72 +478,77 @@ __device__ __forceinline__ uint32_t mt_next(uint32_t cur, uint32_t nxt, uint32_t
   return far ^ (y >> 1) ^ ((y & 1u) ? MT_A : 0u);
 }
 
-__global__ __launch_bounds__(256) void k_nbr_ids_torch(const int* __restrict__ node_off, int k,
-                                                       const uint64_t* __restrict__ seeds,
-                                                       const int* __restrict__ src, const int* __restrict__ dst,
-                                                       int* __restrict__ nbr) {
+// One wave per chain (wave-synchronous: LDS ordering by wave barriers, no workgroup barrier in the
+// 624-word loop); the kept draws are extracted per randperm call, not per stream position.
+__device__ __forceinline__ void wave_sync_lds() {
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+}
+
+__global__ __launch_bounds__(64) void k_nbr_ids_torch(const int* __restrict__ node_off, int k,
+                                                      const uint64_t* __restrict__ seeds, int* __restrict__ nbr) {
   __shared__ uint32_t st[MT_N];
   __shared__ uint32_t out[MT_N];
-  __shared__ uint32_t prev_last;
-  const int g = blockIdx.x, tid = threadIdx.x;
+  constexpr int P1 = MT_N - MT_M, P2 = 2 * (MT_N - MT_M);  // 227, 454
+  const int g = blockIdx.x, lane = threadIdx.x;
   const int n0 = node_off[g], n = node_off[g + 1] - n0;
-  const int64_t E = (int64_t)n * k, e0 = (int64_t)n0 * k;
-  const int64_t total = 2 * E * (k - 1);  // draws of the 2E randperm(k) calls
-  if (tid == 0) {                          // init_with_uint32(seed)
+  const int E = n * k, e0 = n0 * k, km1 = k - 1;
+  const int total = 2 * E * km1;  // draws of the 2E randperm(k) calls (host checks the int32 range)
+  if (lane == 0) {                // init_with_uint32(seed)
     uint32_t s = (uint32_t)(seeds[g] & 0xffffffffull);
     st[0] = s;
     for (int i = 1; i < MT_N; ++i) {
       s = 1812433253u * (s ^ (s >> 30)) + (uint32_t)i;
       st[i] = s;
     }
-    prev_last = 0u;
   }
-  __syncthreads();
-  for (int64_t base = 0; base < total; base += MT_N) {
+  wave_sync_lds();
+  uint32_t prev_last = 0u;  // last tempered word of the previous 624-word block (wave-uniform)
+  for (int base = 0; base < total; base += MT_N) {
+    uint32_t v[4];
     // twist, phase 1: i in [0, 227) from old words only
-    uint32_t v[3];
 #pragma unroll
-    for (int q = 0; q < 3; ++q) {
-      const int i = tid + 256 * q;
-      if (i < MT_N - MT_M) v[q] = mt_next(st[i], st[i + 1], st[i + MT_M]);
+    for (int q = 0; q < 4; ++q) {
+      const int i = lane + 64 * q;
+      if (i < P1) v[q] = mt_next(st[i], st[i + 1], st[i + MT_M]);
     }
-    __syncthreads();
+    wave_sync_lds();
 #pragma unroll
-    for (int q = 0; q < 3; ++q) {
-      const int i = tid + 256 * q;
-      if (i < MT_N - MT_M) st[i] = v[q];
+    for (int q = 0; q < 4; ++q) {
+      const int i = lane + 64 * q;
+      if (i < P1) st[i] = v[q];
     }
-    __syncthreads();
+    wave_sync_lds();
     // phase 2: i in [227, 454): far word i-227 is new (phase 1); i+1 <= 454 is still old
 #pragma unroll
-    for (int q = 0; q < 3; ++q) {
-      const int i = MT_N - MT_M + tid + 256 * q;
-      if (i < 2 * (MT_N - MT_M)) v[q] = mt_next(st[i], st[i + 1], st[i - (MT_N - MT_M)]);
+    for (int q = 0; q < 4; ++q) {
+      const int i = P1 + lane + 64 * q;
+      if (i < P2) v[q] = mt_next(st[i], st[i + 1], st[i - P1]);
     }
-    __syncthreads();
+    wave_sync_lds();
 #pragma unroll
-    for (int q = 0; q < 3; ++q) {
-      const int i = MT_N - MT_M + tid + 256 * q;
-      if (i < 2 * (MT_N - MT_M)) st[i] = v[q];
+    for (int q = 0; q < 4; ++q) {
+      const int i = P1 + lane + 64 * q;
+      if (i < P2) st[i] = v[q];
     }
-    __syncthreads();
+    wave_sync_lds();
     // phase 3: i in [454, 624): far word i-227 from phase 2; word 623 wraps to the new word 0
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
-      const int i = 2 * (MT_N - MT_M) + tid + 256 * q;
-      if (i < MT_N) v[q] = mt_next(st[i], st[i + 1 < MT_N ? i + 1 : 0], st[i - (MT_N - MT_M)]);
+      const int i = P2 + lane + 64 * q;
+      if (i < MT_N) v[q] = mt_next(st[i], st[i + 1 < MT_N ? i + 1 : 0], st[i - P1]);
     }
-    __syncthreads();
+    wave_sync_lds();
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
-      const int i = 2 * (MT_N - MT_M) + tid + 256 * q;
+      const int i = P2 + lane + 64 * q;
       if (i < MT_N) st[i] = v[q];
     }
-    __syncthreads();
+    wave_sync_lds();
     // tempering
 #pragma unroll
-    for (int q = 0; q < 3; ++q) {
-      const int i = tid + 256 * q;
+    for (int q = 0; q < 10; ++q) {
+      const int i = lane + 64 * q;
       if (i < MT_N) {
         uint32_t y = st[i];
         y ^= y >> 11;
@@ -552,35 +558,42 @@ __global__ __launch_bounds__(256) void k_nbr_ids_torch(const int* __restrict__ n
         out[i] = y;
       }
     }
-    __syncthreads();
-    // the two kept draws of every randperm call that touches this block of the stream
-#pragma unroll
-    for (int q = 0; q < 3; ++q) {
-      const int i = tid + 256 * q;
-      const int64_t t = base + i;
-      if (i < MT_N && t < total) {
-        const int64_t c = t / (k - 1);
-        const int j = (int)(t - c * (k - 1));
-        if (j < 2) {
-          const int side = c >= E;
-          const int64_t e = e0 + (side ? c - E : c);
-          const int node = side ? dst[e] : src[e];
-          int p;
-          if (j == 0) {
-            p = (int)(out[i] % (uint32_t)k);
-          } else {
-            const uint32_t u0 = i > 0 ? out[i - 1] : prev_last;
-            const int z0 = (int)(u0 % (uint32_t)k), z1 = (int)(out[i] % (uint32_t)(k - 1));
-            p = (1 + z1 == z0) ? 0 : 1 + z1;
-          }
-          nbr[e * 4 + 2 * side + j] = node * k + p;
-        }
+    wave_sync_lds();
+    // the kept draws (positions 0 and 1 of a call) that fall in this block: calls c with
+    // c*km1 in [base - 1, base + 624)
+    const int c_lo = base / km1, c_hi = min((base + MT_N - 1) / km1, 2 * E - 1);
+    for (int c = c_lo + lane; c <= c_hi; c += 64) {
+      const int t0 = c * km1 - base;  // block offset of the call's first draw
+      if (t0 < -1) continue;          // both kept draws were in the previous block
+      const int side = c >= E;
+      const int e = e0 + (side ? c - E : c);
+      const uint32_t u0 = t0 >= 0 ? out[t0] : prev_last;
+      const int z0 = (int)(u0 % (uint32_t)k);
+      // positions only: the endpoint's in-edge base is added by k_nbr_base (no dependent global
+      // load on the stream's critical path)
+      if (t0 >= 0) nbr[(int64_t)e * 4 + 2 * side] = z0;
+      if (t0 + 1 < MT_N) {
+        const int z1 = (int)(out[t0 + 1] % (uint32_t)km1);
+        nbr[(int64_t)e * 4 + 2 * side + 1] = (1 + z1 == z0) ? 0 : 1 + z1;
       }
     }
-    __syncthreads();
-    if (tid == 0) prev_last = out[MT_N - 1];
-    // (the next block's first barrier orders this write before any read of prev_last)
+    prev_last = out[MT_N - 1];
+    wave_sync_lds();  // every lane's reads of out[] before the next block's tempering
   }
+}
+
+// kept in-edge positions -> edge ids: nbr[e][2*side + j] = endpoint * k + position
+__global__ __launch_bounds__(256) void k_nbr_base(int Et, int k, const int* __restrict__ src,
+                                                  const int* __restrict__ dst, int* __restrict__ nbr) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= Et) return;
+  int4 p = reinterpret_cast<const int4*>(nbr)[e];
+  const int bs = src[e] * k, bd = dst[e] * k;
+  p.x += bs;
+  p.y += bs;
+  p.z += bd;
+  p.w += bd;
+  reinterpret_cast<int4*>(nbr)[e] = p;
 }
 
 // ------------------------------------------------------------------ kNN graph topology
@@ -627,12 +640,20 @@ extern "C" int di_knn_graph(int32_t num_graphs, const int32_t* node_off, int32_t
 }
 
 extern "C" int di_build_nbr_ids_torch(int32_t num_graphs, const int32_t* node_off, int32_t k, const uint64_t* seeds,
-                                      const int32_t* src, const int32_t* dst, int32_t* nbr_out, void* stream) {
-  if (num_graphs <= 0 || num_graphs > 65535 || !node_off || k < 3 || !seeds || !src || !dst || !nbr_out)
+                                      int32_t num_nodes, const int32_t* src, const int32_t* dst, int32_t* nbr_out,
+                                      void* stream) {
+  // chains of <= 4096 nodes (the builder's node-count limit) keep the draw count 2*n*k*(k-1) in int32
+  if (num_graphs <= 0 || num_graphs > 65535 || !node_off || k < 3 || k > 256 || !seeds || num_nodes <= 0 ||
+      (int64_t)num_nodes * k > INT32_MAX || !src || !dst || !nbr_out)
     return DI_EINVAL;
-  hipLaunchKernelGGL(k_nbr_ids_torch, dim3(num_graphs), dim3(256), 0, (hipStream_t)stream, node_off, k, seeds, src,
-                     dst, nbr_out);
+  const int num_edges = num_nodes * k;
+  hipLaunchKernelGGL(k_nbr_ids_torch, dim3(num_graphs), dim3(64), 0, (hipStream_t)stream, node_off, k, seeds,
+                     nbr_out);
   hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return (int)e;
+  hipLaunchKernelGGL(k_nbr_base, dim3((num_edges + 255) / 256), dim3(256), 0, (hipStream_t)stream, num_edges, k, src,
+                     dst, nbr_out);
+  e = hipGetLastError();
   return e == hipSuccess ? DI_OK : (int)e;
 }
 
@@ -642,7 +663,9 @@ extern "C" int di_knn_topk(int32_t num_graphs, const int32_t* node_off, const fl
       max_nodes > KNN_MAX_N || num_graphs > 65535)
     return DI_EINVAL;
   dim3 grid((max_nodes + KNN_WAVES - 1) / KNN_WAVES, num_graphs);
-  hipLaunchKernelGGL(k_knn, grid, dim3(64 * KNN_WAVES), 0, (hipStream_t)stream, node_off, ca, k, idx_out, d2_out);
+  const int S = (max_nodes + 63) & ~63;
+  hipLaunchKernelGGL(k_knn, grid, dim3(64 * KNN_WAVES), (size_t)KNN_WAVES * S * 6, (hipStream_t)stream, node_off, ca,
+                     k, S, idx_out, d2_out);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? DI_OK : (int)e;
 }

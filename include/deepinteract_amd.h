@@ -195,9 +195,11 @@ int di_build_nbr_ids(int32_t num_edges, const int32_t* src, const int32_t* dst, 
  * (deepinteract_utils.py:539-546): chain g's ids are those convert_df_to_dgl_graph produces right
  * after torch.manual_seed(seeds[g]) (torch CPU generator = mt19937; randperm = Fisher-Yates, E src
  * calls then E dst calls). kNN graphs only (uniform in-degree k, dst-major edges, k >= 3).
- * node_off [G+1], seeds [G] (device); src/dst [Et] global node ids; nbr_out [Et,4] global ids. */
+ * node_off [G+1], seeds [G] (device); num_nodes = node_off[G]; src/dst [Et = num_nodes*k] global
+ * node ids; nbr_out [Et,4] global ids. Two launches: the per-chain mt19937 streams (one wave per
+ * chain) write the kept in-edge positions, then every id gets its endpoint's in-edge base. */
 int di_build_nbr_ids_torch(int32_t num_graphs, const int32_t* node_off, int32_t k, const uint64_t* seeds,
-                           const int32_t* src, const int32_t* dst, int32_t* nbr_out, void* stream);
+                           int32_t num_nodes, const int32_t* src, const int32_t* dst, int32_t* nbr_out, void* stream);
 
 /* ---- module-at-a-time API ---------------------------------------------------------------- */
 /* ConformationModule alone (kind-6 blob): conf_out [Et,128] = F + SiLU(final_linear(...)), from the

@@ -259,3 +259,27 @@ def test_raw_arrays_through_builder_to_logits(model_f32, case):
     print(f"{case} raw arrays -> builder -> logits rel {el:.3e}")
     assert el < F32_TOL
     assert rel_max(_np(probs[0]), z["probs"]) < F32_TOL
+
+
+@pytest.mark.parametrize("k,n", [(3, 97), (7, 300), (20, 1000)])
+def test_torch_seeded_nbr_ids_vs_torch_randperm(k, n):
+    """di_build_nbr_ids_torch against torch's own CPU generator: after torch.manual_seed(seed) the
+    reference draws randperm(k) once per edge for the src side, then once per edge for the dst
+    side, and keeps the first two entries as positions in the endpoint's in-edge list
+    (deepinteract_utils.py:539-546; in-edges of v are v*k .. v*k+k-1). Two chains per batch, so
+    the second chain's ids carry the batch edge offset."""
+    from deepinteract_amd import synth
+    from deepinteract_amd.builder import build_graph_batch
+    chains = list(synth.synthetic_complex(11, n, n + 5))
+    seeds = [1234, 99]
+    gb = build_graph_batch(chains, k=k, nbr_seeds=seeds)
+    nbr = gb.nbr.cpu().numpy()
+    src, dst = gb.src.cpu().numpy(), gb.dst.cpu().numpy()
+    for g, seed in enumerate(seeds):
+        e0, e1 = gb.edge_off[g], gb.edge_off[g + 1]
+        E = e1 - e0
+        torch.manual_seed(seed)
+        p_src = torch.stack([torch.randperm(k)[:2] for _ in range(E)]).numpy()
+        p_dst = torch.stack([torch.randperm(k)[:2] for _ in range(E)]).numpy()
+        want = np.concatenate([src[e0:e1, None] * k + p_src, dst[e0:e1, None] * k + p_dst], 1)
+        assert np.array_equal(nbr[e0:e1], want), (k, n, g)
