@@ -17,7 +17,7 @@
 #include <type_traits>
 #include "common.h"
 #include "layout.h"
-#include "../../include/deepinteract_amd.h"
+#include "deepinteract_amd.h"
 
 namespace di {
 
@@ -386,6 +386,10 @@ struct EdgeStages {
       vcur = pipe.v(i);
       return pipe.w(i);
     } else {
+      if (i >= 2) {
+        vcur = pipe.slot_v(i & 1);
+        return pipe.slot_w(i & 1);
+      }
       const T* w = pipe.next();
       if (i + 1 < total) issue(i + 1);
       vcur = pipe.v();
