@@ -2,7 +2,8 @@
 the same reference modules, on the tiny golden case's graph (the oracle itself is pinned to the
 reference's modules by tests/test_oracle_golden.py). Inputs beyond the fixture (current node /
 edge features) are seeded random tensors; weights are the seeded reference-keyed state dict,
-sliced to each module's own keys. fp32 <= 1e-4 relative, bf16 <= 5e-2 (as test_gpu_parity)."""
+sliced to each module's own keys. fp32 <= 1e-4 relative; bf16 bound stated below (measured errors
+printed with -s)."""
 import numpy as np
 import pytest
 import torch
@@ -11,7 +12,15 @@ from gpu_common import load_case, rel_max
 from oracle import geot_oracle as O
 
 pytestmark = pytest.mark.gpu
-TOL = {"f32": 1e-4, "bf16": 5e-2}
+# bf16 measured on MI355X: init_edge 4.3e-3, conformation 5.7e-3, mha 8.1e-3,
+# gt layer 5.2e-3, final 5.4e-3 (max-abs error / max-abs reference); bound ~2x the largest
+TOL = {"f32": 1e-4, "bf16": 1.6e-2}
+
+
+def check(what, dtype, out, ref):
+    err = rel_max(_np(out), _np(ref))
+    print(f"{what} {dtype}: {err:.3e}")
+    assert err < TOL[dtype], (what, dtype, err)
 P = "gnn_module.0.gt_block.0"
 
 
@@ -54,7 +63,7 @@ def test_init_edge_module(sd, case, dtype):
     m = InitEdgeModule(dtype).load_reference_state_dict(sub(sd, "gnn_module.0.init_edge_module."))
     out = m(g)
     ref = O.init_edge(sd, og, G)
-    assert rel_max(_np(out), _np(ref)) < TOL[dtype]
+    check("init_edge", dtype, out, ref)
 
 
 @pytest.mark.parametrize("dtype", ["f32", "bf16"])
@@ -65,7 +74,7 @@ def test_conformation_module(sd, case, dtype):
     m = ConformationModule(dtype).load_reference_state_dict(sub(sd, f"{P}.conformation_module."))
     out = m(g, G)
     ref = O.conformation(sd, f"{P}.conformation_module", og, edge, G)
-    assert rel_max(_np(out), _np(ref)) < TOL[dtype]
+    check("conformation", dtype, out, ref)
 
 
 @pytest.mark.parametrize("update_edge_feats", [True, False])
@@ -78,10 +87,10 @@ def test_mha_layer(sd, case, dtype, update_edge_feats):
     h, e = m(g, node, edge)
     rh, re = O.mha(sd, f"{P}.mha_module", og, node, edge, update_edge_feats)
     assert h.shape == (node.shape[0], 4, 32)
-    assert rel_max(_np(h), _np(rh)) < TOL[dtype]
+    check("mha node", dtype, h, rh)
     if update_edge_feats:
         assert e.shape == (edge.shape[0], 4, 32)
-        assert rel_max(_np(e), _np(re)) < TOL[dtype]
+        check("mha edge", dtype, e, re)
     else:
         assert e is None
 
@@ -98,11 +107,11 @@ def test_geometric_transformer_module(sd, case, dtype, final):
     out = m(g, G)
     rn, re, _ = O.gt_layer(sd, li, og, node, edge, G, final)
     if final:
-        assert rel_max(_np(out), _np(rn)) < TOL[dtype]
+        check("final gt node", dtype, out, rn)
     else:
         n, e = out
-        assert rel_max(_np(n), _np(rn)) < TOL[dtype]
-        assert rel_max(_np(e), _np(re)) < TOL[dtype]
+        check("gt node", dtype, n, rn)
+        check("gt edge", dtype, e, re)
 
 
 def test_gemm_bias_act_matches_torch():

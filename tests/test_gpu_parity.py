@@ -3,7 +3,8 @@
 
 Tolerances (BASELINE.json north_star): fp32 outputs <= 1e-4 relative (max-abs error over the
 tensor / max-abs of the reference tensor); kNN indices bit-exact. bf16 (stated looser bound):
-GeoT node/edge outputs <= 5e-2 relative, measured against the same fp32 reference.
+GeoT node/edge outputs <= 1.5e-2 relative (measured <= 6.6e-3 on tiny/c1/c2), against
+the same fp32 reference.
 """
 import numpy as np
 import pytest
@@ -15,7 +16,7 @@ pytestmark = pytest.mark.gpu
 
 CASES = ["tiny", "c1", "c2"]
 F32_TOL = 1e-4
-BF16_TOL = 5e-2
+BF16_TOL = 1.5e-2  # measured <= 6.6e-3 (tiny/c1/c2); ~2x
 
 
 @pytest.fixture(scope="module")
