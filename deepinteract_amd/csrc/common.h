@@ -179,6 +179,13 @@ struct RawRow<u16> {
     }
   }
 };
+// Make the wave wait for a row's loads HERE (an empty asm that reads its registers): placed
+// before a weight-stage DMA issue, it keeps a later use of the row from waiting for the whole
+// in-flight stage (vmcnt retires in order; the compiler cannot count a runtime-length DMA loop).
+__device__ __forceinline__ void settle(const RawRow<u16>& r) {
+#pragma unroll
+  for (int b = 0; b < 8; ++b) asm volatile("" ::"v"(r.u[b].x), "v"(r.u[b].y));
+}
 template <>
 struct RawRow<float> {
   floatx4 v[8];
@@ -191,6 +198,10 @@ struct RawRow<float> {
     for (int b = 0; b < 8; ++b) a.v[b] = v[b];
   }
 };
+__device__ __forceinline__ void settle(const RawRow<float>& r) {
+#pragma unroll
+  for (int b = 0; b < 8; ++b) asm volatile("" ::"v"(r.v[b]));
+}
 
 // edge feature row G [28] (fp32, 112-B rows) as a 32-feature activation, features 28..31 = 0
 __device__ __forceinline__ void load_edge_geo(Act<2>& a, const float* row, int g) {

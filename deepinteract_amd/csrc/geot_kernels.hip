@@ -673,13 +673,19 @@ void k_edge_layer(EdgeArgs a) {
 }
 
 // ================================================================ fused node layer
+// Every bias vector rides in its stage's LDS slot (init_vec_lds) and the node's own input row is
+// added right after the stage barrier, before the next stage's DMA is issued: a global load
+// consumed after a DMA issue makes the wave wait for the whole in-flight weight stage (vmcnt
+// counts in order, and the compiler cannot count a runtime-length DMA loop), which exposed the
+// DMA latency at every stage.
 template <class DT, bool FINAL>
 __global__ __launch_bounds__(THREADS, 2) void k_node_layer(NodeArgs a) {
   using T = typename DT::T;
   DI_GEOT_ENTRY();
   constexpr bool FAST = DT::kBF16;
   constexpr bool DB = DT::kBF16;
-  __shared__ __attribute__((aligned(16))) T lds[(DB ? 2 : 1) * MAT128 * BLK];
+  using Pipe = WPipe<T, WAVES, DB, MAT128, 128>;
+  __shared__ __attribute__((aligned(16))) char lds[(DB ? 2 : 1) * Pipe::SLOT_BYTES];
   const int lane = lane_id(), g = lane >> 4;
   const int r = row_id<WAVES>();
   const bool valid = r < a.Nt;
@@ -687,8 +693,10 @@ __global__ __launch_bounds__(THREADS, 2) void k_node_layer(NodeArgs a) {
   const T* W = reinterpret_cast<const T*>(a.wmat);
   const float* V = a.wvec;
   const T* qkv = reinterpret_cast<const T*>(a.qkv);
-  WPipe<T, WAVES, DB, MAT128> pipe(lds);
-  pipe.issue(W + NL_ON * BLK, MAT128);
+  Pipe pipe(lds);
+  pipe.issue(W + NL_ON * BLK, MAT128, V + NLV_ON, 128);
+  RawRow<T> hin;  // in1 of the residual, consumed after the O stage barrier
+  hin.load(reinterpret_cast<const T*>(a.h_in) + (int64_t)v * HID, g);
 
   // send_and_recv(u_mul_e('V_h','score'), sum) and (copy_e('score'), sum); h = wV / (z + 1e-6)
   Act<8> wv;
@@ -738,11 +746,16 @@ __global__ __launch_bounds__(THREADS, 2) void k_node_layer(NodeArgs a) {
   }
   // n = in1 + O_node(h)
   const T* w = pipe.next();
-  pipe.issue(W + NL_F1 * BLK, MAT128);
+  settle(hin);  // landed with the O stage (the barrier drained vmcnt); no wait on the F1 DMA later
+  pipe.issue(W + NL_F1 * BLK, MAT128, V + NLV_F1, 128);
   Act<8> n;
-  init_vec(n, V + NLV_ON, g);
+  init_vec_lds(n, pipe.v(), g);
+  {
+    Act<8> hv;
+    hin.to_act(hv);
+    add_(n, hv);
+  }
   linear<DT, 8, 4>(n, wv, w, lane);
-  add_row(n, reinterpret_cast<const T*>(a.h_in) + (int64_t)v * HID, g);
   // n = n + W2 silu(W1 BN2(n))
   Act<8> o;
   zero(o);
@@ -751,12 +764,12 @@ __global__ __launch_bounds__(THREADS, 2) void k_node_layer(NodeArgs a) {
     w = pipe.next();
     pipe.issue(W + (NL_F2 + MAT128 * half) * BLK, MAT128);
     Act<8> t;
-    init_vec(t, V + NLV_F1 + 128 * half, g);
+    init_vec_lds(t, pipe.v(), g);
     linear<DT, 8, 4>(t, n, w, lane);
     silu2_<8, FAST>(t);
     w = pipe.next();
-    if (half == 0) pipe.issue(W + (NL_F1 + MAT128) * BLK, MAT128);
-    else if (!FINAL) pipe.issue(W + NL_Q * BLK, MAT128);
+    if (half == 0) pipe.issue(W + (NL_F1 + MAT128) * BLK, MAT128, V + NLV_F1 + 128, 128);
+    else if (!FINAL) pipe.issue(W + NL_Q * BLK, MAT128, V + NLV_Q, 128);
     linear<DT, 8, 4>(o, t, w, lane);
   }
   add_(n, o);
@@ -777,9 +790,9 @@ __global__ __launch_bounds__(THREADS, 2) void k_node_layer(NodeArgs a) {
 #pragma unroll 1
     for (int q = 0; q < 3; ++q) {
       w = pipe.next();
-      if (q < 2) pipe.issue(W + (NL_Q + MAT128 * (q + 1)) * BLK, MAT128);
+      if (q < 2) pipe.issue(W + (NL_Q + MAT128 * (q + 1)) * BLK, MAT128, V + NLV_Q + 128 * (q + 1), 128);
       Act<8> t;
-      init_vec(t, V + NLV_Q + 128 * q, g);
+      init_vec_lds(t, pipe.v(), g);
       linear<DT, 8, 4>(t, n, w, lane);
       if (valid) store_row(t, qo + (int64_t)v * 3 * HID + q * HID, g);
     }
