@@ -82,8 +82,11 @@ def physical_cores():
     return max(len(seen), 1), len(cpus)
 
 
-def kernel_units(kind, nodes, edges, l1l2):
+def kernel_units(kind, nodes, edges, l1l2, esz=2):
     """(algorithmic FLOPs, algorithmic HBM bytes) of one launch."""
+    if kind == "node_aggr":
+        # per in-edge: the gathered V row, its 4 alphas, its source id; per node: in_ptr + the fp32 row out
+        return None, edges * (H * esz + 16 + 4) + nodes * (4 + H * 4)
     if kind in EDGE_MAC:
         return 2.0 * EDGE_MAC[kind] * edges, None
     if kind.startswith("node"):
@@ -264,6 +267,8 @@ def main():
     ap.add_argument("--layers", type=int, default=None, help="GeoT layers (default 2; c5: 4)")
     ap.add_argument("--node-limit", type=int, default=None,
                     help="max_num_graph_nodes of the synthetic model (default 2304; c5: 4096)")
+    ap.add_argument("--edge-kernel", type=int, default=None, choices=[0, 1],
+                    help="bf16 edge-layer kernel (di_edge_config): 0 two 4-wave blocks per CU, 1 grouped/lean form")
     ap.add_argument("--lib", default=None, help="tuning: a launch-shape variant of the HIP library "
                                                  "(deepinteract_amd.build.build_variant)")
     args = ap.parse_args()
@@ -303,6 +308,11 @@ def main():
     cfg = GeoTConfig(num_gnn_layers=args.layers, knn=k, node_count_limit=args.node_limit)
     sd = seeded_state_dict(0, cfg, with_head=False)
     eng = GeoTEngine(sd, args.dtype, cfg, device=dev)
+    if args.edge_kernel is not None:
+        _lib_check = eng.lib.di_edge_config(args.edge_kernel)
+        if _lib_check < 0:
+            raise SystemExit(f"di_edge_config({args.edge_kernel}) failed")
+    edge_kernel = eng.lib.di_edge_config(-1)
     num_cus = torch.cuda.get_device_properties(dev).multi_processor_count
     if args.pair_cus:
         if not args.overlap:
@@ -420,7 +430,7 @@ def main():
     for name, pairs in events.items():
         ms = [s.elapsed_time(e) for s, e in pairs]
         avg_s = float(np.mean(ms)) / 1e3
-        flops, byts = kernel_units(name, nodes, edges, l1l2)
+        flops, byts = kernel_units(name, nodes, edges, l1l2, esz)
         rec = {"launches": len(ms), "avg_us": avg_s * 1e6, "total_ms": float(np.sum(ms))}
         if flops is not None:
             rec["tflops"] = flops / avg_s / 1e12
@@ -461,7 +471,8 @@ def main():
                    + (f"; pair on {args.pair_cus} dedicated CUs ({args.cu_layout}), GeoT on "
                       f"{num_cus - args.pair_cus}" if args.pair_cus else "")
                    + f"; pair kernel {args.pair_kernel}"
-                   + (f", pace {args.pair_pace}" if args.pair_pace else "")},
+                   + (f", pace {args.pair_pace}" if args.pair_pace else "")
+                   + f"; edge-layer kernel {['k_edge_layer', 'k_edge_lean'][edge_kernel] if args.dtype == 'bf16' else 'k_edge_layer (f32)'}"},
         "hbm_frac_of_peak": round(hbm_frac, 4),
         "mfma_frac_of_peak": round(mfma_frac, 4),
         "algorithmic_per_complex": {"bytes": bytes_c, "flops": flops_c,

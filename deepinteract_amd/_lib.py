@@ -39,7 +39,10 @@ _SIGS = {
     "di_init_edge": ([ctypes.POINTER(DiGraph), _I, _P, _P, _P, _P, _P, _P, _P, _P], ctypes.c_int),
     "di_edge_layer": ([ctypes.POINTER(DiGraph), _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
                       ctypes.c_int),
+    "di_edge_config": ([_I], ctypes.c_int),
     "di_node_layer": ([ctypes.POINTER(DiGraph), _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P], ctypes.c_int),
+    "di_node_aggregate": ([ctypes.POINTER(DiGraph), _I, _P, _P, _P, _P], ctypes.c_int),
+    "di_node_update": ([ctypes.POINTER(DiGraph), _I, _I, _P, _P, _P, _P, _P, _P, _P, _P], ctypes.c_int),
     "di_pair_tensor": ([_I, _P, _I, _I, _I, _I, _I, _P, _P, _I, _P, _P], ctypes.c_int),
     "di_pair_config": ([_I, _I, _I], ctypes.c_int),
     "di_pair_pace": ([_I], ctypes.c_int),

@@ -225,6 +225,15 @@ __device__ __forceinline__ void silu2_(Act<NB>& a) {
     for (int r = 0; r < 4; ++r) a.v[b][r] = silu2<FAST>(a.v[b][r]);
 }
 
+// Pin an activation: an empty asm that reads and rewrites its registers, so every value is
+// computed HERE. Without it the compiler may sink a chain of VALU work (a gate product, a running
+// sum's terms) past later stages to its last use, keeping all the chain's inputs live meanwhile.
+template <int NB>
+__device__ __forceinline__ void pin(Act<NB>& a) {
+#pragma unroll
+  for (int b = 0; b < NB; ++b) asm volatile("" : "+v"(a.v[b]));
+}
+
 // a += k * b (one v_fma per value: folds the ln(2) of a log2-unit SiLU output into a residual add)
 template <int NB>
 __device__ __forceinline__ void add_scaled_(Act<NB>& a, const Act<NB>& b_, float k) {
@@ -323,10 +332,41 @@ struct DmaPump {
     }
   }
 };
+// Explicitly pipelined form (DI_MMA_ORDER 4): A fragments read DI_MMA_DEPTH MFMAs ahead of their
+// use through a register ring, with scheduling fences between steps, so at most DEPTH fragments
+// (4 VGPRs each) are live: bounds register pressure for the 4-waves-per-SIMD kernels.
+#ifndef DI_MMA_DEPTH
+#define DI_MMA_DEPTH 3
+#endif
+template <int NBO, int NS>
+__device__ __forceinline__ void mma_ring(Act<NBO>& out, const Op<BF16T, NS>& op, const u16* w, int lane) {
+  constexpr int G = NBO < 2 ? NBO : 2;
+  constexpr int N = NBO * NS;
+  constexpr int D = DI_MMA_DEPTH < N ? DI_MMA_DEPTH : N;
+  // step i -> (output block, k-step), output-block-pair major
+  auto blk = [](int i) { return (i / (G * NS)) * G + (i % G); };
+  auto kst = [](int i) { return (i % (G * NS)) / G; };
+  bf16x8 fr[D];
+#pragma unroll
+  for (int i = 0; i < D; ++i)
+    fr[i] = *reinterpret_cast<const bf16x8*>(w + (blk(i) * NS + kst(i)) * BLK + lane * 8);
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    __builtin_amdgcn_sched_barrier(0);
+    const int bo = blk(i), s = kst(i);
+    out.v[bo] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[i % D], op.f[s], out.v[bo], 0, 0, 0);
+    if (i + D < N)
+      fr[i % D] = *reinterpret_cast<const bf16x8*>(w + (blk(i + D) * NS + kst(i + D)) * BLK + lane * 8);
+  }
+  __builtin_amdgcn_sched_barrier(0);
+}
+
 template <int NBO, int NS>
 __device__ __forceinline__ void mma(Act<NBO>& out, const Op<BF16T, NS>& op, const u16* w, int lane,
                                     DmaPump* pp = nullptr) {
-  if constexpr (DI_MMA_ORDER == 0 || DI_MMA_ORDER == 2) {  // k-step major
+  if constexpr (DI_MMA_ORDER == 4) {
+    mma_ring<NBO, NS>(out, op, w, lane);
+  } else if constexpr (DI_MMA_ORDER == 0 || DI_MMA_ORDER == 2) {  // k-step major
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
 #pragma unroll

@@ -63,6 +63,7 @@ struct EdgeArgs {
 
 struct NodeArgs {
   int Nt;
+  const float* attn;  // optional [Nt, 128] aggregated attention rows (k_node_aggr); null: gather here
   void* hT_out;  // optional [128, Nt] transposed copy of h_out (pair-tensor input)
   const int* src;
   const int* in_ptr;
@@ -672,6 +673,489 @@ void k_edge_layer(EdgeArgs a) {
   }
 }
 
+// ================================================================ fused edge layer, grouped form (bf16)
+// The same stage sequence and arithmetic as k_edge_layer<BF16T, 0/1>, with each wave carrying
+// LG independent 16-row groups through every weight stage (LG = 2: 128 rows per 4-wave block and
+// weight pass, so every LDS-DMA'd stage and every stage barrier serves twice the rows of
+// k_edge_layer; two blocks per CU as before). Within a stage the groups are computed one after
+// the other from the same LDS slot: their chains are independent, so one group's SiLU VALU work
+// can issue beside the other group's MFMAs.
+// Register diet (two waves per SIMD at 240 registers): one tile per block (no next-tile prefetch
+// state); the edge's own row F is re-read (L2-hot) for each of its uses instead of being held;
+// the dist gate is computed k-step by k-step and multiplied straight into the packed
+// downward_proj operand; the edge FFN accumulates into the residual e1.
+#ifndef DI_LEAN_NW
+#define DI_LEAN_NW 4
+#endif
+#ifndef DI_LEAN_G
+#define DI_LEAN_G 1
+#endif
+#ifndef DI_LEAN_VGPR
+#define DI_LEAN_VGPR 120  // x2 on gfx950 (unified file counted in pairs): 240 registers
+#endif
+#ifndef DI_LEAN_WPE
+#define DI_LEAN_WPE 2
+#endif
+// scheduling fence between row groups / phases (keeps the compiler from interleaving, and so
+// doubling the live state of, independent groups)
+#ifndef DI_LEAN_FENCE
+#define DI_LEAN_FENCE 1
+#endif
+// The memory clobber also keeps the groups' reads of the same LDS slot (A fragments, biases)
+// from being merged into one live copy shared by both groups.
+#define DI_FENCE()                                \
+  do {                                            \
+    if (DI_LEAN_FENCE) {                          \
+      asm volatile("" ::: "memory");              \
+      __builtin_amdgcn_sched_barrier(0);          \
+    }                                             \
+  } while (0)
+// MFMA chains of the lean kernel: the explicitly pipelined fragment ring (common.h mma_ring) by
+// default, which bounds the live A fragments (the compiler otherwise hoists most of a layer's
+// ds_reads and needs ~40 more registers)
+#ifndef DI_LEAN_RING
+#define DI_LEAN_RING 1
+#endif
+template <int NBO, int NS>
+__device__ __forceinline__ void lmma(Act<NBO>& out, const Op<BF16T, NS>& op, const u16* w, int lane) {
+  if constexpr (DI_LEAN_RING) mma_ring<NBO, NS>(out, op, w, lane);
+  else mma<NBO, NS>(out, op, w, lane);
+}
+struct Lean {
+  static constexpr int NW = DI_LEAN_NW;
+  static constexpr int LG = DI_LEAN_G;
+  static constexpr int THREADS = 64 * NW;
+  static constexpr int GROUP_ROWS = ROWS_PER_WAVE * NW;
+  static constexpr int ROWS = GROUP_ROWS * LG;
+};
+// DI_LEAN_DBUF=0: one synchronous stage slot per block (36.5 KiB), so three or four blocks fit in
+// a CU's LDS; each block's DMA wait is then covered by the other blocks' compute
+#ifndef DI_LEAN_DBUF
+#define DI_LEAN_DBUF 1
+#endif
+using LeanPipe = WPipe<u16, Lean::NW, DI_LEAN_DBUF != 0, EL_CAP, 128>;
+
+// stage sequencer of one tile: next() publishes stage i and issues the DMA of stage i + 1
+template <int NS>
+struct LeanStages {
+  LeanPipe& pipe;
+  const u16* W;
+  const float* V;
+  int i;
+  __device__ void issue(int s) {
+    const int vo = EL_VEC[s];
+    pipe.issue(W + EL_ORDER[s] * BLK, EL_SIZE[s], vo >= 0 ? V + vo : nullptr, 128);
+  }
+  __device__ const u16* next() {
+    const u16* w = pipe.next();
+    if (i + 1 < NS) issue(i + 1);
+    ++i;
+    return w;
+  }
+  __device__ const float* v() const { return pipe.v(); }
+};
+
+// y = W . x (+ bias from the stage's LDS slot); x as a packed operand
+template <int NBO, int NS>
+__device__ __forceinline__ void lin_op(Act<NBO>& y, const Op<BF16T, NS>& x, const u16* w, const float* bias, int lane,
+                                       int g) {
+  if (bias) init_vec_lds(y, bias, g);
+  else zero(y);
+  lmma<NBO, NS>(y, x, w, lane);
+}
+
+__device__ __forceinline__ void raw_op(Op<BF16T, 4>& o, const RawRow<u16>& r) {
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    o.f[k] = __builtin_bit_cast(bf16x8, (uint4){r.u[2 * k].x, r.u[2 * k].y, r.u[2 * k + 1].x, r.u[2 * k + 1].y});
+}
+
+// per-group row state
+struct LeanRow {
+  int e;
+  bool valid;
+};
+
+template <int NS>
+__device__ __forceinline__ void lean_res_block(Act<8> (&x)[Lean::LG], LeanStages<NS>& st, int lane, int g) {
+  Op<BF16T, 4> op[Lean::LG];
+#pragma unroll
+  for (int q = 0; q < Lean::LG; ++q) make_op(op[q], x[q]);
+#pragma unroll 1
+  for (int l = 0; l < 3; ++l) {
+    const u16* w = st.next();
+#pragma unroll
+    for (int q = 0; q < Lean::LG; ++q) {
+    DI_FENCE();
+      Act<8> t;
+      lin_op<8, 4>(t, op[q], w, st.v(), lane, g);
+      silu2_<8, true>(t);  // log2 units: folded into the next linear / the residual fma
+      if (l < 2) make_op(op[q], t);
+      else add_scaled_(x[q], t, silu2_unit<true>());
+    }
+  }
+}
+
+// y = silu2(W x + b); x = F + ln2 * y  (res_connect_linear / final_linear residual)
+// F rows are loaded BEFORE the stage's barrier and DMA issue: vmcnt retires in order, so a load
+// issued after the stage's LDS-DMA pieces would make its use wait for the whole weight stage.
+__device__ __forceinline__ void load_f(RawRow<u16> (&fr)[Lean::LG], const u16* const (&f_row)[Lean::LG], int g) {
+#pragma unroll
+  for (int q = 0; q < Lean::LG; ++q) fr[q].load(f_row[q], g);
+}
+
+__device__ __forceinline__ void lean_f_residual(Act<8> (&x)[Lean::LG], const u16* w, const float* v,
+                                                const RawRow<u16> (&fr)[Lean::LG], int lane, int g) {
+#pragma unroll
+  for (int q = 0; q < Lean::LG; ++q) {
+    DI_FENCE();
+    Op<BF16T, 4> op;
+    make_op(op, x[q]);
+    Act<8> y;
+    lin_op<8, 4>(y, op, w, v, lane, g);
+    silu2_<8, true>(y);
+    fr[q].to_act(x[q]);
+    add_scaled_(x[q], y, silu2_unit<true>());
+  }
+}
+
+template <int MODE>
+__global__ __attribute__((amdgpu_flat_work_group_size(1, 64 * DI_LEAN_NW), amdgpu_waves_per_eu(DI_LEAN_WPE, DI_LEAN_WPE),
+                          amdgpu_num_vgpr(DI_LEAN_VGPR)))
+void k_edge_lean(EdgeArgs a) {
+  constexpr bool FINAL = MODE == 1;
+  constexpr int NS = FINAL ? EL_NSTAGE_FINAL : EL_NSTAGE;
+  constexpr int LG = Lean::LG;
+  DI_GEOT_ENTRY();
+  __shared__ __attribute__((aligned(16))) char lds[(DI_LEAN_DBUF ? 2 : 1) * LeanPipe::SLOT_BYTES];
+  const int lane = lane_id(), g = lane >> 4;
+  const u16* fn_in = reinterpret_cast<const u16*>(a.fn_in);
+  const u16* qkv = reinterpret_cast<const u16*>(a.qkv);
+  LeanRow rw[LG];
+  const u16* f_row[LG];
+#pragma unroll
+  for (int q = 0; q < LG; ++q) {
+    DI_FENCE();
+    const int r = blockIdx.x * Lean::ROWS + q * Lean::GROUP_ROWS + (threadIdx.x >> 6) * ROWS_PER_WAVE + (threadIdx.x & 15);
+    rw[q].valid = r < a.Et;
+    rw[q].e = rw[q].valid ? r : a.Et - 1;
+    f_row[q] = reinterpret_cast<const u16*>(a.f_in) + (int64_t)rw[q].e * HID;
+  }
+
+  LeanPipe pipe(lds);
+  LeanStages<NS> st{pipe, reinterpret_cast<const u16*>(a.wmat), a.wvec, 0};
+  st.issue(0);
+
+  Op<BF16T, 1> gop[LG];
+#pragma unroll
+  for (int q = 0; q < LG; ++q) {
+    DI_FENCE();
+    Act<2> geo;
+    load_edge_geo(geo, a.edge_f + (int64_t)rw[q].e * NFEAT_E, g);
+    make_op(gop[q], geo);
+  }
+  RawRow<u16> xn;  // the gathered neighbour row in flight (group-major order: q, then j)
+  int4 nb = *reinterpret_cast<const int4*>(a.nbr + (int64_t)rw[0].e * 4);
+  xn.load(fn_in + (int64_t)nb.x * HID, g);
+
+  // ---- neighbour-edge messages (conformation_module_message_func :384-418)
+  const u16* w = st.next();  // stage 0: geometric gates + downward_proj
+  Act<4> s[LG];
+#pragma unroll
+  for (int q = 0; q < LG; ++q) {
+    DI_FENCE();
+    Act<4> gate;
+    {
+      Act<4> t1;
+      zero(gate);
+      lmma<4, 1>(gate, gop[q], w + 8 * BLK, lane);
+      zero(t1);
+      lmma<4, 1>(t1, gop[q], w + 12 * BLK, lane);
+      mul_(gate, t1);
+      zero(t1);
+      lmma<4, 1>(t1, gop[q], w + 16 * BLK, lane);
+      mul_(gate, t1);
+      pin(gate);
+    }
+    zero(s[q]);
+    const int4 nbq = nb;
+    if (q + 1 < LG) nb = *reinterpret_cast<const int4*>(a.nbr + (int64_t)rw[q + 1].e * 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      DI_FENCE();
+      // x = silu(nbr_linear(F))[nbr_j] * dist gate, packed k-step by k-step
+      Op<BF16T, 4> xop;
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        // recomputed per neighbour (2 MFMAs per k-step) rather than held live across the loop:
+        // the memory clobber stops the compiler from merging the neighbours' copies (32 VGPRs)
+        asm volatile("" ::: "memory");
+        DI_FENCE();
+        Act<2> dg;
+        zero(dg);
+        lmma<2, 1>(dg, gop[q], w + 2 * ks * BLK, lane);
+        // opaque until here: keeps the compiler from unpacking the whole gathered row to fp32 as
+        // soon as it lands (32 registers instead of 16)
+        asm volatile("" : "+v"(xn.u[2 * ks]), "+v"(xn.u[2 * ks + 1]));
+        const uint2 lo = xn.u[2 * ks], hi = xn.u[2 * ks + 1];
+        uint4 u;
+        u.x = pack_bf16x2(__builtin_bit_cast(float, lo.x << 16) * dg.v[0][0],
+                          __builtin_bit_cast(float, lo.x & 0xffff0000u) * dg.v[0][1]);
+        u.y = pack_bf16x2(__builtin_bit_cast(float, lo.y << 16) * dg.v[0][2],
+                          __builtin_bit_cast(float, lo.y & 0xffff0000u) * dg.v[0][3]);
+        u.z = pack_bf16x2(__builtin_bit_cast(float, hi.x << 16) * dg.v[1][0],
+                          __builtin_bit_cast(float, hi.x & 0xffff0000u) * dg.v[1][1]);
+        u.w = pack_bf16x2(__builtin_bit_cast(float, hi.y << 16) * dg.v[1][2],
+                          __builtin_bit_cast(float, hi.y & 0xffff0000u) * dg.v[1][3]);
+        xop.f[ks] = __builtin_bit_cast(bf16x8, u);
+      }
+      // the next gathered row, in flight under this one's downward_proj
+      if (j < 3) {
+        const int nx = j == 0 ? nbq.y : (j == 1 ? nbq.z : nbq.w);
+        xn.load(fn_in + (int64_t)nx * HID, g);
+      } else if (q + 1 < LG) {
+        xn.load(fn_in + (int64_t)nb.x * HID, g);
+      }
+      DI_FENCE();
+      Act<4> y;
+      zero(y);
+      lmma<4, 4>(y, xop, w + 20 * BLK, lane);  // downward_proj
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) s[q].v[b][r] += silu2<true>(y.v[b][r]) * gate.v[b][r];
+      pin(s[q]);
+    }
+  }
+  Act<8> x[LG];
+  RawRow<u16> fr[LG];
+  {
+    w = st.next();  // stage 1: upward_proj (+ orig_msg_linear bias)
+#pragma unroll
+    for (int q = 0; q < LG; ++q) {
+    DI_FENCE();
+      Op<BF16T, 2> sop;
+      make_op(sop, s[q]);
+      lin_op<8, 2>(x[q], sop, w, nullptr, lane, g);
+      silu2_<8, true>(x[q]);
+      Act<8> bo;
+      init_vec_lds(bo, st.v(), g);
+#pragma unroll
+      for (int b = 0; b < 8; ++b) x[q].v[b] = silu2_unit<true>() * x[q].v[b] + bo.v[b];
+    }
+  }
+  load_f(fr, f_row, g);
+  {
+    w = st.next();  // stage 2: orig_msg_linear(res) + nbr
+#pragma unroll
+    for (int q = 0; q < LG; ++q) {
+    DI_FENCE();
+      Op<BF16T, 4> fop;
+      raw_op(fop, fr[q]);
+      lmma<8, 4>(x[q], fop, w, lane);
+    }
+  }
+  lean_res_block(x, st, lane, g);
+  lean_res_block(x, st, lane, g);
+  load_f(fr, f_row, g);
+  w = st.next();  // res_connect_linear: x = F + silu(rc(x))
+  lean_f_residual(x, w, st.v(), fr, lane, g);
+  lean_res_block(x, st, lane, g);
+  lean_res_block(x, st, lane, g);
+  w = st.next();  // final geometric gate
+#pragma unroll
+  for (int q = 0; q < LG; ++q) {
+    DI_FENCE();
+    Act<8> fg;
+    zero(fg);
+    lmma<8, 1>(fg, gop[q], w, lane);
+    mul_(x[q], fg);
+  }
+  load_f(fr, f_row, g);
+  w = st.next();  // final_linear: x = F + silu(final(x)) = conformation output
+  lean_f_residual(x, w, st.v(), fr, lane, g);
+
+  // ---- attention scores (propagate_attention :76-91)
+  RawRow<u16> kr[LG], qr[LG];  // K[src], Q[dst]: issued before the stage barrier
+#pragma unroll
+  for (int q = 0; q < LG; ++q) {
+    DI_FENCE();
+    const int e = rw[q].e;
+    kr[q].load(qkv + (int64_t)a.src[e] * 3 * HID + HID, g);
+    qr[q].load(qkv + (int64_t)a.dst[e] * 3 * HID, g);
+  }
+  w = st.next();  // edge_feats_projection(BN1e(conf))
+  Op<BF16T, 4> pop[LG];
+#pragma unroll
+  for (int q = 0; q < LG; ++q) {
+    DI_FENCE();
+    const int e = rw[q].e;
+    Op<BF16T, 4> op;
+    make_op(op, x[q]);
+    Act<8> p;
+    lin_op<8, 4>(p, op, w, st.v(), lane, g);
+    Act<8> kq, qd;
+    kr[q].to_act(kq);
+    qr[q].to_act(qd);
+#pragma unroll
+    for (int b = 0; b < 8; ++b)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float sc = (kq.v[b][r] * qd.v[b][r]) * (1.0f / 5.656854249492381f);  // / np.sqrt(32)
+        sc = fminf(fmaxf(sc, -5.f), 5.f);
+        p.v[b][r] = sc * p.v[b][r];  // score = e_out
+      }
+    floatx4 al;
+#pragma unroll
+    for (int h = 0; h < 4; ++h) al[h] = expf_<true>(fminf(fmaxf(head_sum(p, h), -5.f), 5.f));
+    if (rw[q].valid && g == 0) st4(a.alpha_out + (int64_t)e * 4, al);
+    if constexpr (!FINAL) make_op(pop[q], p);
+  }
+  if constexpr (!FINAL) {
+    // ---- edge output: e = in + O_e(e_out); e = e + FFN(BN2e(e)) (:697-724)
+    load_f(fr, f_row, g);
+    w = st.next();  // O_edge_feats
+    Act<8> e1[LG];
+#pragma unroll
+    for (int q = 0; q < LG; ++q) {
+    DI_FENCE();
+      init_vec_lds(e1[q], st.v(), g);
+      lmma<8, 4>(e1[q], pop[q], w, lane);
+      Act<8> fa;
+      fr[q].to_act(fa);
+      add_(e1[q], fa);
+    }
+    Op<BF16T, 4> eop[LG];
+#pragma unroll
+    for (int q = 0; q < LG; ++q) make_op(eop[q], e1[q]);
+#pragma unroll 1
+    for (int half = 0; half < 2; ++half) {
+      w = st.next();  // edge_feats_MLP.0 (BN2e folded), hidden half
+      Op<BF16T, 4> top[LG];
+#pragma unroll
+      for (int q = 0; q < LG; ++q) {
+    DI_FENCE();
+        Act<8> t;
+        lin_op<8, 4>(t, eop[q], w, st.v(), lane, g);
+        silu2_<8, true>(t);
+        make_op(top[q], t);
+      }
+      w = st.next();  // edge_feats_MLP.3, input half: accumulated into the residual
+#pragma unroll
+      for (int q = 0; q < LG; ++q) lmma<8, 4>(e1[q], top[q], w, lane);
+    }
+#pragma unroll
+    for (int q = 0; q < LG; ++q) {
+    DI_FENCE();
+      if (rw[q].valid) store_row(e1[q], reinterpret_cast<u16*>(a.f_out) + (int64_t)rw[q].e * HID, g);
+      make_op(eop[q], e1[q]);
+    }
+    w = st.next();  // next layer's silu(nbr_linear(.))
+#pragma unroll
+    for (int q = 0; q < LG; ++q) {
+    DI_FENCE();
+      Act<8> fn;
+      lin_op<8, 4>(fn, eop[q], w, st.v(), lane, g);
+      silu_<8, true>(fn);
+      if (rw[q].valid) store_row(fn, reinterpret_cast<u16*>(a.fn_out) + (int64_t)rw[q].e * HID, g);
+    }
+  }
+}
+
+// edge-layer kernel choice (di_edge_config): 0 = k_edge_layer (two 4-wave blocks per CU, 16 rows
+// per wave), 1 = k_edge_lean (two 4-wave blocks per CU, Lean::LG 16-row groups per wave)
+static int g_edge_kernel = 0;
+
+// ================================================================ node aggregation (CSR segment sum)
+// h_attn[v] = sum_{e in in(v)} alpha[e, head] * V[src e]  /  (sum_e alpha[e, head] + 1e-6)
+// (send_and_recv(u_mul_e('V_h','score'), sum) and (copy_e('score'), sum), then wV / (z + 1e-6):
+// deepinteract_modules.py:93-96, 116). Edges are destination-major (CSR in_ptr), so a node's
+// in-edges are one contiguous range.
+// 16 lanes per destination, 8 features (16 B of bf16) per lane: a gathered V row is one coalesced
+// 256-B access. In-edges go in chunks of U: the chunk's source ids arrive with ONE coalesced load
+// (lane j of the node's 16 reads src[e0 + j], broadcast by ds_bpermute) and the next chunk's ids are
+// in flight while this chunk's alphas and V rows land, so a chunk costs one memory latency; U rows
+// per lane in flight and 16 nodes per 256-thread block (grid = Nt / 16, several blocks per CU) hide
+// it. The products are added one edge at a time in edge order with the same fused multiply-adds as
+// the fused node kernel, so h_attn is bit-identical to what k_node_layer computes internally.
+template <class DT>
+struct AggrCfg {
+  static constexpr int U = DT::kBF16 ? 16 : 8;  // in-edges per chunk (V bytes in flight per lane: U x 16/32)
+};
+struct AggrArgs {
+  int Nt;
+  const int* src;
+  const int* in_ptr;
+  const float* alpha;
+  const void* qkv;
+  float* attn;
+};
+
+template <class DT>
+__global__ __launch_bounds__(256) void k_node_aggr(AggrArgs a) {
+  using T = typename DT::T;
+  constexpr int U = AggrCfg<DT>::U;
+  constexpr int FPL = 8;  // features per lane
+  const int j = threadIdx.x & 15;
+  const int v = blockIdx.x * 16 + (threadIdx.x >> 4);
+  if (v >= a.Nt) return;  // whole 16-lane groups exit together (shuffles stay within a group)
+  const int head = (FPL * j) >> 5;
+  const T* vbase = reinterpret_cast<const T*>(a.qkv) + 2 * HID + FPL * j;
+  const int e0 = a.in_ptr[v], e1 = a.in_ptr[v + 1];
+  float acc[FPL];
+#pragma unroll
+  for (int f = 0; f < FPL; ++f) acc[f] = 0.f;
+  float z = 0.f;
+  const int lane_base = threadIdx.x & 48;  // first lane of this node's 16 (within the wave)
+  int id_next = e0 + j < e1 ? a.src[e0 + j] : 0;
+#pragma unroll 1
+  for (int c = e0; c < e1; c += U) {
+    const int n = min(U, e1 - c);
+    // this chunk's ids (lanes 0..n-1 of the group hold them) and alphas / V rows in flight
+    const int id_cur = id_next;
+    int ids[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) ids[u] = __shfl(id_cur, lane_base + (u & 15), 64);
+    float al[U];
+    T vv[U][FPL];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (u < n) {
+        al[u] = a.alpha[(int64_t)(c + u) * 4 + head];
+        const T* row = vbase + (int64_t)ids[u] * 3 * HID;
+        if constexpr (DT::kBF16) {
+          *reinterpret_cast<uint4*>(vv[u]) = *reinterpret_cast<const uint4*>(row);
+        } else {
+          *reinterpret_cast<float4*>(vv[u]) = *reinterpret_cast<const float4*>(row);
+          *reinterpret_cast<float4*>(vv[u] + 4) = *reinterpret_cast<const float4*>(row + 4);
+        }
+      }
+    }
+    // ids of the next chunk (U <= 16 lanes of the group)
+    if (c + U < e1) id_next = c + U + j < e1 && j < U ? a.src[c + U + j] : 0;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (u < n) {
+#pragma unroll
+        for (int f = 0; f < FPL; ++f) {
+          float x;
+          if constexpr (DT::kBF16) x = __builtin_bit_cast(float, (uint32_t)vv[u][f] << 16);
+          else x = vv[u][f];
+          acc[f] += al[u] * x;
+        }
+        z += al[u];
+      }
+    }
+  }
+  const float d = z + 1e-6f;
+  float4 o0, o1;
+  o0.x = acc[0] / d; o0.y = acc[1] / d; o0.z = acc[2] / d; o0.w = acc[3] / d;
+  o1.x = acc[4] / d; o1.y = acc[5] / d; o1.z = acc[6] / d; o1.w = acc[7] / d;
+  float* out = a.attn + (int64_t)v * HID + FPL * j;
+  *reinterpret_cast<float4*>(out) = o0;
+  *reinterpret_cast<float4*>(out + 4) = o1;
+}
+
 // ================================================================ fused node layer
 // Every bias vector rides in its stage's LDS slot (init_vec_lds) and the node's own input row is
 // added right after the stage barrier, before the next stage's DMA is issued: a global load
@@ -700,6 +1184,9 @@ __global__ __launch_bounds__(THREADS, 2) void k_node_layer(NodeArgs a) {
 
   // send_and_recv(u_mul_e('V_h','score'), sum) and (copy_e('score'), sum); h = wV / (z + 1e-6)
   Act<8> wv;
+  if (a.attn != nullptr) {  // aggregated by k_node_aggr (same products, order and division)
+    load_row(wv, a.attn + (int64_t)v * HID, g);
+  } else {
   zero(wv);
   floatx4 z = {0.f, 0.f, 0.f, 0.f};
   // In-edges in groups of UNR: the group's source ids, alphas and V[src] rows are all in flight
@@ -743,6 +1230,7 @@ __global__ __launch_bounds__(THREADS, 2) void k_node_layer(NodeArgs a) {
     const float d = z[b >> 1] + 1e-6f;
 #pragma unroll
     for (int q = 0; q < 4; ++q) wv.v[b][q] = wv.v[b][q] / d;
+  }
   }
   // n = in1 + O_node(h)
   const T* w = pipe.next();
@@ -878,7 +1366,11 @@ extern "C" int di_edge_layer(const di_graph* g, di_dtype dt, int final_layer, co
   EdgeArgs a{g->num_edges, edge_f, g->src, g->dst, g->nbr, f_in, fn_in, qkv, wmat, wvec, alpha_out,
              f_out, fn_out};
   hipStream_t s = (hipStream_t)stream;
-  if (dt == DI_BF16) {
+  if (dt == DI_BF16 && g_edge_kernel == 1) {
+    dim3 grid(grid_rows(a.Et, Lean::ROWS)), block(Lean::THREADS);
+    if (final_layer) hipLaunchKernelGGL((k_edge_lean<1>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((k_edge_lean<0>), grid, block, 0, s, a);
+  } else if (dt == DI_BF16) {
     // persistent: two resident blocks per CU
 #ifndef DI_EDGE_PERSIST
 #define DI_EDGE_PERSIST 0
@@ -896,6 +1388,13 @@ extern "C" int di_edge_layer(const di_graph* g, di_dtype dt, int final_layer, co
     else hipLaunchKernelGGL((k_edge_layer<F32T, 0>), grid, block, 0, s, a);
   }
   return launch_status();
+}
+
+extern "C" int di_edge_config(int32_t kernel) {
+  if (kernel < -1 || kernel > 1) return DI_EINVAL;
+  const int prev = g_edge_kernel;
+  if (kernel >= 0) g_edge_kernel = kernel;
+  return prev;
 }
 
 extern "C" int di_conformation(const di_graph* g, di_dtype dt, const float* edge_f, const void* f_in,
@@ -920,7 +1419,36 @@ extern "C" int di_node_layer(const di_graph* g, di_dtype dt, int final_layer, co
                              void* h_out, void* qkv_out, void* hT_out, void* stream) {
   if (!g || !alpha || !h_in || !qkv || !wmat || !wvec || !h_out || g->num_nodes <= 0) return DI_EINVAL;
   if (!final_layer && !qkv_out) return DI_EINVAL;
-  NodeArgs a{g->num_nodes, hT_out, g->src, g->in_ptr, alpha, h_in, qkv, wmat, wvec, h_out, qkv_out};
+  NodeArgs a{g->num_nodes, nullptr, hT_out, g->src, g->in_ptr, alpha, h_in, qkv, wmat, wvec, h_out, qkv_out};
+  hipStream_t s = (hipStream_t)stream;
+  dim3 grid(grid_rows(a.Nt)), block(THREADS);
+  if (dt == DI_BF16) {
+    if (final_layer) hipLaunchKernelGGL((k_node_layer<BF16T, true>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((k_node_layer<BF16T, false>), grid, block, 0, s, a);
+  } else {
+    if (final_layer) hipLaunchKernelGGL((k_node_layer<F32T, true>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((k_node_layer<F32T, false>), grid, block, 0, s, a);
+  }
+  return launch_status();
+}
+
+extern "C" int di_node_aggregate(const di_graph* g, di_dtype dt, const float* alpha, const void* qkv, float* attn_out,
+                                 void* stream) {
+  if (!g || !alpha || !qkv || !attn_out || !g->src || !g->in_ptr || g->num_nodes <= 0) return DI_EINVAL;
+  AggrArgs a{g->num_nodes, g->src, g->in_ptr, alpha, qkv, attn_out};
+  hipStream_t s = (hipStream_t)stream;
+  dim3 grid((a.Nt + 15) / 16), block(256);
+  if (dt == DI_BF16) hipLaunchKernelGGL(k_node_aggr<BF16T>, grid, block, 0, s, a);
+  else hipLaunchKernelGGL(k_node_aggr<F32T>, grid, block, 0, s, a);
+  return launch_status();
+}
+
+extern "C" int di_node_update(const di_graph* g, di_dtype dt, int final_layer, const float* attn, const void* h_in,
+                              const void* wmat, const float* wvec, void* h_out, void* qkv_out, void* hT_out,
+                              void* stream) {
+  if (!g || !attn || !h_in || !wmat || !wvec || !h_out || g->num_nodes <= 0) return DI_EINVAL;
+  if (!final_layer && !qkv_out) return DI_EINVAL;
+  NodeArgs a{g->num_nodes, attn, hT_out, nullptr, nullptr, nullptr, h_in, nullptr, wmat, wvec, h_out, qkv_out};
   hipStream_t s = (hipStream_t)stream;
   dim3 grid(grid_rows(a.Nt)), block(THREADS);
   if (dt == DI_BF16) {

@@ -82,6 +82,10 @@ class GeoTEngine:
         self.packed = PackedGeoT(state_dict, dtype, cfg, self.device)
         self._check_blob_sizes()
         self._ws = {}
+        # node layer as two launches (di_node_aggregate + di_node_update; bit-identical to the
+        # fused di_node_layer): the segment reduction at full occupancy instead of 16 lanes per
+        # node inside the MFMA kernel's one-block-per-CU grid
+        self.split_node = True
 
     def _check_blob_sizes(self):
         p, dt = self.packed, _DI_DT[self.dtype]
@@ -118,13 +122,15 @@ class GeoTEngine:
                 "f": [torch.empty(ce, H, dtype=dt, device=dev) for _ in range(2)],
                 "fn": [torch.empty(ce, H, dtype=dt, device=dev) for _ in range(2)],
                 "alpha": torch.empty(ce, 4, dtype=torch.float32, device=dev),
+                "attn": torch.empty(cn, H, dtype=torch.float32, device=dev),
                 "hT": torch.empty(H * cn, dtype=dt, device=dev),
             })
         b, H = cap[1], self.cfg.num_gnn_hidden_channels
         return {
             "h": [t[:num_nodes] for t in b["h"]], "qkv": [t[:num_nodes] for t in b["qkv"]],
             "f": [t[:num_edges] for t in b["f"]], "fn": [t[:num_edges] for t in b["fn"]],
-            "alpha": b["alpha"][:num_edges], "hT": b["hT"][:H * num_nodes].view(H, num_nodes),
+            "alpha": b["alpha"][:num_edges], "attn": b["attn"][:num_nodes],
+            "hT": b["hT"][:H * num_nodes].view(H, num_nodes),
         }
 
     def forward(self, gb: GraphBatch, clone: bool = True, events=None, slot: int = 0, after_init=None):
@@ -167,10 +173,20 @@ class GeoTEngine:
                                          _ptr(None if final else f[nxt]), _ptr(None if final else fn[nxt]),
                                          st), "di_edge_layer")
             nm, nv = p.node[li]
-            tick("node_layer_final" if final else "node_layer")
-            _lib.check(lib.di_node_layer(g, dt, int(final), _ptr(alpha), _ptr(h[cur]), _ptr(qkv[cur]),
-                                         _ptr(nm), _ptr(nv), _ptr(h[nxt]), _ptr(None if final else qkv[nxt]),
-                                         _ptr(ws["hT"] if final else None), st), "di_node_layer")
+            if self.split_node:
+                # CSR segment reduction of the attention messages, then O_node / FFN / next Q,K,V
+                tick("node_aggr")
+                _lib.check(lib.di_node_aggregate(g, dt, _ptr(alpha), _ptr(qkv[cur]), _ptr(ws["attn"]), st),
+                           "di_node_aggregate")
+                tick("node_layer_final" if final else "node_layer")
+                _lib.check(lib.di_node_update(g, dt, int(final), _ptr(ws["attn"]), _ptr(h[cur]), _ptr(nm), _ptr(nv),
+                                              _ptr(h[nxt]), _ptr(None if final else qkv[nxt]),
+                                              _ptr(ws["hT"] if final else None), st), "di_node_update")
+            else:
+                tick("node_layer_final" if final else "node_layer")
+                _lib.check(lib.di_node_layer(g, dt, int(final), _ptr(alpha), _ptr(h[cur]), _ptr(qkv[cur]),
+                                             _ptr(nm), _ptr(nv), _ptr(h[nxt]), _ptr(None if final else qkv[nxt]),
+                                             _ptr(ws["hT"] if final else None), st), "di_node_layer")
             if not final:
                 f_out = nxt
             cur = nxt

@@ -97,11 +97,26 @@ int di_edge_layer(const di_graph* g, di_dtype dt, int final_layer, const float* 
                   const void* f_in, const void* fn_in, const void* qkv,
                   const void* wmat, const float* wvec,
                   float* alpha_out /*[Et,4]*/, void* f_out, void* fn_out, void* stream);
+/* Edge-layer kernel of the bf16 path (process-wide scheduling knob, not a reference interface):
+ * 0 = two 4-wave blocks per CU (240 registers per wave), 1 = lean form, two 8-wave blocks per CU
+ * (120 registers, four waves per SIMD). -1 only queries. Returns the previous choice. */
+int di_edge_config(int32_t kernel);
 
 /* hT_out (optional, may be NULL): also write h_out transposed, [128, Nt] (pair-tensor input) */
 int di_node_layer(const di_graph* g, di_dtype dt, int final_layer, const float* alpha,
                   const void* h_in, const void* qkv, const void* wmat, const float* wvec,
                   void* h_out, void* qkv_out, void* hT_out, void* stream);
+/* The node layer in two launches (what GeoTEngine runs): the attention aggregation as a CSR
+ * segment reduction over each node's in-edges (replaces send_and_recv(u_mul_e, sum) +
+ * (copy_e, sum) + wV / (z + 1e-6), deepinteract_modules.py:93-96, 116):
+ *   attn_out[v, :] = sum_{e: dst(e) = v} alpha[e, head] * V[src(e), :] / (sum_e alpha[e, head] + 1e-6)
+ * (fp32 [Nt, 128]; V = columns 256..383 of qkv), then O_node + residual + FFN (+ next layer's
+ * Q/K/V, + optional transposed copy) from those rows. Bit-identical to di_node_layer. */
+int di_node_aggregate(const di_graph* g, di_dtype dt, const float* alpha /*[Et,4]*/, const void* qkv /*[Nt,384]*/,
+                      float* attn_out /*[Nt,128]*/, void* stream);
+int di_node_update(const di_graph* g, di_dtype dt, int final_layer, const float* attn /*[Nt,128]*/,
+                   const void* h_in, const void* wmat, const float* wvec, void* h_out, void* qkv_out,
+                   void* hT_out, void* stream);
 
 /* h [Nt, hidden] node features; hT (optional, may be NULL) the same transposed [hidden, Nt]
  * (di_node_layer's hT_out), which turns chain-2 column reads into 16-B vector loads.

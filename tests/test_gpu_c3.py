@@ -34,8 +34,9 @@ def _oracle_graph(gb, g):
             "edge_f": gb.edge_f[e0:e1].cpu()}
 
 
-def test_c3_bench_path_bf16_two_slots_two_streams():
-    from deepinteract_amd import synth
+@pytest.mark.parametrize("edge_kernel", [0, 1])
+def test_c3_bench_path_bf16_two_slots_two_streams(edge_kernel):
+    from deepinteract_amd import _lib, synth
     from deepinteract_amd.builder import build_graph_batch
     from deepinteract_amd.engine import GeoTEngine, PairTensorOp
     from deepinteract_amd.graph import select_graphs
@@ -53,6 +54,7 @@ def test_c3_bench_path_bf16_two_slots_two_streams():
     h2r = [gb0.node_off[2 * j + 1] for j in range(M)]
     l1 = l2 = [N_RES] * M
     pair = PairTensorOp(kernel="vector")
+    prev = _lib.load().di_edge_config(edge_kernel)
     try:
         s_geot = torch.cuda.current_stream()
         s_pair = torch.cuda.Stream()
@@ -76,7 +78,8 @@ def test_c3_bench_path_bf16_two_slots_two_streams():
             keep.append((hc, ec, views))
         torch.cuda.synchronize()
     finally:
-        PairTensorOp(kernel="rows")  # process-wide launch knob back to its default
+        PairTensorOp(kernel="rows")  # process-wide launch knobs back to their defaults
+        _lib.load().di_edge_config(prev)
 
     errs = {}
     for m, j in ((0, 0), (0, 5), (2, 3)):
@@ -103,5 +106,5 @@ def test_c3_bench_path_bf16_two_slots_two_streams():
         pt = O.pair_tensor(ref[0], ref[1])[0].numpy()
         got = t[0][torch.as_tensor(idx[:, 0]), torch.as_tensor(idx[:, 1]), torch.as_tensor(idx[:, 2])]
         errs[f"mb{m}_c{j}_pair"] = rel_max(got.float().cpu().numpy(), pt[idx[:, 0], idx[:, 1], idx[:, 2]])
-    print("C3 bf16 errors (max-abs / max-abs ref):", {k: f"{v:.3e}" for k, v in errs.items()})
+    print(f"C3 bf16 errors, edge kernel {edge_kernel} (max-abs / max-abs ref):", {k: f"{v:.3e}" for k, v in errs.items()})
     assert max(errs.values()) < BF16_GEOT_TOL, errs

@@ -17,6 +17,20 @@ VARIANTS = {
     "xcd": ["DI_XCD_TILES=1"],
     "prio1": ["DI_GEOT_PRIO=1"],
     "persist": ["DI_EDGE_PERSIST=1"],
+    # grouped/lean edge layer (bench --edge-kernel 1): waves per block, waves per SIMD, VGPR cap / 2
+    "lean4": ["DI_LEAN_NW=4", "DI_LEAN_WPE=2", "DI_LEAN_VGPR=120"],
+    "lean6": ["DI_LEAN_NW=6", "DI_LEAN_WPE=3", "DI_LEAN_VGPR=80"],
+    "lean8": ["DI_LEAN_NW=8", "DI_LEAN_WPE=4", "DI_LEAN_VGPR=64"],
+    "lean12": ["DI_LEAN_NW=12", "DI_LEAN_WPE=3", "DI_LEAN_VGPR=80"],
+    "lean4d6": ["DI_LEAN_NW=4", "DI_LEAN_WPE=2", "DI_LEAN_VGPR=120", "DI_MMA_DEPTH=6"],
+    "lean4d10": ["DI_LEAN_NW=4", "DI_LEAN_WPE=2", "DI_LEAN_VGPR=120", "DI_MMA_DEPTH=10"],
+    "lean12d6": ["DI_LEAN_NW=12", "DI_LEAN_WPE=3", "DI_LEAN_VGPR=80", "DI_MMA_DEPTH=6"],
+    "lean8d5": ["DI_LEAN_NW=8", "DI_LEAN_WPE=4", "DI_LEAN_VGPR=64", "DI_MMA_DEPTH=5"],
+    "base_ring8": ["DI_MMA_ORDER=4", "DI_MMA_DEPTH=8"],
+    "lean4s3": ["DI_LEAN_NW=4", "DI_LEAN_WPE=3", "DI_LEAN_VGPR=80", "DI_LEAN_DBUF=0", "DI_MMA_DEPTH=6"],
+    "lean4s4": ["DI_LEAN_NW=4", "DI_LEAN_WPE=4", "DI_LEAN_VGPR=64", "DI_LEAN_DBUF=0", "DI_MMA_DEPTH=5"],
+    "lean8d5v60": ["DI_LEAN_NW=8", "DI_LEAN_WPE=4", "DI_LEAN_VGPR=60", "DI_MMA_DEPTH=5"],
+    "lean4g2": ["DI_LEAN_NW=4", "DI_LEAN_WPE=2", "DI_LEAN_VGPR=120", "DI_LEAN_G=2"],
 }
 
 if __name__ == "__main__":
