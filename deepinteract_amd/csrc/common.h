@@ -266,6 +266,11 @@ struct Op<F32T, NS> {
 };
 
 template <int NS>
+__device__ __forceinline__ void pin(Op<BF16T, NS>& o) {
+#pragma unroll
+  for (int s = 0; s < NS; ++s) asm volatile("" : "+v"(o.f[s]));
+}
+template <int NS>
 __device__ __forceinline__ void make_op(Op<BF16T, NS>& o, const Act<2 * NS>& a) {
 #pragma unroll
   for (int s = 0; s < NS; ++s) {

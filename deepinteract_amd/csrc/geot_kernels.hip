@@ -790,8 +790,13 @@ __device__ __forceinline__ void lean_res_block(Act<8> (&x)[Lean::LG], LeanStages
       Act<8> t;
       lin_op<8, 4>(t, op[q], w, st.v(), lane, g);
       silu2_<8, true>(t);  // log2 units: folded into the next linear / the residual fma
-      if (l < 2) make_op(op[q], t);
-      else add_scaled_(x[q], t, silu2_unit<true>());
+      if (l < 2) {
+        make_op(op[q], t);
+        pin(op[q]);
+      } else {
+        add_scaled_(x[q], t, silu2_unit<true>());
+        pin(x[q]);
+      }
     }
   }
 }
@@ -816,6 +821,7 @@ __device__ __forceinline__ void lean_f_residual(Act<8> (&x)[Lean::LG], const u16
     silu2_<8, true>(y);
     fr[q].to_act(x[q]);
     add_scaled_(x[q], y, silu2_unit<true>());
+    pin(x[q]);
   }
 }
 
@@ -942,6 +948,7 @@ void k_edge_lean(EdgeArgs a) {
       init_vec_lds(bo, st.v(), g);
 #pragma unroll
       for (int b = 0; b < 8; ++b) x[q].v[b] = silu2_unit<true>() * x[q].v[b] + bo.v[b];
+      pin(x[q]);
     }
   }
   load_f(fr, f_row, g);
@@ -953,6 +960,7 @@ void k_edge_lean(EdgeArgs a) {
       Op<BF16T, 4> fop;
       raw_op(fop, fr[q]);
       lmma<8, 4>(x[q], fop, w, lane);
+      pin(x[q]);
     }
   }
   lean_res_block(x, st, lane, g);
@@ -970,6 +978,7 @@ void k_edge_lean(EdgeArgs a) {
     zero(fg);
     lmma<8, 1>(fg, gop[q], w, lane);
     mul_(x[q], fg);
+    pin(x[q]);
   }
   load_f(fr, f_row, g);
   w = st.next();  // final_linear: x = F + silu(final(x)) = conformation output
@@ -1009,7 +1018,10 @@ void k_edge_lean(EdgeArgs a) {
 #pragma unroll
     for (int h = 0; h < 4; ++h) al[h] = expf_<true>(fminf(fmaxf(head_sum(p, h), -5.f), 5.f));
     if (rw[q].valid && g == 0) st4(a.alpha_out + (int64_t)e * 4, al);
-    if constexpr (!FINAL) make_op(pop[q], p);
+    if constexpr (!FINAL) {
+      make_op(pop[q], p);
+      pin(pop[q]);
+    }
   }
   if constexpr (!FINAL) {
     // ---- edge output: e = in + O_e(e_out); e = e + FFN(BN2e(e)) (:697-724)
@@ -1024,10 +1036,14 @@ void k_edge_lean(EdgeArgs a) {
       Act<8> fa;
       fr[q].to_act(fa);
       add_(e1[q], fa);
+      pin(e1[q]);
     }
     Op<BF16T, 4> eop[LG];
 #pragma unroll
-    for (int q = 0; q < LG; ++q) make_op(eop[q], e1[q]);
+    for (int q = 0; q < LG; ++q) {
+      make_op(eop[q], e1[q]);
+      pin(eop[q]);
+    }
 #pragma unroll 1
     for (int half = 0; half < 2; ++half) {
       w = st.next();  // edge_feats_MLP.0 (BN2e folded), hidden half
@@ -1039,10 +1055,15 @@ void k_edge_lean(EdgeArgs a) {
         lin_op<8, 4>(t, eop[q], w, st.v(), lane, g);
         silu2_<8, true>(t);
         make_op(top[q], t);
+        pin(top[q]);
       }
       w = st.next();  // edge_feats_MLP.3, input half: accumulated into the residual
 #pragma unroll
-      for (int q = 0; q < LG; ++q) lmma<8, 4>(e1[q], top[q], w, lane);
+      for (int q = 0; q < LG; ++q) {
+        DI_FENCE();
+        lmma<8, 4>(e1[q], top[q], w, lane);
+        pin(e1[q]);
+      }
     }
 #pragma unroll
     for (int q = 0; q < LG; ++q) {

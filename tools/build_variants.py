@@ -31,6 +31,8 @@ VARIANTS = {
     "lean4s4": ["DI_LEAN_NW=4", "DI_LEAN_WPE=4", "DI_LEAN_VGPR=64", "DI_LEAN_DBUF=0", "DI_MMA_DEPTH=5"],
     "lean8d5v60": ["DI_LEAN_NW=8", "DI_LEAN_WPE=4", "DI_LEAN_VGPR=60", "DI_MMA_DEPTH=5"],
     "lean4g2": ["DI_LEAN_NW=4", "DI_LEAN_WPE=2", "DI_LEAN_VGPR=120", "DI_LEAN_G=2"],
+    "lean4g2d6": ["DI_LEAN_NW=4", "DI_LEAN_WPE=2", "DI_LEAN_VGPR=120", "DI_LEAN_G=2", "DI_MMA_DEPTH=6"],
+    "lean8g2": ["DI_LEAN_NW=8", "DI_LEAN_WPE=2", "DI_LEAN_VGPR=120", "DI_LEAN_G=2", "DI_MMA_DEPTH=6"],
 }
 
 if __name__ == "__main__":
