@@ -721,6 +721,11 @@ __device__ __forceinline__ void lmma(Act<NBO>& out, const Op<BF16T, NS>& op, con
   if constexpr (DI_LEAN_RING) mma_ring<NBO, NS>(out, op, w, lane);
   else mma<NBO, NS>(out, op, w, lane);
 }
+// DI_LEAN_HOLD_F=1: the edge's own F rows stay in registers (16 per group) from stage 2 through
+// final_linear (three uses, one read) instead of being re-read (L2 / HBM) for each use
+#ifndef DI_LEAN_HOLD_F
+#define DI_LEAN_HOLD_F 0
+#endif
 struct Lean {
   static constexpr int NW = DI_LEAN_NW;
   static constexpr int LG = DI_LEAN_G;
@@ -965,7 +970,7 @@ void k_edge_lean(EdgeArgs a) {
   }
   lean_res_block(x, st, lane, g);
   lean_res_block(x, st, lane, g);
-  load_f(fr, f_row, g);
+  if (!DI_LEAN_HOLD_F) load_f(fr, f_row, g);
   w = st.next();  // res_connect_linear: x = F + silu(rc(x))
   lean_f_residual(x, w, st.v(), fr, lane, g);
   lean_res_block(x, st, lane, g);
@@ -980,7 +985,7 @@ void k_edge_lean(EdgeArgs a) {
     mul_(x[q], fg);
     pin(x[q]);
   }
-  load_f(fr, f_row, g);
+  if (!DI_LEAN_HOLD_F) load_f(fr, f_row, g);
   w = st.next();  // final_linear: x = F + silu(final(x)) = conformation output
   lean_f_residual(x, w, st.v(), fr, lane, g);
 
@@ -1025,7 +1030,7 @@ void k_edge_lean(EdgeArgs a) {
   }
   if constexpr (!FINAL) {
     // ---- edge output: e = in + O_e(e_out); e = e + FFN(BN2e(e)) (:697-724)
-    load_f(fr, f_row, g);
+    load_f(fr, f_row, g);  // O_edge: re-read (the attention stage has no room for it)
     w = st.next();  // O_edge_feats
     Act<8> e1[LG];
 #pragma unroll
@@ -1175,6 +1180,129 @@ __global__ __launch_bounds__(256) void k_node_aggr(AggrArgs a) {
   float* out = a.attn + (int64_t)v * HID + FPL * j;
   *reinterpret_cast<float4*>(out) = o0;
   *reinterpret_cast<float4*>(out + 4) = o1;
+}
+
+// ================================================================ node update (bf16), 4-slot weight ring
+// O_node + residual + FFN (+ next layer's Q/K/V, + hT) from the aggregated rows of k_node_aggr.
+// Nt / 64 blocks is one block per CU, so a stage's 32 MFMAs per wave (~0.3 us) are far shorter than
+// an LDS-DMA stage's landing latency (~1 us): the double-buffered pipe of k_node_layer waits on
+// every stage. Here ALL the layer's biases land once at entry and the 32-KiB stages stream through
+// a 4-slot ring, three stages ahead: entering stage s the wave waits only for its own pieces of
+// stage s (s_waitcnt vmcnt(8 x stages issued after it): each wave issues exactly 8 one-KiB pieces
+// per stage, and every other vector-memory operation is older than them: outputs are held in
+// registers and stored at the end), then a barrier publishes the stage and frees the slot of
+// stage s-1 for stage s+3. Arithmetic identical to k_node_layer (same operands, same order).
+constexpr int NU_SLOTS = 4;
+constexpr int NU_STAGE = MAT128;  // blocks per stage
+__device__ __forceinline__ void nu_wait_younger(int n_stages_younger) {
+  // vmcnt takes an immediate: the three counts this ring can need
+  if (n_stages_younger >= 2) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  else if (n_stages_younger == 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+template <bool FINAL>
+__global__ __launch_bounds__(THREADS, 1) void k_node_update_ring(NodeArgs a) {
+  constexpr int NS = FINAL ? 5 : 8;
+  constexpr int NVEC = FINAL ? NLV_N_FINAL : NLV_N;
+  // one LDS object: [4 ring slots | all biases]
+  __shared__ __attribute__((aligned(16))) char lds[NU_SLOTS * NU_STAGE * BLK * 2 + NLV_N * 4];
+  u16* wring = reinterpret_cast<u16*>(lds);
+  float* vlds = reinterpret_cast<float*>(lds + NU_SLOTS * NU_STAGE * BLK * 2);
+  const int lane = lane_id(), g = lane >> 4;
+  const int r = row_id<WAVES>();
+  const bool valid = r < a.Nt;
+  const int v = valid ? r : a.Nt - 1;
+  const u16* W = reinterpret_cast<const u16*>(a.wmat);
+  // stage s -> first packed block
+  auto stage_blk = [](int s) {
+    return s == 0 ? NL_ON : (s == 1 ? NL_F1 : (s == 2 ? NL_F2 : (s == 3 ? NL_F1 + MAT128 : (s == 4 ? NL_F2 + MAT128 : NL_Q + MAT128 * (s - 5)))));
+  };
+  auto issue = [&](int s) { dma_blocks<WAVES>(wring + (s % NU_SLOTS) * NU_STAGE * BLK, W + stage_blk(s) * BLK, NU_STAGE); };
+  // biases and stage 0, then this node's rows, landed here (the compiler cannot count the DMA
+  // loops, so a row used later would make it wait for every stage in flight), then stages 1-2
+  dma_vec<WAVES>(vlds, a.wvec, NVEC / 128);
+  issue(0);
+  RawRow<u16> hin;
+  hin.load(reinterpret_cast<const u16*>(a.h_in) + (int64_t)v * HID, g);
+  Act<8> wv;
+  load_row(wv, a.attn + (int64_t)v * HID, g);
+  settle(hin);
+#pragma unroll
+  for (int b = 0; b < 8; ++b) asm volatile("" ::"v"(wv.v[b]));
+  issue(1);
+  issue(2);
+  auto enter = [&](int s) -> const u16* {
+    nu_wait_younger(min(2, NS - 1 - s));
+    // a bare s_barrier: __syncthreads()' workgroup fence would wait for every outstanding
+    // vector-memory operation, i.e. also for the stages in flight behind this one
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (s + 3 < NS) issue(s + 3);
+    return wring + (s % NU_SLOTS) * NU_STAGE * BLK;
+  };
+  // n = in1 + O_node(h)
+  const u16* w = enter(0);
+  Act<8> n;
+  init_vec_lds(n, vlds + NLV_ON, g);
+  {
+    Act<8> hv;
+    hin.to_act(hv);
+    add_(n, hv);
+  }
+  linear<BF16T, 8, 4>(n, wv, w, lane);
+  // n = n + W2 silu(W1 BN2(n))
+  Act<8> o;
+  zero(o);
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+    w = enter(1 + 2 * half);
+    Act<8> t;
+    init_vec_lds(t, vlds + NLV_F1 + 128 * half, g);
+    linear<BF16T, 8, 4>(t, n, w, lane);
+    silu2_<8, true>(t);
+    w = enter(2 + 2 * half);
+    linear<BF16T, 8, 4>(o, t, w, lane);
+  }
+  add_(n, o);
+  if constexpr (FINAL) {
+    if (valid) store_row(n, reinterpret_cast<u16*>(a.h_out) + (int64_t)v * HID, g);
+    if (a.hT_out != nullptr && valid) {
+      u16* hT = reinterpret_cast<u16*>(a.hT_out);
+#pragma unroll
+      for (int b = 0; b < 8; ++b)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          hT[(int64_t)(16 * b + 4 * g + q) * a.Nt + v] = (u16)(pack_bf16x2(n.v[b][q], 0.f) & 0xffffu);
+    }
+  } else {
+    Op<BF16T, 4> nop;
+    make_op(nop, n);  // bf16 bits of n: the h_out row and the Q/K/V operand
+    Op<BF16T, 4> qkv_rows[3];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      w = enter(5 + q);
+      Act<8> t;
+      init_vec_lds(t, vlds + NLV_Q + 128 * q, g);
+      mma<8, 4>(t, nop, w, lane);
+      make_op(qkv_rows[q], t);
+    }
+    if (valid) {
+      // packed operand -> row-major bf16: f[s] = {blk 2s regs 0-3, blk 2s+1 regs 0-3} = 4+4 features
+      auto store_op = [&](const Op<BF16T, 4>& op, u16* row) {
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const uint4 u = __builtin_bit_cast(uint4, op.f[s]);
+          *reinterpret_cast<uint2*>(row + 16 * (2 * s) + 4 * g) = (uint2){u.x, u.y};
+          *reinterpret_cast<uint2*>(row + 16 * (2 * s + 1) + 4 * g) = (uint2){u.z, u.w};
+        }
+      };
+      store_op(nop, reinterpret_cast<u16*>(a.h_out) + (int64_t)v * HID);
+      u16* qo = reinterpret_cast<u16*>(a.qkv_out) + (int64_t)v * 3 * HID;
+#pragma unroll
+      for (int q = 0; q < 3; ++q) store_op(qkv_rows[q], qo + q * HID);
+    }
+  }
 }
 
 // ================================================================ fused node layer
@@ -1473,8 +1601,8 @@ extern "C" int di_node_update(const di_graph* g, di_dtype dt, int final_layer, c
   hipStream_t s = (hipStream_t)stream;
   dim3 grid(grid_rows(a.Nt)), block(THREADS);
   if (dt == DI_BF16) {
-    if (final_layer) hipLaunchKernelGGL((k_node_layer<BF16T, true>), grid, block, 0, s, a);
-    else hipLaunchKernelGGL((k_node_layer<BF16T, false>), grid, block, 0, s, a);
+    if (final_layer) hipLaunchKernelGGL((k_node_update_ring<true>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((k_node_update_ring<false>), grid, block, 0, s, a);
   } else {
     if (final_layer) hipLaunchKernelGGL((k_node_layer<F32T, true>), grid, block, 0, s, a);
     else hipLaunchKernelGGL((k_node_layer<F32T, false>), grid, block, 0, s, a);
