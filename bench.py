@@ -269,6 +269,8 @@ def main():
                     help="max_num_graph_nodes of the synthetic model (default 2304; c5: 4096)")
     ap.add_argument("--edge-kernel", type=int, default=None, choices=[0, 1],
                     help="bf16 edge-layer kernel (di_edge_config): 0 two 4-wave blocks per CU, 1 grouped/lean form")
+    ap.add_argument("--only", default=None, choices=["geot", "pair"],
+                    help="diagnostic (not the metric): run only the GeoT stream or only the pair-tensor stream")
     ap.add_argument("--lib", default=None, help="tuning: a launch-shape variant of the HIP library "
                                                  "(deepinteract_amd.build.build_variant)")
     args = ap.parse_args()
@@ -366,6 +368,7 @@ def main():
     else:
         s_geot = torch.cuda.current_stream(dev)
         s_pair = torch.cuda.Stream(dev) if args.overlap else s_geot
+    pair_only_inputs = {}  # --only pair: each slot's GeoT outputs, computed once in the warm-up
     done = [None, None]  # per workspace slot: event after the pair tensor that last read it
 
     def launch_pair(h, hT, ready, slot, after=None, events=None):
@@ -391,10 +394,17 @@ def main():
             with torch.cuda.stream(s_geot):
                 if done[slot] is not None:
                     s_geot.wait_event(done[slot])
-                h, _ = eng.forward(gb, clone=False, events=events, slot=slot, after_init=after)
-                hT = eng.last_hT
+                if args.only == "pair" and slot in pair_only_inputs:
+                    h, hT = pair_only_inputs[slot]
+                else:
+                    h, _ = eng.forward(gb, clone=False, events=events, slot=slot, after_init=after)
+                    hT = eng.last_hT
+                    if args.only == "pair":
+                        pair_only_inputs[slot] = (h, hT)
                 ready = torch.cuda.Event()
                 ready.record(s_geot)
+            if args.only == "geot":
+                continue
             if args.overlap == 2:
                 if prev is not None:
                     launch_pair(*prev, after=after, events=events)
@@ -471,6 +481,7 @@ def main():
                    + (f"; pair on {args.pair_cus} dedicated CUs ({args.cu_layout}), GeoT on "
                       f"{num_cus - args.pair_cus}" if args.pair_cus else "")
                    + f"; pair kernel {args.pair_kernel}"
+                   + (f"; DIAGNOSTIC: {args.only} stream only (not the metric)" if args.only else "")
                    + (f", pace {args.pair_pace}" if args.pair_pace else "")
                    + f"; edge-layer kernel {['k_edge_layer', 'k_edge_lean'][edge_kernel] if args.dtype == 'bf16' else 'k_edge_layer (f32)'}"},
         "hbm_frac_of_peak": round(hbm_frac, 4),
