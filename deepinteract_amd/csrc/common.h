@@ -341,7 +341,7 @@ struct DmaPump {
 // use through a register ring, with scheduling fences between steps, so at most DEPTH fragments
 // (4 VGPRs each) are live: bounds register pressure for the 4-waves-per-SIMD kernels.
 #ifndef DI_MMA_DEPTH
-#define DI_MMA_DEPTH 3
+#define DI_MMA_DEPTH 4
 #endif
 template <int NBO, int NS>
 __device__ __forceinline__ void mma_ring(Act<NBO>& out, const Op<BF16T, NS>& op, const u16* w, int lane) {

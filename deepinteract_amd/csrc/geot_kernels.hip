@@ -688,7 +688,7 @@ void k_edge_layer(EdgeArgs a) {
 #define DI_LEAN_NW 4
 #endif
 #ifndef DI_LEAN_G
-#define DI_LEAN_G 1
+#define DI_LEAN_G 2
 #endif
 #ifndef DI_LEAN_VGPR
 #define DI_LEAN_VGPR 120  // x2 on gfx950 (unified file counted in pairs): 240 registers
@@ -721,6 +721,51 @@ __device__ __forceinline__ void lmma(Act<NBO>& out, const Op<BF16T, NS>& op, con
   if constexpr (DI_LEAN_RING) mma_ring<NBO, NS>(out, op, w, lane);
   else mma<NBO, NS>(out, op, w, lane);
 }
+// Both row groups through one pass over the stage's A fragments: every LDS fragment read feeds
+// one MFMA per group (half the ds_reads per row; tools/diag/mfma_shape_bench.hip V1 vs V0:
+// 336 vs 375 us on the bare compute core). Both groups' accumulators are live across the loop.
+#ifndef DI_LEAN_SHARE
+#define DI_LEAN_SHARE 1
+#endif
+template <int NBO, int NS>
+__device__ __forceinline__ void mma_ring2(Act<NBO>& o0, Act<NBO>& o1, const Op<BF16T, NS>& a0, const Op<BF16T, NS>& a1,
+                                          const u16* w, int lane) {
+  constexpr int G = NBO < 2 ? NBO : 2;
+  constexpr int N = NBO * NS;
+  constexpr int D = DI_MMA_DEPTH < N ? DI_MMA_DEPTH : N;
+  auto blk = [](int i) { return (i / (G * NS)) * G + (i % G); };
+  auto kst = [](int i) { return (i % (G * NS)) / G; };
+  bf16x8 fr[D];
+#pragma unroll
+  for (int i = 0; i < D; ++i)
+    fr[i] = *reinterpret_cast<const bf16x8*>(w + (blk(i) * NS + kst(i)) * BLK + lane * 8);
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    __builtin_amdgcn_sched_barrier(0);
+    const int bo = blk(i), s = kst(i);
+    o0.v[bo] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[i % D], a0.f[s], o0.v[bo], 0, 0, 0);
+    o1.v[bo] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[i % D], a1.f[s], o1.v[bo], 0, 0, 0);
+    if (i + D < N)
+      fr[i % D] = *reinterpret_cast<const bf16x8*>(w + (blk(i + D) * NS + kst(i + D)) * BLK + lane * 8);
+  }
+  __builtin_amdgcn_sched_barrier(0);
+}
+// out[q] (= bias or 0) += W . op[q] for every row group
+template <int LG, int NBO, int NS>
+__device__ __forceinline__ void lin_groups(Act<NBO> (&out)[LG], const Op<BF16T, NS> (&op)[LG], const u16* w,
+                                           const float* bias, int lane, int g) {
+#pragma unroll
+  for (int q = 0; q < LG; ++q) {
+    if (bias) init_vec_lds(out[q], bias, g);
+    else zero(out[q]);
+  }
+  if constexpr (LG == 2 && DI_LEAN_SHARE) {
+    mma_ring2<NBO, NS>(out[0], out[1], op[0], op[1], w, lane);
+  } else {
+#pragma unroll
+    for (int q = 0; q < LG; ++q) lmma<NBO, NS>(out[q], op[q], w, lane);
+  }
+}
 // DI_LEAN_HOLD_F=1: the edge's own F rows stay in registers (16 per group) from stage 2 through
 // final_linear (three uses, one read) instead of being re-read (L2 / HBM) for each use
 #ifndef DI_LEAN_HOLD_F
@@ -732,6 +777,7 @@ struct Lean {
   static constexpr int THREADS = 64 * NW;
   static constexpr int GROUP_ROWS = ROWS_PER_WAVE * NW;
   static constexpr int ROWS = GROUP_ROWS * LG;
+  static constexpr bool SHARED = LG == 2 && DI_LEAN_SHARE;  // groups share each A fragment
 };
 // DI_LEAN_DBUF=0: one synchronous stage slot per block (36.5 KiB), so three or four blocks fit in
 // a CU's LDS; each block's DMA wait is then covered by the other blocks' compute
@@ -789,18 +835,35 @@ __device__ __forceinline__ void lean_res_block(Act<8> (&x)[Lean::LG], LeanStages
 #pragma unroll 1
   for (int l = 0; l < 3; ++l) {
     const u16* w = st.next();
+    if constexpr (Lean::SHARED) {
+      Act<8> t[Lean::LG];
+      lin_groups<Lean::LG, 8, 4>(t, op, w, st.v(), lane, g);
 #pragma unroll
-    for (int q = 0; q < Lean::LG; ++q) {
-    DI_FENCE();
-      Act<8> t;
-      lin_op<8, 4>(t, op[q], w, st.v(), lane, g);
-      silu2_<8, true>(t);  // log2 units: folded into the next linear / the residual fma
-      if (l < 2) {
-        make_op(op[q], t);
-        pin(op[q]);
-      } else {
-        add_scaled_(x[q], t, silu2_unit<true>());
-        pin(x[q]);
+      for (int q = 0; q < Lean::LG; ++q) {
+        DI_FENCE();
+        silu2_<8, true>(t[q]);
+        if (l < 2) {
+          make_op(op[q], t[q]);
+          pin(op[q]);
+        } else {
+          add_scaled_(x[q], t[q], silu2_unit<true>());
+          pin(x[q]);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < Lean::LG; ++q) {
+        DI_FENCE();
+        Act<8> t;
+        lin_op<8, 4>(t, op[q], w, st.v(), lane, g);
+        silu2_<8, true>(t);  // log2 units: folded into the next linear / the residual fma
+        if (l < 2) {
+          make_op(op[q], t);
+          pin(op[q]);
+        } else {
+          add_scaled_(x[q], t, silu2_unit<true>());
+          pin(x[q]);
+        }
       }
     }
   }
@@ -816,6 +879,22 @@ __device__ __forceinline__ void load_f(RawRow<u16> (&fr)[Lean::LG], const u16* c
 
 __device__ __forceinline__ void lean_f_residual(Act<8> (&x)[Lean::LG], const u16* w, const float* v,
                                                 const RawRow<u16> (&fr)[Lean::LG], int lane, int g) {
+  if constexpr (Lean::SHARED) {
+    Op<BF16T, 4> op[Lean::LG];
+#pragma unroll
+    for (int q = 0; q < Lean::LG; ++q) make_op(op[q], x[q]);
+    Act<8> y[Lean::LG];
+    lin_groups<Lean::LG, 8, 4>(y, op, w, v, lane, g);
+#pragma unroll
+    for (int q = 0; q < Lean::LG; ++q) {
+      DI_FENCE();
+      silu2_<8, true>(y[q]);
+      fr[q].to_act(x[q]);
+      add_scaled_(x[q], y[q], silu2_unit<true>());
+      pin(x[q]);
+    }
+    return;
+  }
 #pragma unroll
   for (int q = 0; q < Lean::LG; ++q) {
     DI_FENCE();
@@ -959,13 +1038,22 @@ void k_edge_lean(EdgeArgs a) {
   load_f(fr, f_row, g);
   {
     w = st.next();  // stage 2: orig_msg_linear(res) + nbr
+    if constexpr (Lean::SHARED) {
+      Op<BF16T, 4> fop[LG];
 #pragma unroll
-    for (int q = 0; q < LG; ++q) {
-    DI_FENCE();
-      Op<BF16T, 4> fop;
-      raw_op(fop, fr[q]);
-      lmma<8, 4>(x[q], fop, w, lane);
-      pin(x[q]);
+      for (int q = 0; q < LG; ++q) raw_op(fop[q], fr[q]);
+      mma_ring2<8, 4>(x[0], x[1], fop[0], fop[1], w, lane);
+#pragma unroll
+      for (int q = 0; q < LG; ++q) pin(x[q]);
+    } else {
+#pragma unroll
+      for (int q = 0; q < LG; ++q) {
+        DI_FENCE();
+        Op<BF16T, 4> fop;
+        raw_op(fop, fr[q]);
+        lmma<8, 4>(x[q], fop, w, lane);
+        pin(x[q]);
+      }
     }
   }
   lean_res_block(x, st, lane, g);
@@ -1000,14 +1088,25 @@ void k_edge_lean(EdgeArgs a) {
   }
   w = st.next();  // edge_feats_projection(BN1e(conf))
   Op<BF16T, 4> pop[LG];
+  Act<8> pg[Lean::SHARED ? LG : 1];
+  if constexpr (Lean::SHARED) {
+    Op<BF16T, 4> xop[LG];
+#pragma unroll
+    for (int q = 0; q < LG; ++q) make_op(xop[q], x[q]);
+    lin_groups<LG, 8, 4>(pg, xop, w, st.v(), lane, g);
+  }
 #pragma unroll
   for (int q = 0; q < LG; ++q) {
     DI_FENCE();
     const int e = rw[q].e;
-    Op<BF16T, 4> op;
-    make_op(op, x[q]);
     Act<8> p;
-    lin_op<8, 4>(p, op, w, st.v(), lane, g);
+    if constexpr (Lean::SHARED) {
+      p = pg[q];
+    } else {
+      Op<BF16T, 4> op;
+      make_op(op, x[q]);
+      lin_op<8, 4>(p, op, w, st.v(), lane, g);
+    }
     Act<8> kq, qd;
     kr[q].to_act(kq);
     qr[q].to_act(qd);
@@ -1033,11 +1132,14 @@ void k_edge_lean(EdgeArgs a) {
     load_f(fr, f_row, g);  // O_edge: re-read (the attention stage has no room for it)
     w = st.next();  // O_edge_feats
     Act<8> e1[LG];
+    if constexpr (Lean::SHARED) lin_groups<LG, 8, 4>(e1, pop, w, st.v(), lane, g);
 #pragma unroll
     for (int q = 0; q < LG; ++q) {
-    DI_FENCE();
-      init_vec_lds(e1[q], st.v(), g);
-      lmma<8, 4>(e1[q], pop[q], w, lane);
+      DI_FENCE();
+      if constexpr (!Lean::SHARED) {
+        init_vec_lds(e1[q], st.v(), g);
+        lmma<8, 4>(e1[q], pop[q], w, lane);
+      }
       Act<8> fa;
       fr[q].to_act(fa);
       add_(e1[q], fa);
@@ -1053,21 +1155,39 @@ void k_edge_lean(EdgeArgs a) {
     for (int half = 0; half < 2; ++half) {
       w = st.next();  // edge_feats_MLP.0 (BN2e folded), hidden half
       Op<BF16T, 4> top[LG];
+      if constexpr (Lean::SHARED) {
+        Act<8> t[LG];
+        lin_groups<LG, 8, 4>(t, eop, w, st.v(), lane, g);
 #pragma unroll
-      for (int q = 0; q < LG; ++q) {
-    DI_FENCE();
-        Act<8> t;
-        lin_op<8, 4>(t, eop[q], w, st.v(), lane, g);
-        silu2_<8, true>(t);
-        make_op(top[q], t);
-        pin(top[q]);
+        for (int q = 0; q < LG; ++q) {
+          DI_FENCE();
+          silu2_<8, true>(t[q]);
+          make_op(top[q], t[q]);
+          pin(top[q]);
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < LG; ++q) {
+          DI_FENCE();
+          Act<8> t;
+          lin_op<8, 4>(t, eop[q], w, st.v(), lane, g);
+          silu2_<8, true>(t);
+          make_op(top[q], t);
+          pin(top[q]);
+        }
       }
       w = st.next();  // edge_feats_MLP.3, input half: accumulated into the residual
+      if constexpr (Lean::SHARED) {
+        mma_ring2<8, 4>(e1[0], e1[1], top[0], top[1], w, lane);
 #pragma unroll
-      for (int q = 0; q < LG; ++q) {
-        DI_FENCE();
-        lmma<8, 4>(e1[q], top[q], w, lane);
-        pin(e1[q]);
+        for (int q = 0; q < LG; ++q) pin(e1[q]);
+      } else {
+#pragma unroll
+        for (int q = 0; q < LG; ++q) {
+          DI_FENCE();
+          lmma<8, 4>(e1[q], top[q], w, lane);
+          pin(e1[q]);
+        }
       }
     }
 #pragma unroll
@@ -1077,11 +1197,14 @@ void k_edge_lean(EdgeArgs a) {
       make_op(eop[q], e1[q]);
     }
     w = st.next();  // next layer's silu(nbr_linear(.))
+    Act<8> fng[Lean::SHARED ? LG : 1];
+    if constexpr (Lean::SHARED) lin_groups<LG, 8, 4>(fng, eop, w, st.v(), lane, g);
 #pragma unroll
     for (int q = 0; q < LG; ++q) {
-    DI_FENCE();
+      DI_FENCE();
       Act<8> fn;
-      lin_op<8, 4>(fn, eop[q], w, st.v(), lane, g);
+      if constexpr (Lean::SHARED) fn = fng[q];
+      else lin_op<8, 4>(fn, eop[q], w, st.v(), lane, g);
       silu_<8, true>(fn);
       if (rw[q].valid) store_row(fn, reinterpret_cast<u16*>(a.fn_out) + (int64_t)rw[q].e * HID, g);
     }
@@ -1089,8 +1212,10 @@ void k_edge_lean(EdgeArgs a) {
 }
 
 // edge-layer kernel choice (di_edge_config): 0 = k_edge_layer (two 4-wave blocks per CU, 16 rows
-// per wave), 1 = k_edge_lean (two 4-wave blocks per CU, Lean::LG 16-row groups per wave)
-static int g_edge_kernel = 0;
+// per wave), 1 = k_edge_lean (two 4-wave blocks per CU, Lean::LG = 2 16-row groups per wave sharing
+// every A fragment; default: C3 micro-batch alone 446 vs 496 us, final 350 vs 383 us, overlapped
+// 5.3-5.4 k vs 5.2 k complexes/s)
+static int g_edge_kernel = 1;
 
 // ================================================================ node aggregation (CSR segment sum)
 // h_attn[v] = sum_{e in in(v)} alpha[e, head] * V[src e]  /  (sum_e alpha[e, head] + 1e-6)

@@ -11,3 +11,12 @@ if ROOT not in sys.path:
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs on the GPU box)")
     config.addinivalue_line("markers", "slow: long-running CPU test")
+
+
+def pytest_sessionstart(session):
+    # tuning only: DI_TEST_VARIANT=<path> runs the GPU tests against a kernel variant of the
+    # library (tools/build_variants.py) before it is made the default build
+    path = os.environ.get("DI_TEST_VARIANT")
+    if path:
+        from deepinteract_amd import _lib
+        _lib.load_variant(path)

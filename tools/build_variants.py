@@ -32,6 +32,8 @@ VARIANTS = {
     "lean8d5v60": ["DI_LEAN_NW=8", "DI_LEAN_WPE=4", "DI_LEAN_VGPR=60", "DI_MMA_DEPTH=5"],
     "lean4g2": ["DI_LEAN_NW=4", "DI_LEAN_WPE=2", "DI_LEAN_VGPR=120", "DI_LEAN_G=2"],
     "lean4g2d6": ["DI_LEAN_NW=4", "DI_LEAN_WPE=2", "DI_LEAN_VGPR=120", "DI_LEAN_G=2", "DI_MMA_DEPTH=6"],
+    "lean4g2ns": ["DI_LEAN_NW=4", "DI_LEAN_WPE=2", "DI_LEAN_VGPR=120", "DI_LEAN_G=2", "DI_LEAN_SHARE=0"],
+    "lean4g2d4": ["DI_LEAN_NW=4", "DI_LEAN_WPE=2", "DI_LEAN_VGPR=120", "DI_LEAN_G=2", "DI_MMA_DEPTH=4"],
     "lean8g2": ["DI_LEAN_NW=8", "DI_LEAN_WPE=2", "DI_LEAN_VGPR=120", "DI_LEAN_G=2", "DI_MMA_DEPTH=6"],
 }
 
