@@ -252,8 +252,9 @@ def main():
                     help="K > 0: pair tensor on a CU-masked stream of K dedicated CUs (K blocks x 8 waves), "
                          "GeoT on the other CUs (needs --overlap 1)")
     ap.add_argument("--cu-layout", default="stride", choices=["stride", "contig"])
-    ap.add_argument("--pair-kernel", default=None, choices=["rows", "vector"],
-                    help="aligned pair-tensor kernel (default: rows alone, vector beside GeoT)")
+    ap.add_argument("--pair-kernel", default=None, choices=["rows", "vector", "rows_bounded"],
+                    help="aligned pair-tensor kernel (default: rows alone, rows_bounded in 2-wave blocks "
+                         "beside GeoT)")
     ap.add_argument("--pair-blocks", type=int, default=0)
     ap.add_argument("--pair-waves", type=int, default=0)
     ap.add_argument("--pair-pace", type=int, default=None,
@@ -295,7 +296,9 @@ def main():
     args.node_limit = args.node_limit or 2304
 
     if args.pair_kernel is None:
-        args.pair_kernel = "vector" if args.overlap and not args.pair_cus else "rows"
+        args.pair_kernel = "rows_bounded" if args.overlap and not args.pair_cus else "rows"
+    if args.pair_kernel == "rows_bounded" and not args.pair_waves:
+        args.pair_waves = 2  # one 2-wave block per CU beside GeoT (4-wave blocks starve InitEdge)
     ws, rank, local = dist_setup()
     dev = torch.device("cuda", local)
     from deepinteract_amd import synth

@@ -143,8 +143,18 @@ __global__ __launch_bounds__(PAIR_THREADS) void k_pair_tensor(const di_pair_desc
 // Block size is a launch parameter (di_pair_config): 4 waves x one block per CU when the kernel
 // shares every CU with GeoT, 8 waves on a few dedicated CUs (CU-masked stream): 64 CUs alone
 // store 5.6 TB/s, 32 CUs 3.4 TB/s (C3 micro-batch of 8 complexes).
+// INFLIGHT = n > 0 (the "rows_bounded" kernel, di_pair_config kernel 3, the default beside GeoT):
+// after every row the wave waits until at most n of its stores are outstanding. The per-CU
+// vector-memory queue is in order, so a store-only wave that runs 60 stores ahead parks every
+// load of the co-resident GeoT waves (weight-stage DMA, gathers) behind ~1k cycles of store drain;
+// a bounded queue keeps GeoT's loads near the front. Measured beside GeoT (C3, 256 complexes,
+// one 2-wave block per CU): n = 1/2/3/4/6 -> 5.14/5.53/5.50/5.37-5.61/5.23 k complexes/s, the
+// unbounded rows kernel 5.01 k, the per-vector kernel 5.27-5.33 k; 4-wave blocks starve InitEdge.
+#ifndef DI_PAIR_INFLIGHT
+#define DI_PAIR_INFLIGHT 3
+#endif
 constexpr int PAIR_SEG = 128;  // 16-B chunks per row segment (2 per lane)
-template <typename T>
+template <typename T, int INFLIGHT>
 __global__ __launch_bounds__(1024) __attribute__((amdgpu_num_vgpr(32)))
 void k_pair_rows(const di_pair_desc* __restrict__ descs, int hidden, const T* __restrict__ h,
                  const T* __restrict__ hT, int nrows, int rblocks, int items, T* __restrict__ out, int pace) {
@@ -196,6 +206,8 @@ void k_pair_rows(const di_pair_desc* __restrict__ descs, int hidden, const T* __
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uintx4, v0), r, k0 * 16, soff, DI_PAIR_STORE);
         if (two && k1 < nch)
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uintx4, v1), r, k1 * 16, soff, DI_PAIR_STORE);
+        if constexpr (INFLIGHT > 0)  // bound this wave's queued stores (see DI_PAIR_INFLIGHT)
+          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(INFLIGHT) : "memory");
         for (int t = 0; t < pace; ++t) __builtin_amdgcn_s_sleep(1);  // store-rate pacing (di_pair_pace)
       }
     }
@@ -214,7 +226,8 @@ static int env_int(const char* name, int dflt) {
 }
 static int g_pair_blocks = env_int("DI_PAIR_BLOCKS", PAIR_MAX_BLOCKS);
 static int g_pair_waves = env_int("DI_PAIR_WAVES", 4);
-static int g_pair_kernel = env_int("DI_PAIR_KERNEL", 1);  // 1 row-streaming, 2 per-vector (aligned path)
+static int g_pair_kernel = env_int("DI_PAIR_KERNEL", 1);  // 1 row-streaming, 2 per-vector, 3 row-streaming
+                                                          // with bounded in-flight stores (aligned path)
 static int g_pair_pace = env_int("DI_PAIR_PACE", 0);      // s_sleep(1) (~64 clk) per row / per trip of stores
 
 // Store-rate pacing of the aligned pair kernels when they share the GPU with GeoT: each wave
@@ -227,7 +240,7 @@ extern "C" int di_pair_pace(int32_t pace) {
 }
 
 extern "C" int di_pair_config(int32_t blocks, int32_t waves_per_block, int32_t kernel) {
-  if (blocks < 0 || waves_per_block < 0 || waves_per_block > 16 || kernel < 0 || kernel > 2) return DI_EINVAL;
+  if (blocks < 0 || waves_per_block < 0 || waves_per_block > 16 || kernel < 0 || kernel > 3) return DI_EINVAL;
   if (blocks > 0) g_pair_blocks = blocks;
   if (waves_per_block > 0) g_pair_waves = waves_per_block;
   if (kernel > 0) g_pair_kernel = kernel;
@@ -252,18 +265,25 @@ extern "C" int di_pair_tensor(di_dtype dt, const di_pair_desc* descs, int32_t nu
   // elements: 16-B vector loads and non-temporal 16-B stores.
   const int vec = dt == DI_BF16 ? 8 : 4;
 #ifndef DI_PAIR_LEGACY
-  if (aligned16 && g_pair_kernel == 1) {
+  if (aligned16 && (g_pair_kernel == 1 || g_pair_kernel == 3)) {
     const int rows = 64 * g_pair_waves;  // rows per work item
     const int rblocks = (max_l1 + rows - 1) / rows;
     const int64_t ritems64 = (int64_t)num_complexes * 2 * hidden * rblocks;
     if (ritems64 > INT32_MAX) return DI_ERANGE;
     const int ritems = (int)ritems64;
     const unsigned rgrid = (unsigned)(ritems < max_blocks ? ritems : max_blocks);
-    if (dt == DI_BF16)
-      hipLaunchKernelGGL((k_pair_rows<u16>), dim3(rgrid), dim3(rows), 0, s, descs, hidden, (const u16*)h,
+    const bool bounded = g_pair_kernel == 3;
+    if (dt == DI_BF16 && bounded)
+      hipLaunchKernelGGL((k_pair_rows<u16, DI_PAIR_INFLIGHT>), dim3(rgrid), dim3(rows), 0, s, descs, hidden,
+                         (const u16*)h, (const u16*)hT, num_rows, rblocks, ritems, (u16*)out, g_pair_pace);
+    else if (dt == DI_BF16)
+      hipLaunchKernelGGL((k_pair_rows<u16, 0>), dim3(rgrid), dim3(rows), 0, s, descs, hidden, (const u16*)h,
                          (const u16*)hT, num_rows, rblocks, ritems, (u16*)out, g_pair_pace);
+    else if (bounded)
+      hipLaunchKernelGGL((k_pair_rows<float, DI_PAIR_INFLIGHT>), dim3(rgrid), dim3(rows), 0, s, descs, hidden,
+                         (const float*)h, (const float*)hT, num_rows, rblocks, ritems, (float*)out, g_pair_pace);
     else
-      hipLaunchKernelGGL((k_pair_rows<float>), dim3(rgrid), dim3(rows), 0, s, descs, hidden,
+      hipLaunchKernelGGL((k_pair_rows<float, 0>), dim3(rgrid), dim3(rows), 0, s, descs, hidden,
                          (const float*)h, (const float*)hT, num_rows, rblocks, ritems, (float*)out, g_pair_pace);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? DI_OK : (int)e;

@@ -202,11 +202,11 @@ class GeoTEngine:
 class PairTensorOp:
     """construct_interact_tensor (deepinteract_utils.py:158-172) for a batch of complexes."""
 
-    KERNELS = {"rows": 1, "vector": 2}
+    KERNELS = {"rows": 1, "vector": 2, "rows_bounded": 3}
 
     def __init__(self, device="cuda", blocks: int = 0, waves_per_block: int = 0, kernel: str | None = None,
                  pace: int | None = None):
-        """blocks / waves_per_block / kernel ("rows" | "vector"): launch shape and kernel of the
+        """blocks / waves_per_block / kernel ("rows" | "vector" | "rows_bounded"): launch shape and kernel of the
         16-B-aligned path (di_pair_config; 0 / None keep the library's current setting); pace:
         store-rate pacing, s_sleep(1) per row / vector trip (di_pair_pace; None keeps it)."""
         self.device = gpu_device(device)

@@ -125,9 +125,10 @@ int di_node_update(const di_graph* g, di_dtype dt, int final_layer, const float*
 /* Launch shape of the persistent pair-tensor kernels (process-wide; 0 keeps a value): `blocks`
  * resident blocks, `waves_per_block` (1..16) waves per row-streaming block, `kernel` for the
  * 16-B-aligned case: 1 row-streaming (loads hoisted out of the store stream; fastest alone),
- * 2 per-vector (one load per 16-B store; lighter on a GPU shared with GeoT). Defaults 256 / 4 /
- * 1 (env DI_PAIR_BLOCKS / DI_PAIR_WAVES / DI_PAIR_KERNEL). Not a reference interface: a
- * scheduling knob of this build. */
+ * 2 per-vector (one load per 16-B store), 3 row-streaming with at most a few stores in flight
+ * per wave (the schedule beside GeoT: its loads do not queue behind a long store backlog).
+ * Defaults 256 / 4 / 1 (env DI_PAIR_BLOCKS / DI_PAIR_WAVES / DI_PAIR_KERNEL). Not a reference
+ * interface: a scheduling knob of this build. */
 int di_pair_config(int32_t blocks, int32_t waves_per_block, int32_t kernel);
 /* Store-rate pacing of the aligned pair kernels (scheduling knob, not a reference interface):
  * every wave sleeps pace x ~64 clocks after each row (row kernel) / vector trip (vector kernel),

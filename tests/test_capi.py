@@ -39,7 +39,7 @@ def test_invalid_arguments_rejected_without_gpu():
     assert lib.di_pair_tensor(0, None, 0, 0, 0, 128, 1, None, None, 0, None, None) == -1
     assert lib.di_knn_topk(1, None, None, 20, 10, None, None, None) == -1
     assert lib.di_pair_config(-1, 4, 0) == -1 and lib.di_pair_config(0, 17, 0) == -1
-    assert lib.di_pair_config(0, 0, 3) == -1
+    assert lib.di_pair_config(0, 0, 4) == -1
     assert lib.di_pair_config(0, 0, 0) == 0  # keeps the current launch shape
     assert lib.di_head_prologue(0, None, 1, 8, 8, 128, 128, 1, None, None, None, None, None, 1e-6,
                                 None, None, None) == -1

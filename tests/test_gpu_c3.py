@@ -34,8 +34,8 @@ def _oracle_graph(gb, g):
             "edge_f": gb.edge_f[e0:e1].cpu()}
 
 
-@pytest.mark.parametrize("edge_kernel", [0, 1])
-def test_c3_bench_path_bf16_two_slots_two_streams(edge_kernel):
+@pytest.mark.parametrize("edge_kernel,pair_kernel", [(1, "rows_bounded"), (0, "vector")])
+def test_c3_bench_path_bf16_two_slots_two_streams(edge_kernel, pair_kernel):
     from deepinteract_amd import _lib, synth
     from deepinteract_amd.builder import build_graph_batch
     from deepinteract_amd.engine import GeoTEngine, PairTensorOp
@@ -53,7 +53,8 @@ def test_c3_bench_path_bf16_two_slots_two_streams(edge_kernel):
     h1r = [gb0.node_off[2 * j] for j in range(M)]
     h2r = [gb0.node_off[2 * j + 1] for j in range(M)]
     l1 = l2 = [N_RES] * M
-    pair = PairTensorOp(kernel="vector")
+    # bench.py's schedule beside GeoT: the bounded row-streaming kernel in one 2-wave block per CU
+    pair = PairTensorOp(kernel=pair_kernel, waves_per_block=2 if pair_kernel == "rows_bounded" else 0)
     prev = _lib.load().di_edge_config(edge_kernel)
     try:
         s_geot = torch.cuda.current_stream()
@@ -78,7 +79,7 @@ def test_c3_bench_path_bf16_two_slots_two_streams(edge_kernel):
             keep.append((hc, ec, views))
         torch.cuda.synchronize()
     finally:
-        PairTensorOp(kernel="rows")  # process-wide launch knobs back to their defaults
+        PairTensorOp(kernel="rows", waves_per_block=4)  # process-wide launch knobs back to their defaults
         _lib.load().di_edge_config(prev)
 
     errs = {}
@@ -106,5 +107,5 @@ def test_c3_bench_path_bf16_two_slots_two_streams(edge_kernel):
         pt = O.pair_tensor(ref[0], ref[1])[0].numpy()
         got = t[0][torch.as_tensor(idx[:, 0]), torch.as_tensor(idx[:, 1]), torch.as_tensor(idx[:, 2])]
         errs[f"mb{m}_c{j}_pair"] = rel_max(got.float().cpu().numpy(), pt[idx[:, 0], idx[:, 1], idx[:, 2]])
-    print(f"C3 bf16 errors, edge kernel {edge_kernel} (max-abs / max-abs ref):", {k: f"{v:.3e}" for k, v in errs.items()})
+    print(f"C3 bf16 errors, edge kernel {edge_kernel}, pair kernel {pair_kernel} (max-abs / max-abs ref):", {k: f"{v:.3e}" for k, v in errs.items()})
     assert max(errs.values()) < BF16_GEOT_TOL, errs

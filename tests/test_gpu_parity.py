@@ -104,14 +104,17 @@ def test_pair_tensor_batched_bf16_unaligned():
         assert torch.equal(v, ref)
 
 
+@pytest.mark.parametrize("kernel,waves", [("rows", 4), ("rows_bounded", 2), ("vector", 4), ("rows", 1)])
 @pytest.mark.parametrize("dtype,sizes", [
     (torch.bfloat16, [(16, 24), (264, 8), (520, 1000), (8, 4104)]),   # 4104: 5 row segments
     (torch.float32, [(12, 4), (300, 1000), (4, 2052)]),
 ])
-def test_pair_tensor_batched_aligned(dtype, sizes):
-    """Ragged aligned batch through the row-streaming kernel: planes spanning several row blocks,
-    rows spanning several 128-chunk segments, varying L1/L2 per complex."""
+def test_pair_tensor_batched_aligned(dtype, sizes, kernel, waves):
+    """Ragged aligned batch through each aligned kernel (row-streaming, row-streaming with bounded
+    in-flight stores, per-vector) and row-block shape: planes spanning several row blocks, rows
+    spanning several 128-chunk segments, varying L1/L2 per complex."""
     from deepinteract_amd.engine import PairTensorOp
+    PairTensorOp(kernel=kernel, waves_per_block=waves)
     torch.manual_seed(1)
     rows = sum(a + b for a, b in sizes)
     h = torch.randn(rows, 128, device="cuda").to(dtype)
@@ -120,8 +123,11 @@ def test_pair_tensor_batched_aligned(dtype, sizes):
         h1r.append(r)
         h2r.append(r + a)
         r += a + b
-    _, views = PairTensorOp()(h, h1r, h2r, [a for a, _ in sizes], [b for _, b in sizes], hT=h.t().contiguous())
-    torch.cuda.synchronize()
+    try:
+        _, views = PairTensorOp()(h, h1r, h2r, [a for a, _ in sizes], [b for _, b in sizes], hT=h.t().contiguous())
+        torch.cuda.synchronize()
+    finally:
+        PairTensorOp(kernel="rows", waves_per_block=4)  # process-wide knobs back to the defaults
     for (a, b), s1, s2, v in zip(sizes, h1r, h2r, views):
         ref = torch.cat((h[s1:s1 + a].t().unsqueeze(0).unsqueeze(3).expand(1, 128, a, b),
                          h[s2:s2 + b].t().unsqueeze(0).unsqueeze(2).expand(1, 128, a, b)), 1)

@@ -34,6 +34,13 @@ VARIANTS = {
     "lean4g2d6": ["DI_LEAN_NW=4", "DI_LEAN_WPE=2", "DI_LEAN_VGPR=120", "DI_LEAN_G=2", "DI_MMA_DEPTH=6"],
     "lean4g2ns": ["DI_LEAN_NW=4", "DI_LEAN_WPE=2", "DI_LEAN_VGPR=120", "DI_LEAN_G=2", "DI_LEAN_SHARE=0"],
     "lean4g2d4": ["DI_LEAN_NW=4", "DI_LEAN_WPE=2", "DI_LEAN_VGPR=120", "DI_LEAN_G=2", "DI_MMA_DEPTH=4"],
+    "inflight1": ["DI_PAIR_INFLIGHT=1"],
+    "inflight2": ["DI_PAIR_INFLIGHT=2"],
+    "inflight3": ["DI_PAIR_INFLIGHT=3"],
+    "inflight4": ["DI_PAIR_INFLIGHT=4"],
+    "inflight6": ["DI_PAIR_INFLIGHT=6"],
+    "inflight8": ["DI_PAIR_INFLIGHT=8"],
+    "inflight16": ["DI_PAIR_INFLIGHT=16"],
     "lean8g2": ["DI_LEAN_NW=8", "DI_LEAN_WPE=2", "DI_LEAN_VGPR=120", "DI_LEAN_G=2", "DI_MMA_DEPTH=6"],
 }
 
