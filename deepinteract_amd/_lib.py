@@ -15,7 +15,10 @@ DI_F32, DI_BF16 = 0, 1
 class DiGraph(ctypes.Structure):
     _fields_ = [("num_nodes", ctypes.c_int32), ("num_edges", ctypes.c_int32),
                 ("src", ctypes.c_void_p), ("dst", ctypes.c_void_p), ("nbr", ctypes.c_void_p),
-                ("node_pos", ctypes.c_void_p), ("in_ptr", ctypes.c_void_p)]
+                ("node_pos", ctypes.c_void_p), ("in_ptr", ctypes.c_void_p), ("flags", ctypes.c_int32)]
+
+
+DI_GRAPH_GEO_REF = 1
 
 
 class DiGeoArgs(ctypes.Structure):
@@ -76,7 +79,7 @@ def _bind(path: str):
         fn = getattr(lib, name)
         fn.argtypes = argtypes
         fn.restype = restype
-    if lib.di_abi_version() != 1:
+    if lib.di_abi_version() != 2:
         raise RuntimeError("deepinteract_amd ABI version mismatch")
     return lib
 

@@ -142,8 +142,10 @@ def build_graph_batch(chains, k=KNN, nb=GEO_NBRHD_SIZE, seed=0, device="cuda", r
     else:
         _lib.check(lib.di_build_nbr_ids(nt * k, _p(src), _p(dst), _p(in_ptr), ctypes.c_uint64(seed), _p(nbr),
                                         _stream()), "di_build_nbr_ids")
+    # k_geo_feats writes the featuriser's constant direction / orientation columns (0,0,0,0,0,0,1)
+    # for every edge, so the batch carries DI_GRAPH_GEO_REF by construction (no device check)
     gb = GraphBatch(src, dst, nbr, node_f, edge_f, sizes, [n * k for n in sizes], node_count_limit=node_count_limit,
-                    in_ptr=in_ptr, node_pos=node_pos)
+                    in_ptr=in_ptr, node_pos=node_pos, geo_ref=True)
     gb._keep = (d_all,)  # inputs referenced by in-flight launches
     if return_aux:
         return gb, {"knn_idx": idx, "knn_d2": d2}

@@ -186,7 +186,11 @@ __global__ __launch_bounds__(THREADS) void k_node_embed(EmbedArgs a) {
 }
 
 // ================================================================ InitEdgeModule (+ layer-0 nbr_linear)
-template <class DT>
+// GC (DI_GRAPH_GEO_REF batches): the direction terms silu(dir_linear_{0,1}(0)) = 0 are skipped and
+// the orientation terms are the packed constants IEV_ORC / IEV_OGATE; the layer-0
+// silu(nbr_linear(F)) rows are only computed when fn_out is given (the grouped edge kernel does
+// not gather them for such batches).
+template <class DT, bool GC>
 __global__ __attribute__((amdgpu_flat_work_group_size(1, 64 * DI_GEO_NW), amdgpu_waves_per_eu(2, 2)))
 void k_init_edge(InitArgs a) {
   using T = typename DT::T;
@@ -213,17 +217,21 @@ void k_init_edge(InitArgs a) {
   Act<8> acc;
   load_row(acc, a.pos_src + (int64_t)a.node_pos[a.src[e]] * HID, g);
   add_row(acc, a.pos_dst + (int64_t)a.node_pos[a.dst[e]] * HID, g);
+  if constexpr (GC) add_vec(acc, a.wvec + IEV_ORC, g);  // orientation term (constant)
+  // geometric terms t = 1..4 (dist, dir, orient, amide); GC: dist and amide only
+  constexpr int NT = GC ? 2 : 4;
+  auto geo_t = [](int i) { return GC ? (i == 0 ? 1 : 4) : i + 1; };
   {
     // t = 0: edge_messages_linear_0 and its combined_linear_0 slice, collapsed on the host into one
     // [128, 2] map of the message columns (no activation between them, :237-241)
     const T* w = pipe.next();
-    pipe.issue(W + (IE_T0 + 40) * BLK, 40);
+    pipe.issue(W + (IE_T0 + 40 * geo_t(0)) * BLK, 40);
     mma<8, 1>(acc, gop, w, lane, PP);
   }
 #pragma unroll 1
-  for (int t = 1; t < 5; ++t) {
+  for (int i = 0; i < NT; ++i) {
     const T* w = pipe.next();
-    if (t < 4) pipe.issue(W + (IE_T0 + 40 * (t + 1)) * BLK, 40);
+    if (i + 1 < NT) pipe.issue(W + (IE_T0 + 40 * geo_t(i + 1)) * BLK, 40);
     else pipe.issue(W + IE_GEO1 * BLK, 40);
     Act<8> y;
     zero(y);
@@ -237,9 +245,11 @@ void k_init_edge(InitArgs a) {
     const T* w = pipe.next();
     pipe.issue(W + IE_C1 * BLK, 16);
     Act<8> gs;
-    zero(gs);
+    if constexpr (GC) init_vec(gs, a.wvec + IEV_OGATE, g);  // silu(o1): constant; silu(r1) = 0
+    else zero(gs);
 #pragma unroll 1
     for (int t = 0; t < 5; ++t) {
+      if (GC && (t == 2 || t == 3)) continue;
       Act<8> y;
       zero(y);
       mma<8, 1>(y, gop, w + 8 * t * BLK, lane, PP);
@@ -248,11 +258,12 @@ void k_init_edge(InitArgs a) {
     }
     mul_(acc, gs);
   }
+  const bool with_fn = a.fn_out != nullptr;  // uniform
   // combined_linear_2(combined_linear_1(.)) : 128 -> 28 (padded 32) -> 128
   Act<8> f;
   {
     const T* w = pipe.next();
-    pipe.issue(W + IE_NBR * BLK, MAT128);
+    if (with_fn) pipe.issue(W + IE_NBR * BLK, MAT128);
     Act<2> z;
     zero(z);
     linear<DT, 2, 4>(z, acc, w, lane, PP);
@@ -260,6 +271,7 @@ void k_init_edge(InitArgs a) {
     linear<DT, 8, 1>(f, z, w + 8 * BLK, lane, PP);
   }
   if (valid) store_row(f, reinterpret_cast<T*>(a.f_out) + (int64_t)e * HID, g);
+  if (!with_fn) return;
   // layer-0 silu(nbr_linear(F)), applied once per edge and gathered by the conformation module
   // (silu(nbr_linear(F[ids])) == silu(nbr_linear(F))[ids], deepinteract_modules.py:386-390)
   {
@@ -786,16 +798,20 @@ struct Lean {
 #endif
 using LeanPipe = WPipe<u16, Lean::NW, DI_LEAN_DBUF != 0, EL_CAP, 128>;
 
-// stage sequencer of one tile: next() publishes stage i and issues the DMA of stage i + 1
-template <int NS>
+// stage sequencer of one tile: next() publishes stage i and issues the DMA of stage i + 1.
+// GC (DI_GRAPH_GEO_REF batches): the sequence starts at orig_msg_linear (stages 0-1, the neighbour
+// messages, are exactly zero), which then carries the orig_msg_linear bias, and (intermediate
+// layers) ends before the next layer's nbr_linear (its gathered rows are never needed).
+template <int NS, bool GC = false>
 struct LeanStages {
   LeanPipe& pipe;
   const u16* W;
   const float* V;
   int i;
   __device__ void issue(int s) {
-    const int vo = EL_VEC[s];
-    pipe.issue(W + EL_ORDER[s] * BLK, EL_SIZE[s], vo >= 0 ? V + vo : nullptr, 128);
+    const int si = GC ? s + 2 : s;
+    const int vo = (GC && s == 0) ? ELV_OM : EL_VEC[si];
+    pipe.issue(W + EL_ORDER[si] * BLK, EL_SIZE[si], vo >= 0 ? V + vo : nullptr, 128);
   }
   __device__ const u16* next() {
     const u16* w = pipe.next();
@@ -827,8 +843,8 @@ struct LeanRow {
   bool valid;
 };
 
-template <int NS>
-__device__ __forceinline__ void lean_res_block(Act<8> (&x)[Lean::LG], LeanStages<NS>& st, int lane, int g) {
+template <int NS, bool GC>
+__device__ __forceinline__ void lean_res_block(Act<8> (&x)[Lean::LG], LeanStages<NS, GC>& st, int lane, int g) {
   Op<BF16T, 4> op[Lean::LG];
 #pragma unroll
   for (int q = 0; q < Lean::LG; ++q) make_op(op[q], x[q]);
@@ -909,12 +925,12 @@ __device__ __forceinline__ void lean_f_residual(Act<8> (&x)[Lean::LG], const u16
   }
 }
 
-template <int MODE>
+template <int MODE, bool GC>
 __global__ __attribute__((amdgpu_flat_work_group_size(1, 64 * DI_LEAN_NW), amdgpu_waves_per_eu(DI_LEAN_WPE, DI_LEAN_WPE),
                           amdgpu_num_vgpr(DI_LEAN_VGPR)))
 void k_edge_lean(EdgeArgs a) {
   constexpr bool FINAL = MODE == 1;
-  constexpr int NS = FINAL ? EL_NSTAGE_FINAL : EL_NSTAGE;
+  constexpr int NS = (FINAL ? EL_NSTAGE_FINAL : EL_NSTAGE) - (GC ? (FINAL ? 2 : 3) : 0);
   constexpr int LG = Lean::LG;
   DI_GEOT_ENTRY();
   __shared__ __attribute__((aligned(16))) char lds[(DI_LEAN_DBUF ? 2 : 1) * LeanPipe::SLOT_BYTES];
@@ -933,7 +949,7 @@ void k_edge_lean(EdgeArgs a) {
   }
 
   LeanPipe pipe(lds);
-  LeanStages<NS> st{pipe, reinterpret_cast<const u16*>(a.wmat), a.wvec, 0};
+  LeanStages<NS, GC> st{pipe, reinterpret_cast<const u16*>(a.wmat), a.wvec, 0};
   st.issue(0);
 
   Op<BF16T, 1> gop[LG];
@@ -944,100 +960,110 @@ void k_edge_lean(EdgeArgs a) {
     load_edge_geo(geo, a.edge_f + (int64_t)rw[q].e * NFEAT_E, g);
     make_op(gop[q], geo);
   }
-  RawRow<u16> xn;  // the gathered neighbour row in flight (group-major order: q, then j)
-  int4 nb = *reinterpret_cast<const int4*>(a.nbr + (int64_t)rw[0].e * 4);
-  xn.load(fn_in + (int64_t)nb.x * HID, g);
-
-  // ---- neighbour-edge messages (conformation_module_message_func :384-418)
-  const u16* w = st.next();  // stage 0: geometric gates + downward_proj
-  Act<4> s[LG];
-#pragma unroll
-  for (int q = 0; q < LG; ++q) {
-    DI_FENCE();
-    Act<4> gate;
-    {
-      Act<4> t1;
-      zero(gate);
-      lmma<4, 1>(gate, gop[q], w + 8 * BLK, lane);
-      zero(t1);
-      lmma<4, 1>(t1, gop[q], w + 12 * BLK, lane);
-      mul_(gate, t1);
-      zero(t1);
-      lmma<4, 1>(t1, gop[q], w + 16 * BLK, lane);
-      mul_(gate, t1);
-      pin(gate);
-    }
-    zero(s[q]);
-    const int4 nbq = nb;
-    if (q + 1 < LG) nb = *reinterpret_cast<const int4*>(a.nbr + (int64_t)rw[q + 1].e * 4);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      DI_FENCE();
-      // x = silu(nbr_linear(F))[nbr_j] * dist gate, packed k-step by k-step
-      Op<BF16T, 4> xop;
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        // recomputed per neighbour (2 MFMAs per k-step) rather than held live across the loop:
-        // the memory clobber stops the compiler from merging the neighbours' copies (32 VGPRs)
-        asm volatile("" ::: "memory");
-        DI_FENCE();
-        Act<2> dg;
-        zero(dg);
-        lmma<2, 1>(dg, gop[q], w + 2 * ks * BLK, lane);
-        // opaque until here: keeps the compiler from unpacking the whole gathered row to fp32 as
-        // soon as it lands (32 registers instead of 16)
-        asm volatile("" : "+v"(xn.u[2 * ks]), "+v"(xn.u[2 * ks + 1]));
-        const uint2 lo = xn.u[2 * ks], hi = xn.u[2 * ks + 1];
-        uint4 u;
-        u.x = pack_bf16x2(__builtin_bit_cast(float, lo.x << 16) * dg.v[0][0],
-                          __builtin_bit_cast(float, lo.x & 0xffff0000u) * dg.v[0][1]);
-        u.y = pack_bf16x2(__builtin_bit_cast(float, lo.y << 16) * dg.v[0][2],
-                          __builtin_bit_cast(float, lo.y & 0xffff0000u) * dg.v[0][3]);
-        u.z = pack_bf16x2(__builtin_bit_cast(float, hi.x << 16) * dg.v[1][0],
-                          __builtin_bit_cast(float, hi.x & 0xffff0000u) * dg.v[1][1]);
-        u.w = pack_bf16x2(__builtin_bit_cast(float, hi.y << 16) * dg.v[1][2],
-                          __builtin_bit_cast(float, hi.y & 0xffff0000u) * dg.v[1][3]);
-        xop.f[ks] = __builtin_bit_cast(bf16x8, u);
-      }
-      // the next gathered row, in flight under this one's downward_proj
-      if (j < 3) {
-        const int nx = j == 0 ? nbq.y : (j == 1 ? nbq.z : nbq.w);
-        xn.load(fn_in + (int64_t)nx * HID, g);
-      } else if (q + 1 < LG) {
-        xn.load(fn_in + (int64_t)nb.x * HID, g);
-      }
-      DI_FENCE();
-      Act<4> y;
-      zero(y);
-      lmma<4, 4>(y, xop, w + 20 * BLK, lane);  // downward_proj
-#pragma unroll
-      for (int b = 0; b < 4; ++b)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) s[q].v[b][r] += silu2<true>(y.v[b][r]) * gate.v[b][r];
-      pin(s[q]);
-    }
-  }
+  const u16* w;
   Act<8> x[LG];
   RawRow<u16> fr[LG];
-  {
-    w = st.next();  // stage 1: upward_proj (+ orig_msg_linear bias)
+  if constexpr (GC) {
+    // DI_GRAPH_GEO_REF: the neighbour messages are multiplied by dir_linear_1(dir_linear_0(0)) = 0
+    // (:408), so x = orig_msg_linear(F) + b exactly; no gathered rows, no stages 0-1
+    load_f(fr, f_row, g);
+    w = st.next();  // orig_msg_linear (+ its bias)
 #pragma unroll
+    for (int q = 0; q < LG; ++q) init_vec_lds(x[q], st.v(), g);
+  } else {
+    RawRow<u16> xn;  // the gathered neighbour row in flight (group-major order: q, then j)
+    int4 nb = *reinterpret_cast<const int4*>(a.nbr + (int64_t)rw[0].e * 4);
+    xn.load(fn_in + (int64_t)nb.x * HID, g);
+
+    // ---- neighbour-edge messages (conformation_module_message_func :384-418)
+    w = st.next();  // stage 0: geometric gates + downward_proj
+    Act<4> s[LG];
+  #pragma unroll
     for (int q = 0; q < LG; ++q) {
-    DI_FENCE();
-      Op<BF16T, 2> sop;
-      make_op(sop, s[q]);
-      lin_op<8, 2>(x[q], sop, w, nullptr, lane, g);
-      silu2_<8, true>(x[q]);
-      Act<8> bo;
-      init_vec_lds(bo, st.v(), g);
-#pragma unroll
-      for (int b = 0; b < 8; ++b) x[q].v[b] = silu2_unit<true>() * x[q].v[b] + bo.v[b];
-      pin(x[q]);
+      DI_FENCE();
+      Act<4> gate;
+      {
+        Act<4> t1;
+        zero(gate);
+        lmma<4, 1>(gate, gop[q], w + 8 * BLK, lane);
+        zero(t1);
+        lmma<4, 1>(t1, gop[q], w + 12 * BLK, lane);
+        mul_(gate, t1);
+        zero(t1);
+        lmma<4, 1>(t1, gop[q], w + 16 * BLK, lane);
+        mul_(gate, t1);
+        pin(gate);
+      }
+      zero(s[q]);
+      const int4 nbq = nb;
+      if (q + 1 < LG) nb = *reinterpret_cast<const int4*>(a.nbr + (int64_t)rw[q + 1].e * 4);
+  #pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        DI_FENCE();
+        // x = silu(nbr_linear(F))[nbr_j] * dist gate, packed k-step by k-step
+        Op<BF16T, 4> xop;
+  #pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+          // recomputed per neighbour (2 MFMAs per k-step) rather than held live across the loop:
+          // the memory clobber stops the compiler from merging the neighbours' copies (32 VGPRs)
+          asm volatile("" ::: "memory");
+          DI_FENCE();
+          Act<2> dg;
+          zero(dg);
+          lmma<2, 1>(dg, gop[q], w + 2 * ks * BLK, lane);
+          // opaque until here: keeps the compiler from unpacking the whole gathered row to fp32 as
+          // soon as it lands (32 registers instead of 16)
+          asm volatile("" : "+v"(xn.u[2 * ks]), "+v"(xn.u[2 * ks + 1]));
+          const uint2 lo = xn.u[2 * ks], hi = xn.u[2 * ks + 1];
+          uint4 u;
+          u.x = pack_bf16x2(__builtin_bit_cast(float, lo.x << 16) * dg.v[0][0],
+                            __builtin_bit_cast(float, lo.x & 0xffff0000u) * dg.v[0][1]);
+          u.y = pack_bf16x2(__builtin_bit_cast(float, lo.y << 16) * dg.v[0][2],
+                            __builtin_bit_cast(float, lo.y & 0xffff0000u) * dg.v[0][3]);
+          u.z = pack_bf16x2(__builtin_bit_cast(float, hi.x << 16) * dg.v[1][0],
+                            __builtin_bit_cast(float, hi.x & 0xffff0000u) * dg.v[1][1]);
+          u.w = pack_bf16x2(__builtin_bit_cast(float, hi.y << 16) * dg.v[1][2],
+                            __builtin_bit_cast(float, hi.y & 0xffff0000u) * dg.v[1][3]);
+          xop.f[ks] = __builtin_bit_cast(bf16x8, u);
+        }
+        // the next gathered row, in flight under this one's downward_proj
+        if (j < 3) {
+          const int nx = j == 0 ? nbq.y : (j == 1 ? nbq.z : nbq.w);
+          xn.load(fn_in + (int64_t)nx * HID, g);
+        } else if (q + 1 < LG) {
+          xn.load(fn_in + (int64_t)nb.x * HID, g);
+        }
+        DI_FENCE();
+        Act<4> y;
+        zero(y);
+        lmma<4, 4>(y, xop, w + 20 * BLK, lane);  // downward_proj
+  #pragma unroll
+        for (int b = 0; b < 4; ++b)
+  #pragma unroll
+          for (int r = 0; r < 4; ++r) s[q].v[b][r] += silu2<true>(y.v[b][r]) * gate.v[b][r];
+        pin(s[q]);
+      }
     }
-  }
-  load_f(fr, f_row, g);
-  {
+    {
+      w = st.next();  // stage 1: upward_proj (+ orig_msg_linear bias)
+  #pragma unroll
+      for (int q = 0; q < LG; ++q) {
+      DI_FENCE();
+        Op<BF16T, 2> sop;
+        make_op(sop, s[q]);
+        lin_op<8, 2>(x[q], sop, w, nullptr, lane, g);
+        silu2_<8, true>(x[q]);
+        Act<8> bo;
+        init_vec_lds(bo, st.v(), g);
+  #pragma unroll
+        for (int b = 0; b < 8; ++b) x[q].v[b] = silu2_unit<true>() * x[q].v[b] + bo.v[b];
+        pin(x[q]);
+      }
+    }
+    load_f(fr, f_row, g);
     w = st.next();  // stage 2: orig_msg_linear(res) + nbr
+  }
+  {
     if constexpr (Lean::SHARED) {
       Op<BF16T, 4> fop[LG];
 #pragma unroll
@@ -1196,6 +1222,7 @@ void k_edge_lean(EdgeArgs a) {
       if (rw[q].valid) store_row(e1[q], reinterpret_cast<u16*>(a.f_out) + (int64_t)rw[q].e * HID, g);
       make_op(eop[q], e1[q]);
     }
+    if constexpr (GC) return;  // the next layer gathers no silu(nbr_linear(F)) rows
     w = st.next();  // next layer's silu(nbr_linear(.))
     Act<8> fng[Lean::SHARED ? LG : 1];
     if constexpr (Lean::SHARED) lin_groups<LG, 8, 4>(fng, eop, w, st.v(), lane, g);
@@ -1617,16 +1644,19 @@ extern "C" int di_node_embed(const di_graph* g, di_dtype dt, int32_t in_dim, con
 extern "C" int di_init_edge(const di_graph* g, di_dtype dt, const float* edge_f, const void* wmat,
                             const float* wvec, const float* pos_src_tab, const float* pos_dst_tab,
                             void* f_out, void* fn_out, void* stream) {
-  if (!g || !edge_f || !wmat || !wvec || !pos_src_tab || !pos_dst_tab || !f_out || !fn_out ||
+  const bool gc = (g ? g->flags : 0) & DI_GRAPH_GEO_REF;
+  if (!g || !edge_f || !wmat || !wvec || !pos_src_tab || !pos_dst_tab || !f_out || (!fn_out && !gc) ||
       g->num_edges <= 0)
     return DI_EINVAL;
   InitArgs a{g->num_edges, edge_f, g->src, g->dst, g->node_pos, wmat, wvec, pos_src_tab, pos_dst_tab,
              f_out, fn_out};
   hipStream_t s = (hipStream_t)stream;
-  if (dt == DI_BF16)
-    hipLaunchKernelGGL(k_init_edge<BF16T>, dim3(grid_rows(a.Et, Geo<BF16T>::ROWS)), dim3(Geo<BF16T>::THREADS), 0, s, a);
-  else
-    hipLaunchKernelGGL(k_init_edge<F32T>, dim3(grid_rows(a.Et, Geo<F32T>::ROWS)), dim3(Geo<F32T>::THREADS), 0, s, a);
+  const dim3 gb(grid_rows(a.Et, Geo<BF16T>::ROWS)), bb(Geo<BF16T>::THREADS);
+  const dim3 gf(grid_rows(a.Et, Geo<F32T>::ROWS)), bf(Geo<F32T>::THREADS);
+  if (dt == DI_BF16 && gc) hipLaunchKernelGGL((k_init_edge<BF16T, true>), gb, bb, 0, s, a);
+  else if (dt == DI_BF16) hipLaunchKernelGGL((k_init_edge<BF16T, false>), gb, bb, 0, s, a);
+  else if (gc) hipLaunchKernelGGL((k_init_edge<F32T, true>), gf, bf, 0, s, a);
+  else hipLaunchKernelGGL((k_init_edge<F32T, false>), gf, bf, 0, s, a);
   return launch_status();
 }
 
@@ -1634,16 +1664,21 @@ extern "C" int di_edge_layer(const di_graph* g, di_dtype dt, int final_layer, co
                              const void* f_in, const void* fn_in, const void* qkv, const void* wmat,
                              const float* wvec, float* alpha_out, void* f_out, void* fn_out,
                              void* stream) {
-  if (!g || !edge_f || !f_in || !fn_in || !qkv || !wmat || !wvec || !alpha_out || g->num_edges <= 0)
+  // DI_GRAPH_GEO_REF on the grouped bf16 kernel: the neighbour-message branch is skipped, fn_in is
+  // not read and fn_out not written; every other kernel computes the (exactly zero) branch
+  const bool gc = g && (g->flags & DI_GRAPH_GEO_REF) && dt == DI_BF16 && g_edge_kernel == 1;
+  if (!g || !edge_f || !f_in || (!fn_in && !gc) || !qkv || !wmat || !wvec || !alpha_out || g->num_edges <= 0)
     return DI_EINVAL;
-  if (!final_layer && (!f_out || !fn_out)) return DI_EINVAL;
+  if (!final_layer && (!f_out || (!fn_out && !gc))) return DI_EINVAL;
   EdgeArgs a{g->num_edges, edge_f, g->src, g->dst, g->nbr, f_in, fn_in, qkv, wmat, wvec, alpha_out,
              f_out, fn_out};
   hipStream_t s = (hipStream_t)stream;
   if (dt == DI_BF16 && g_edge_kernel == 1) {
     dim3 grid(grid_rows(a.Et, Lean::ROWS)), block(Lean::THREADS);
-    if (final_layer) hipLaunchKernelGGL((k_edge_lean<1>), grid, block, 0, s, a);
-    else hipLaunchKernelGGL((k_edge_lean<0>), grid, block, 0, s, a);
+    if (final_layer && gc) hipLaunchKernelGGL((k_edge_lean<1, true>), grid, block, 0, s, a);
+    else if (final_layer) hipLaunchKernelGGL((k_edge_lean<1, false>), grid, block, 0, s, a);
+    else if (gc) hipLaunchKernelGGL((k_edge_lean<0, true>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((k_edge_lean<0, false>), grid, block, 0, s, a);
   } else if (dt == DI_BF16) {
     // persistent: two resident blocks per CU
 #ifndef DI_EDGE_PERSIST

@@ -21,7 +21,10 @@ constexpr int IE_C1 = 240;    // combined_linear_1 (28 -> 32 rows) [2 x 4]
 constexpr int IE_C2 = 248;    // combined_linear_2 (K 28 -> 32)    [8 x 1]
 constexpr int IE_NBR = 256;   // layer-0 nbr_linear [8 x 4]
 constexpr int IE_NBLK = 288;
-constexpr int IEV_NBR = 0, IEV_N = 128;
+// vectors: nbr_linear bias; with DI_GRAPH_GEO_REF the orientation terms as constants (kernel units):
+// IEV_ORC = combined_linear_0's orientation slice . silu(orient_linear_0 (0,0,0,1)),
+// IEV_OGATE = silu(orient_linear_1 (0,0,0,1))
+constexpr int IEV_NBR = 0, IEV_ORC = 128, IEV_OGATE = 256, IEV_N = 384;
 
 // ---- kind 2/3: edge layer (conformation + attention scores [+ edge output]) --------------
 // stage 0 = geometric gates + downward_proj (one 36-block stage), final gate rides with final_linear

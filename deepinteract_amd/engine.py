@@ -151,6 +151,11 @@ class GeoTEngine:
         g = ctypes.byref(gb.c_graph)
         st = _stream()
         h, qkv, f, fn, alpha = ws["h"], ws["qkv"], ws["f"], ws["fn"], ws["alpha"]
+        # DI_GRAPH_GEO_REF batches on the grouped bf16 edge kernel: the conformation module's
+        # neighbour messages are exactly zero (include/deepinteract_amd.h), so the gathered
+        # silu(nbr_linear(F)) rows are neither written nor read
+        if gb.geo_ref and self.dtype == "bf16" and lib.di_edge_config(-1) == 1:
+            fn = [None, None]
         tick = _Ticker(events)
         tick("node_embed")
         _lib.check(lib.di_node_embed(g, dt, gb.node_f.shape[1], _ptr(gb.node_f), _ptr(p.embed[0]), _ptr(p.embed[1]),

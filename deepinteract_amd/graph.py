@@ -16,7 +16,21 @@ from typing import Sequence
 import torch
 
 from .config import NODE_COUNT_LIMIT
-from ._lib import DiGraph
+from ._lib import DI_GRAPH_GEO_REF, DiGraph
+
+# edge_f[:, 20:27] of every edge as the reference featuriser produces them: direction (0, 0, 0),
+# orientation quaternion (0, 0, 0, 1) (csrc di_graph.flags, DI_GRAPH_GEO_REF)
+GEO_REF_COLS = (20, 27)
+GEO_REF_VALUES = (0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 1.0)
+
+
+def edge_feats_geo_ref(edge_f: torch.Tensor) -> bool:
+    """True when every edge's direction / orientation columns are the reference featuriser's
+    constants (one device reduction and a host sync; the device builder knows it by construction)."""
+    if edge_f is None or edge_f.dim() != 2 or edge_f.shape[0] == 0 or edge_f.shape[1] < GEO_REF_COLS[1]:
+        return False
+    ref = torch.tensor(GEO_REF_VALUES, dtype=edge_f.dtype, device=edge_f.device)
+    return bool((edge_f[:, GEO_REF_COLS[0]:GEO_REF_COLS[1]] == ref).all())
 
 
 class ResidueGraph:
@@ -122,9 +136,11 @@ class GraphBatch:
     """
 
     def __init__(self, src, dst, nbr, node_f, edge_f, nodes_per_graph, edges_per_graph,
-                 node_count_limit=NODE_COUNT_LIMIT, in_ptr=None, node_pos=None):
+                 node_count_limit=NODE_COUNT_LIMIT, in_ptr=None, node_pos=None, geo_ref=None):
         """in_ptr / node_pos: precomputed by the device builder (di_knn_graph); when given, the
-        destination-major order is guaranteed by construction and not re-checked on the host."""
+        destination-major order is guaranteed by construction and not re-checked on the host.
+        geo_ref: whether every edge carries the reference featuriser's constant direction /
+        orientation columns (di_graph.flags DI_GRAPH_GEO_REF); None = check edge_f."""
         self.src, self.dst, self.nbr = src, dst, nbr
         self.node_f, self.edge_f = node_f, edge_f
         self.nodes_per_graph = [int(x) for x in nodes_per_graph]
@@ -156,8 +172,23 @@ class GraphBatch:
         for n, e in zip(self.nodes_per_graph, self.edges_per_graph):
             self.node_off.append(self.node_off[-1] + n)
             self.edge_off.append(self.edge_off[-1] + e)
+        self.geo_ref = edge_feats_geo_ref(edge_f) if geo_ref is None else bool(geo_ref) and self.num_edges > 0
         self._c = DiGraph(self.num_nodes, self.num_edges, self.src.data_ptr(), self.dst.data_ptr(),
-                          self.nbr.data_ptr(), self.node_pos.data_ptr(), self.in_ptr.data_ptr())
+                          self.nbr.data_ptr(), self.node_pos.data_ptr(), self.in_ptr.data_ptr(),
+                          DI_GRAPH_GEO_REF if self.geo_ref else 0)
+
+    def with_geo_ref(self, on: bool) -> "GraphBatch":
+        """The same batch with the DI_GRAPH_GEO_REF property set or cleared (clearing always keeps
+        results exact; setting it is only valid when edge_feats_geo_ref(edge_f) holds)."""
+        if on and not edge_feats_geo_ref(self.edge_f):
+            raise ValueError("edge features do not carry the reference featuriser's constant direction / orientation")
+        gb = GraphBatch.__new__(GraphBatch)
+        gb.__dict__.update(self.__dict__)
+        gb.geo_ref = bool(on)
+        gb._c = DiGraph(self.num_nodes, self.num_edges, self.src.data_ptr(), self.dst.data_ptr(),
+                        self.nbr.data_ptr(), self.node_pos.data_ptr(), self.in_ptr.data_ptr(),
+                        DI_GRAPH_GEO_REF if on else 0)
+        return gb
 
     @property
     def c_graph(self) -> DiGraph:
@@ -227,7 +258,8 @@ def concat_batches(batches: Sequence[GraphBatch]) -> GraphBatch:
     return GraphBatch(torch.cat(srcs).contiguous(), torch.cat(dsts).contiguous(), torch.cat(nbrs).contiguous(),
                       torch.cat(nfs).contiguous(), torch.cat(efs).contiguous(), nn, ne,
                       node_count_limit=max(b.node_count_limit for b in batches),
-                      in_ptr=torch.cat(ptrs).contiguous(), node_pos=torch.cat(poss).contiguous())
+                      in_ptr=torch.cat(ptrs).contiguous(), node_pos=torch.cat(poss).contiguous(),
+                      geo_ref=all(b.geo_ref for b in batches))
 
 
 def select_graphs(gb: GraphBatch, indices: Sequence[int]) -> GraphBatch:
@@ -238,5 +270,5 @@ def select_graphs(gb: GraphBatch, indices: Sequence[int]) -> GraphBatch:
         e0, e1 = gb.edge_off[g], gb.edge_off[g + 1]
         parts.append(GraphBatch(gb.src[e0:e1] - n0, gb.dst[e0:e1] - n0, gb.nbr[e0:e1] - e0, gb.node_f[n0:n1],
                                 gb.edge_f[e0:e1], [n1 - n0], [e1 - e0], node_count_limit=gb.node_count_limit,
-                                in_ptr=gb.in_ptr[n0:n1 + 1] - e0, node_pos=gb.node_pos[n0:n1]))
+                                in_ptr=gb.in_ptr[n0:n1 + 1] - e0, node_pos=gb.node_pos[n0:n1], geo_ref=gb.geo_ref))
     return concat_batches(parts)

@@ -27,7 +27,7 @@ def _l2e(dtype: str) -> float:
 
 # ---- csrc/layout.h mirror -------------------------------------------------------------------
 EM_NBLK, EMV_N = 128, 384
-IE_NBLK, IEV_N = 288, 128
+IE_NBLK, IEV_N = 288, 384
 EL_NBLK, ELV_N = 764, 2560
 EL_NBLK_FINAL, ELV_N_FINAL = 572, 2048
 NL_NBLK, NLV_N = 256, 768
@@ -217,6 +217,14 @@ def init_blob(sd, dtype, p="gnn_module.0.init_edge_module",
     w, b = lin(sd, nbr) if nbr else (np.zeros((128, 128)), np.zeros(128))
     bb.put(256, w)
     bb.putv(0, b)
+    # DI_GRAPH_GEO_REF batches (orientation columns = (0, 0, 0, 1) on every edge): the orientation
+    # terms are per-model constants (deepinteract_modules.py:226, :243), in the kernel's units (x sc)
+    silu = lambda x: x / (1.0 + np.exp(-x))  # noqa: E731
+    t_or = GEO_ORDER.index("orient")
+    o0 = _np(sd[f"{p}.orient_linear_0.weight"])[:, 3]
+    o1 = _np(sd[f"{p}.orient_linear_1.weight"])[:, 3]
+    bb.putv(128, (wc0[:, 256 + 128 * t_or: 384 + 128 * t_or] @ silu(o0)) * sc)
+    bb.putv(256, silu(o1) * sc)
     mat, vec = bb.finish()
     emb = _np(sd[f"{p}.node_embedding.weight"])
     pos_src = torch.from_numpy(emb @ wc0[:, 0:128].T * sc).to(torch.float32)

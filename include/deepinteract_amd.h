@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define DI_ABI_VERSION 1
+#define DI_ABI_VERSION 2
 
 /* activation / weight storage type of the GeoT kernels (accumulation is always fp32) */
 typedef enum { DI_F32 = 0, DI_BF16 = 1 } di_dtype;
@@ -66,7 +66,24 @@ typedef struct {
   const int32_t* nbr;       /* [Et,4] src_nbr_e_ids[0:2], dst_nbr_e_ids[0:2] */
   const int32_t* node_pos;  /* [Nt] node index inside its chain (positional-embedding row) */
   const int32_t* in_ptr;    /* [Nt+1] CSR row pointer of in-edges by destination */
+  int32_t flags;            /* DI_GRAPH_* properties of the batch's edge features (0: none known) */
 } di_graph;
+
+/* di_graph.flags bit: every edge's direction columns edge_f[:, 20:23] are 0 and its orientation
+ * columns edge_f[:, 23:27] are (0, 0, 0, 1) -- what the reference featuriser produces for every
+ * kNN graph (GeometricProteinFeatures is called with E_idx = the destination node itself,
+ * deepinteract_utils.py:474-477, so dU = normalize(0) = 0 and the relative rotation is the
+ * identity quaternion). With all direction features zero, the conformation module's neighbour
+ * messages are multiplied by dir_linear_1(dir_linear_0(0)) = 0 (both bias-free,
+ * deepinteract_modules.py:301-302, :408), so that branch is exactly zero and the gathered
+ * silu(nbr_linear(F)) rows are never needed; InitEdge's direction terms are silu(0) = 0 and its
+ * orientation terms are per-model constants. With this flag:
+ *   di_init_edge  skips the direction terms, adds the orientation terms as packed constants, and
+ *                 writes fn_out only when fn_out != NULL;
+ *   di_edge_layer (bf16, kernel 1) skips the neighbour-message branch: fn_in is not read and
+ *                 fn_out is not written (both may be NULL).
+ * The other kernels ignore the flag (they compute the branch, which is exactly zero). */
+#define DI_GRAPH_GEO_REF 1
 
 /* one complex of a pair-tensor launch (host-built array copied to the device) */
 typedef struct {

@@ -25,7 +25,7 @@ def test_library_builds_and_exports_all_declared_symbols():
 
 def test_abi_version_and_blob_sizes():
     lib = _lib.load()
-    assert lib.di_abi_version() == 1
+    assert lib.di_abi_version() == 2
     for kind, (nblk, nvec) in packing.BLOB_SIZES.items():
         assert lib.di_blob_bytes(kind, _lib.DI_F32, 0) == nblk * 512 * 4
         assert lib.di_blob_bytes(kind, _lib.DI_BF16, 0) == nblk * 512 * 2
@@ -53,9 +53,29 @@ def test_head_prologue_work_bytes():
 
 
 def test_ctypes_struct_layouts():
-    assert ctypes.sizeof(_lib.DiGraph) == 8 + 5 * 8
+    assert ctypes.sizeof(_lib.DiGraph) == 8 + 5 * 8 + 8  # + int32 flags, padded to 8
     assert ctypes.sizeof(_lib.DiPairDesc) == 32
     assert ctypes.sizeof(_lib.DiGeoArgs) == 16 + 8 * 9
+
+
+def _declared_struct_fields(name):
+    src = open(os.path.join(ROOT, "include", "deepinteract_amd.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    for m in re.finditer(r"typedef struct \{(.*?)\}\s*(\w+);", src, flags=re.S):
+        if m.group(2) == name:
+            fields = []
+            for decl in m.group(1).split(";"):
+                decl = decl.strip()
+                if decl:
+                    fields += [f.strip().lstrip("*") for f in decl.split(None, 1)[1].split(",")] \
+                        if "," in decl else [decl.split()[-1].lstrip("*")]
+            return fields
+    raise KeyError(name)
+
+
+def test_ctypes_struct_fields_match_header():
+    for cls, name in ((_lib.DiGraph, "di_graph"), (_lib.DiPairDesc, "di_pair_desc"), (_lib.DiGeoArgs, "di_geo_args")):
+        assert [f for f, _ in cls._fields_] == _declared_struct_fields(name), name
 
 
 def _declared_arg_counts():
