@@ -38,6 +38,14 @@ EDGE_MAC = {"init_edge": 129_024, "edge_layer": 456_656, "edge_layer_final": 374
 H = 128
 
 
+# MACs the bf16 grouped kernels actually issue on MFMA per edge (16x16x32 MFMAs per 16-edge tile x
+# 8192 / 16), by DI_GRAPH_GEO_REF: the reference-equivalent rates above count the reference's work
+# (incl. the neighbour-message branch that is exactly zero for reference-featurised batches and the
+# nbr_linear the reference applies to 4 gathered rows per edge); these count what runs
+EXEC_EDGE_MAC = {True: {"init_edge": 65_536, "edge_layer": 348_160, "edge_layer_final": 266_240},
+                 False: {"init_edge": 131_072, "edge_layer": 428_032, "edge_layer_final": 329_728}}
+
+
 def node_mac(kind):
     q = 3 * H * H
     if kind == "node_embed":
@@ -446,7 +454,9 @@ def main():
         flops, byts = kernel_units(name, nodes, edges, l1l2, esz)
         rec = {"launches": len(ms), "avg_us": avg_s * 1e6, "total_ms": float(np.sum(ms))}
         if flops is not None:
-            rec["tflops"] = flops / avg_s / 1e12
+            rec["tflops"] = flops / avg_s / 1e12  # reference-equivalent (SURVEY §8d MACs)
+            if args.dtype == "bf16" and edge_kernel == 1 and name in EXEC_EDGE_MAC[True]:
+                rec["exec_tflops"] = 2.0 * EXEC_EDGE_MAC[bool(gb0.geo_ref)][name] * edges / avg_s / 1e12
         if byts is not None:
             rec["gbs"] = byts / avg_s / 1e9
         kern[name] = rec

@@ -115,8 +115,9 @@ int di_edge_layer(const di_graph* g, di_dtype dt, int final_layer, const float* 
                   const void* wmat, const float* wvec,
                   float* alpha_out /*[Et,4]*/, void* f_out, void* fn_out, void* stream);
 /* Edge-layer kernel of the bf16 path (process-wide scheduling knob, not a reference interface):
- * 0 = two 4-wave blocks per CU (240 registers per wave), 1 = lean form, two 8-wave blocks per CU
- * (120 registers, four waves per SIMD). -1 only queries. Returns the previous choice. */
+ * 0 = two 4-wave blocks per CU, 16 rows per wave; 1 (default) = grouped form, two 4-wave blocks
+ * per CU, two 16-row groups per wave sharing every LDS weight fragment (the only kernel that
+ * honours DI_GRAPH_GEO_REF). -1 only queries. Returns the previous choice. */
 int di_edge_config(int32_t kernel);
 
 /* hT_out (optional, may be NULL): also write h_out transposed, [128, Nt] (pair-tensor input) */
