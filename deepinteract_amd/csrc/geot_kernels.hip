@@ -350,10 +350,12 @@ constexpr int edge_nstage() { return MODE == 2 ? EL_NSTAGE_CONF : (MODE == 1 ? E
 // w(), its bias vector v()) and keeps the DMA stream ahead of it (ring: two stages, barrier pipe:
 // one); the sequence runs on across the block's tiles (stage 0 of tile t+1 follows the last stage
 // of tile t).
-template <class DT, int MODE>
+// GC (DI_GRAPH_GEO_REF batches, layer modes 0/1): the sequence starts at orig_msg_linear, which
+// then carries the orig_msg_linear bias, and (intermediate layers) ends before nbr_linear
+template <class DT, int MODE, bool GC = false>
 struct EdgeStages {
   using T = typename DT::T;
-  static constexpr int NS = edge_nstage<MODE>();
+  static constexpr int NS = edge_nstage<MODE>() - (GC ? (MODE == 1 ? 2 : 3) : 0);
   EdgePipe<DT>& pipe;
   const T* W;
   const float* V;
@@ -361,8 +363,9 @@ struct EdgeStages {
   int total;  // stages this block runs (tiles x NS)
   const float* vcur;
   __device__ void issue(int i, bool pumped = false) {
-    const int s = i % NS;
-    const int vo = EL_VEC[s];
+    const int s0 = i % NS;
+    const int s = GC ? s0 + 2 : s0;
+    const int vo = (GC && s0 == 0) ? ELV_OM : EL_VEC[s];
     if constexpr (EdgeGeo<DT>::RING) {
       if (pumped) pipe.defer(i, W + EL_ORDER[s] * BLK, EL_SIZE[s], vo >= 0 ? V + vo : nullptr);
       else pipe.issue(i, W + EL_ORDER[s] * BLK, EL_SIZE[s], vo >= 0 ? V + vo : nullptr);
@@ -408,8 +411,8 @@ struct EdgeStages {
   __device__ const float* v() const { return vcur; }
 };
 
-template <class DT, int MODE>
-__device__ __forceinline__ void res_block(Act<8>& x, EdgeStages<DT, MODE>& st, int lane, int g) {
+template <class DT, int MODE, bool GC>
+__device__ __forceinline__ void res_block(Act<8>& x, EdgeStages<DT, MODE, GC>& st, int lane, int g) {
   constexpr bool FAST = DT::kBF16;
   Act<8> y = x;
 #pragma unroll 1
@@ -427,7 +430,7 @@ __device__ __forceinline__ void res_block(Act<8>& x, EdgeStages<DT, MODE>& st, i
 // One tile's per-row inputs, loaded a tile ahead (persistent blocks): neighbour ids, the 28 edge
 // features, the edge's own row F (bf16: raw, it IS the packed MFMA operand) and the first
 // neighbour row. The loads are issued during the previous tile's last stages.
-template <class DT>
+template <class DT, bool GC = false>
 struct EdgeIn {
   using T = typename DT::T;
   int4 nb;
@@ -435,12 +438,12 @@ struct EdgeIn {
   RawRow<T> fraw;
   RawRow<T> xn;
   __device__ __forceinline__ void load_ids(const EdgeArgs& a, int e) {
-    nb = *reinterpret_cast<const int4*>(a.nbr + (int64_t)e * 4);
+    if constexpr (!GC) nb = *reinterpret_cast<const int4*>(a.nbr + (int64_t)e * 4);
   }
   __device__ __forceinline__ void load_rest(const EdgeArgs& a, int e, int g) {
     load_edge_geo(geo, a.edge_f + (int64_t)e * NFEAT_E, g);
     if constexpr (DT::kBF16) fraw.load(reinterpret_cast<const T*>(a.f_in) + (int64_t)e * HID, g);
-    xn.load(reinterpret_cast<const T*>(a.fn_in) + (int64_t)nb.x * HID, g);
+    if constexpr (!GC) xn.load(reinterpret_cast<const T*>(a.fn_in) + (int64_t)nb.x * HID, g);
   }
 };
 
@@ -472,7 +475,9 @@ __device__ __forceinline__ int xcd_tile(int b, int ntiles) {
 // Persistent: each block walks tiles blockIdx.x, +gridDim.x, ...; the weight-stage stream runs on
 // across tiles (the last stage's DMA slot fetches stage 0 of the next tile) and the next tile's
 // inputs are prefetched under the current tile's last stages, so no tile pays a cold prologue.
-template <class DT, int MODE>
+// GC (DI_GRAPH_GEO_REF, modes 0/1): the neighbour-message stages are skipped (exactly zero) and no
+// silu(nbr_linear(F)) rows are gathered or written.
+template <class DT, int MODE, bool GC = false>
 #ifndef DI_EDGE_NUM_VGPR
 #define DI_EDGE_NUM_VGPR 120
 #endif
@@ -497,7 +502,7 @@ void k_edge_layer(EdgeArgs a) {
   const int my_tiles = (ntiles - first + (int)gridDim.x - 1) / (int)gridDim.x;
 
   EdgePipe<DT> pipe(lds);
-  EdgeStages<DT, MODE> st{pipe, W, a.wvec, 0, my_tiles * EdgeStages<DT, MODE>::NS, nullptr};
+  EdgeStages<DT, MODE, GC> st{pipe, W, a.wvec, 0, my_tiles * EdgeStages<DT, MODE, GC>::NS, nullptr};
   st.begin();
   if constexpr (G::RING) {
     // the younger half (waves 4-7) of the block: static priority and/or a start delay, so the two
@@ -507,7 +512,7 @@ void k_edge_layer(EdgeArgs a) {
     if (DI_RING_STAGGER > 0 && young)
       for (int t = 0; t < DI_RING_STAGGER; ++t) __builtin_amdgcn_s_sleep(8);
   }
-  EdgeIn<DT> in;
+  EdgeIn<DT, GC> in;
   {
     bool v0;
     const int e0 = tile_edge<DT>(first, a.Et, v0);
@@ -530,64 +535,72 @@ void k_edge_layer(EdgeArgs a) {
     FRow<DT> fr;
     if constexpr (DT::kBF16) fr.set_raw(in.fraw);
 
-    // ---- neighbour-edge messages (conformation_module_message_func :384-418)
-    const T* w = st.next();  // stage 0: geometric gates + downward_proj
-    Act<4> gate;              // dir . orient . amide embeddings (64)
-    {
-      Act<4> t1;
-      zero(gate);
-      mma<4, 1>(gate, gop, w + 8 * BLK, lane, st.pp());
-      zero(t1);
-      mma<4, 1>(t1, gop, w + 12 * BLK, lane, st.pp());
-      mul_(gate, t1);
-      zero(t1);
-      mma<4, 1>(t1, gop, w + 16 * BLK, lane, st.pp());
-      mul_(gate, t1);
-    }
-    Act<4> s;
-    zero(s);
-    RawRow<T> xn = in.xn;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      Act<8> x;
-      xn.to_act(x);
-      if (j < 3) {  // prefetch the next neighbour row under this one's MFMAs
-        const int nx = j == 0 ? nb.y : (j == 1 ? nb.z : nb.w);
-        xn.load(fn_in + (int64_t)nx * HID, g);
-      }
-      // dist_linear_1(dist_linear_0(dist)), recomputed per neighbour (8 MFMAs) rather than held
-      // live across the loop: the memory clobber stops the compiler from hoisting it (32 VGPRs)
-      asm volatile("" ::: "memory");
-      Act<8> dg;
-      zero(dg);
-      mma<8, 1>(dg, gop, w, lane, st.pp());
-#pragma unroll
-      for (int b = 0; b < 8; ++b)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) x.v[b][q] *= dg.v[b][q];  // gathered rows are silu(nbr_linear(F))
-      Act<4> y;
-      zero(y);
-      linear<DT, 4, 4>(y, x, w + 20 * BLK, lane, st.pp());  // downward_proj
-#pragma unroll
-      for (int b = 0; b < 4; ++b)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) s.v[b][q] += silu2<FAST>(y.v[b][q]) * gate.v[b][q];
-    }
+    const T* w;
     Act<8> x;
-    w = st.next();  // stage 1: upward_proj (+ orig_msg_linear bias)
-    zero(x);
-    linear<DT, 8, 2>(x, s, w, lane, st.pp());
-    silu2_<8, FAST>(x);
-    {
-      Act<8> bo;
-      init_vec_lds(bo, st.v(), g);
+    if constexpr (GC) {
+      // DI_GRAPH_GEO_REF: the neighbour messages are multiplied by dir_linear_1(dir_linear_0(0)) = 0
+      // (:408): x = orig_msg_linear(F) + b exactly
+      w = st.next();  // orig_msg_linear (+ its bias)
+      init_vec_lds(x, st.v(), g);
+    } else {
+      // ---- neighbour-edge messages (conformation_module_message_func :384-418)
+      w = st.next();  // stage 0: geometric gates + downward_proj
+      Act<4> gate;              // dir . orient . amide embeddings (64)
+      {
+        Act<4> t1;
+        zero(gate);
+        mma<4, 1>(gate, gop, w + 8 * BLK, lane, st.pp());
+        zero(t1);
+        mma<4, 1>(t1, gop, w + 12 * BLK, lane, st.pp());
+        mul_(gate, t1);
+        zero(t1);
+        mma<4, 1>(t1, gop, w + 16 * BLK, lane, st.pp());
+        mul_(gate, t1);
+      }
+      Act<4> s;
+      zero(s);
+      RawRow<T> xn = in.xn;
 #pragma unroll
-      for (int b = 0; b < 8; ++b) x.v[b] = silu2_unit<FAST>() * x.v[b] + bo.v[b];
+      for (int j = 0; j < 4; ++j) {
+        Act<8> x;
+        xn.to_act(x);
+        if (j < 3) {  // prefetch the next neighbour row under this one's MFMAs
+          const int nx = j == 0 ? nb.y : (j == 1 ? nb.z : nb.w);
+          xn.load(fn_in + (int64_t)nx * HID, g);
+        }
+        // dist_linear_1(dist_linear_0(dist)), recomputed per neighbour (8 MFMAs) rather than held
+        // live across the loop: the memory clobber stops the compiler from hoisting it (32 VGPRs)
+        asm volatile("" ::: "memory");
+        Act<8> dg;
+        zero(dg);
+        mma<8, 1>(dg, gop, w, lane, st.pp());
+#pragma unroll
+        for (int b = 0; b < 8; ++b)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) x.v[b][q] *= dg.v[b][q];  // gathered rows are silu(nbr_linear(F))
+        Act<4> y;
+        zero(y);
+        linear<DT, 4, 4>(y, x, w + 20 * BLK, lane, st.pp());  // downward_proj
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) s.v[b][q] += silu2<FAST>(y.v[b][q]) * gate.v[b][q];
+      }
+      w = st.next();  // stage 1: upward_proj (+ orig_msg_linear bias)
+      zero(x);
+      linear<DT, 8, 2>(x, s, w, lane, st.pp());
+      silu2_<8, FAST>(x);
+      {
+        Act<8> bo;
+        init_vec_lds(bo, st.v(), g);
+#pragma unroll
+        for (int b = 0; b < 8; ++b) x.v[b] = silu2_unit<FAST>() * x.v[b] + bo.v[b];
+      }
+      w = st.next();  // stage 2: orig_msg_linear(res) + nbr
     }
-    w = st.next();  // stage 2: orig_msg_linear(res) + nbr
     mma<8, 4>(x, fr.operand(f_row, g), w, lane, st.pp());
-    res_block<DT, MODE>(x, st, lane, g);
-    res_block<DT, MODE>(x, st, lane, g);
+    res_block<DT, MODE, GC>(x, st, lane, g);
+    res_block<DT, MODE, GC>(x, st, lane, g);
     {
       w = st.next();  // res_connect_linear
       Act<8> y;
@@ -597,8 +610,8 @@ void k_edge_layer(EdgeArgs a) {
       fr.act(x, f_row, g);
       add_scaled_(x, y, silu2_unit<FAST>());
     }
-    res_block<DT, MODE>(x, st, lane, g);
-    res_block<DT, MODE>(x, st, lane, g);
+    res_block<DT, MODE, GC>(x, st, lane, g);
+    res_block<DT, MODE, GC>(x, st, lane, g);
     {
       w = st.next();  // final geometric gate
       if ((FINAL || CONF) && more) in.load_ids(a, en);
@@ -675,6 +688,7 @@ void k_edge_layer(EdgeArgs a) {
         }
       add_(e1, o);
       if (valid) store_row(e1, reinterpret_cast<T*>(a.f_out) + (int64_t)e * HID, g);
+      if constexpr (GC) continue;  // no silu(nbr_linear(F)) rows for the next layer
       w = st.next();  // next layer's silu(nbr_linear(.))
       Act<8> fn;
       init_vec_lds(fn, st.v(), g);
@@ -1664,9 +1678,9 @@ extern "C" int di_edge_layer(const di_graph* g, di_dtype dt, int final_layer, co
                              const void* f_in, const void* fn_in, const void* qkv, const void* wmat,
                              const float* wvec, float* alpha_out, void* f_out, void* fn_out,
                              void* stream) {
-  // DI_GRAPH_GEO_REF on the grouped bf16 kernel: the neighbour-message branch is skipped, fn_in is
-  // not read and fn_out not written; every other kernel computes the (exactly zero) branch
-  const bool gc = g && (g->flags & DI_GRAPH_GEO_REF) && dt == DI_BF16 && g_edge_kernel == 1;
+  // DI_GRAPH_GEO_REF: the neighbour-message branch is skipped (exactly zero), fn_in is not read and
+  // fn_out not written (every edge-layer kernel; di_conformation computes the branch)
+  const bool gc = g && (g->flags & DI_GRAPH_GEO_REF);
   if (!g || !edge_f || !f_in || (!fn_in && !gc) || !qkv || !wmat || !wvec || !alpha_out || g->num_edges <= 0)
     return DI_EINVAL;
   if (!final_layer && (!f_out || (!fn_out && !gc))) return DI_EINVAL;
@@ -1689,11 +1703,15 @@ extern "C" int di_edge_layer(const di_graph* g, di_dtype dt, int final_layer, co
     const int resident = (EdgeGeo<BF16T>::RING ? 1 : 2) * num_cus();
     const bool persist = EdgeGeo<BF16T>::RING || DI_EDGE_PERSIST;
     dim3 grid(persist && tiles > resident ? resident : xcd_grid(tiles)), block(EdgeGeo<BF16T>::THREADS);
-    if (final_layer) hipLaunchKernelGGL((k_edge_layer<BF16T, 1>), grid, block, 0, s, a);
+    if (final_layer && gc) hipLaunchKernelGGL((k_edge_layer<BF16T, 1, true>), grid, block, 0, s, a);
+    else if (final_layer) hipLaunchKernelGGL((k_edge_layer<BF16T, 1>), grid, block, 0, s, a);
+    else if (gc) hipLaunchKernelGGL((k_edge_layer<BF16T, 0, true>), grid, block, 0, s, a);
     else hipLaunchKernelGGL((k_edge_layer<BF16T, 0>), grid, block, 0, s, a);
   } else {
     dim3 grid(xcd_grid(grid_rows(a.Et, EdgeGeo<F32T>::ROWS))), block(EdgeGeo<F32T>::THREADS);
-    if (final_layer) hipLaunchKernelGGL((k_edge_layer<F32T, 1>), grid, block, 0, s, a);
+    if (final_layer && gc) hipLaunchKernelGGL((k_edge_layer<F32T, 1, true>), grid, block, 0, s, a);
+    else if (final_layer) hipLaunchKernelGGL((k_edge_layer<F32T, 1>), grid, block, 0, s, a);
+    else if (gc) hipLaunchKernelGGL((k_edge_layer<F32T, 0, true>), grid, block, 0, s, a);
     else hipLaunchKernelGGL((k_edge_layer<F32T, 0>), grid, block, 0, s, a);
   }
   return launch_status();

@@ -151,10 +151,10 @@ class GeoTEngine:
         g = ctypes.byref(gb.c_graph)
         st = _stream()
         h, qkv, f, fn, alpha = ws["h"], ws["qkv"], ws["f"], ws["fn"], ws["alpha"]
-        # DI_GRAPH_GEO_REF batches on the grouped bf16 edge kernel: the conformation module's
-        # neighbour messages are exactly zero (include/deepinteract_amd.h), so the gathered
-        # silu(nbr_linear(F)) rows are neither written nor read
-        if gb.geo_ref and self.dtype == "bf16" and lib.di_edge_config(-1) == 1:
+        # DI_GRAPH_GEO_REF batches: the conformation module's neighbour messages are exactly zero
+        # (include/deepinteract_amd.h), so the gathered silu(nbr_linear(F)) rows are neither
+        # written nor read
+        if gb.geo_ref:
             fn = [None, None]
         tick = _Ticker(events)
         tick("node_embed")

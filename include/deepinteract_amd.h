@@ -80,9 +80,9 @@ typedef struct {
  * orientation terms are per-model constants. With this flag:
  *   di_init_edge  skips the direction terms, adds the orientation terms as packed constants, and
  *                 writes fn_out only when fn_out != NULL;
- *   di_edge_layer (bf16, kernel 1) skips the neighbour-message branch: fn_in is not read and
- *                 fn_out is not written (both may be NULL).
- * The other kernels ignore the flag (they compute the branch, which is exactly zero). */
+ *   di_edge_layer skips the neighbour-message branch: fn_in is not read and fn_out is not
+ *                 written (both may be NULL).
+ * di_conformation ignores the flag (it computes the branch, which is exactly zero). */
 #define DI_GRAPH_GEO_REF 1
 
 /* one complex of a pair-tensor launch (host-built array copied to the device) */
@@ -116,8 +116,8 @@ int di_edge_layer(const di_graph* g, di_dtype dt, int final_layer, const float* 
                   float* alpha_out /*[Et,4]*/, void* f_out, void* fn_out, void* stream);
 /* Edge-layer kernel of the bf16 path (process-wide scheduling knob, not a reference interface):
  * 0 = two 4-wave blocks per CU, 16 rows per wave; 1 (default) = grouped form, two 4-wave blocks
- * per CU, two 16-row groups per wave sharing every LDS weight fragment (the only kernel that
- * honours DI_GRAPH_GEO_REF). -1 only queries. Returns the previous choice. */
+ * per CU, two 16-row groups per wave sharing every LDS weight fragment. -1 only queries.
+ * Returns the previous choice. */
 int di_edge_config(int32_t kernel);
 
 /* hT_out (optional, may be NULL): also write h_out transposed, [128, Nt] (pair-tensor input) */
