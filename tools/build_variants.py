@@ -16,6 +16,8 @@ VARIANTS = {
     "noslp": ["-fno-slp-vectorize"],
     "xcd": ["DI_XCD_TILES=1"],
     "prio1": ["DI_GEOT_PRIO=1"],
+    "prio2": ["DI_GEOT_PRIO=2"],
+    "prio3": ["DI_GEOT_PRIO=3"],
     "persist": ["DI_EDGE_PERSIST=1"],
     # grouped/lean edge layer (bench --edge-kernel 1): waves per block, waves per SIMD, VGPR cap / 2
     "lean4": ["DI_LEAN_NW=4", "DI_LEAN_WPE=2", "DI_LEAN_VGPR=120"],
