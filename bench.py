@@ -278,6 +278,10 @@ def main():
                     help="max_num_graph_nodes of the synthetic model (default 2304; c5: 4096)")
     ap.add_argument("--edge-kernel", type=int, default=None, choices=[0, 1],
                     help="bf16 edge-layer kernel (di_edge_config): 0 two 4-wave blocks per CU, 1 grouped/lean form")
+    ap.add_argument("--node-kernel", default=None, choices=["split", "fused"],
+                    help="node layer as di_node_aggregate + di_node_update (split; faster alone: 48 vs 68 us "
+                         "per micro-batch) or one di_node_layer (fused; faster beside the pair stream: 91 vs "
+                         "109 us). Default: fused when overlapped, split otherwise")
     ap.add_argument("--only", default=None, choices=["geot", "pair"],
                     help="diagnostic (not the metric): run only the GeoT stream or only the pair-tensor stream")
     ap.add_argument("--lib", default=None, help="tuning: a launch-shape variant of the HIP library "
@@ -326,6 +330,9 @@ def main():
         if _lib_check < 0:
             raise SystemExit(f"di_edge_config({args.edge_kernel}) failed")
     edge_kernel = eng.lib.di_edge_config(-1)
+    if args.node_kernel is None:
+        args.node_kernel = "fused" if args.overlap else "split"
+    eng.split_node = args.node_kernel == "split"
     num_cus = torch.cuda.get_device_properties(dev).multi_processor_count
     if args.pair_cus:
         if not args.overlap:
@@ -495,6 +502,7 @@ def main():
                       f"{num_cus - args.pair_cus}" if args.pair_cus else "")
                    + f"; pair kernel {args.pair_kernel}"
                    + (f"; DIAGNOSTIC: {args.only} stream only (not the metric)" if args.only else "")
+                   + f"; node layer {args.node_kernel}"
                    + (f", pace {args.pair_pace}" if args.pair_pace else "")
                    + f"; edge-layer kernel {['k_edge_layer', 'k_edge_lean'][edge_kernel] if args.dtype == 'bf16' else 'k_edge_layer (f32)'}"},
         "hbm_frac_of_peak": round(hbm_frac, 4),
