@@ -30,6 +30,13 @@ constexpr int PAIR_UNROLL = 4;
 #ifndef DI_PAIR_STORE
 #define DI_PAIR_STORE 0
 #endif
+// ... and of the bounded row kernel that runs beside GeoT (kernel 3): non-temporal, so the store
+// stream does not evict GeoT's L2-resident weight stages and rows. Measured beside GeoT (C3, 512
+// complexes): nt 7472 vs plain 7002 complexes/s (GeoT edge layer 429 vs 471 us, pair 1045 vs
+// 1082 us); sc0 7018, sc1 3818.
+#ifndef DI_PAIR_STORE_BESIDE
+#define DI_PAIR_STORE_BESIDE 2
+#endif
 
 template <typename T>
 struct Vec16;
@@ -154,7 +161,7 @@ __global__ __launch_bounds__(PAIR_THREADS) void k_pair_tensor(const di_pair_desc
 #define DI_PAIR_INFLIGHT 3
 #endif
 constexpr int PAIR_SEG = 128;  // 16-B chunks per row segment (2 per lane)
-template <typename T, int INFLIGHT>
+template <typename T, int INFLIGHT, int CPOL>
 __global__ __launch_bounds__(1024) __attribute__((amdgpu_num_vgpr(32)))
 void k_pair_rows(const di_pair_desc* __restrict__ descs, int hidden, const T* __restrict__ h,
                  const T* __restrict__ hT, int nrows, int rblocks, int items, T* __restrict__ out, int pace) {
@@ -203,9 +210,9 @@ void k_pair_rows(const di_pair_desc* __restrict__ descs, int hidden, const T* __
           v1 = v0;
         }
         if (k0 < nch)
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uintx4, v0), r, k0 * 16, soff, DI_PAIR_STORE);
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uintx4, v0), r, k0 * 16, soff, CPOL);
         if (two && k1 < nch)
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uintx4, v1), r, k1 * 16, soff, DI_PAIR_STORE);
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uintx4, v1), r, k1 * 16, soff, CPOL);
         if constexpr (INFLIGHT > 0)  // bound this wave's queued stores (see DI_PAIR_INFLIGHT)
           asm volatile("s_waitcnt vmcnt(%0)" ::"n"(INFLIGHT) : "memory");
         for (int t = 0; t < pace; ++t) __builtin_amdgcn_s_sleep(1);  // store-rate pacing (di_pair_pace)
@@ -274,16 +281,16 @@ extern "C" int di_pair_tensor(di_dtype dt, const di_pair_desc* descs, int32_t nu
     const unsigned rgrid = (unsigned)(ritems < max_blocks ? ritems : max_blocks);
     const bool bounded = g_pair_kernel == 3;
     if (dt == DI_BF16 && bounded)
-      hipLaunchKernelGGL((k_pair_rows<u16, DI_PAIR_INFLIGHT>), dim3(rgrid), dim3(rows), 0, s, descs, hidden,
+      hipLaunchKernelGGL((k_pair_rows<u16, DI_PAIR_INFLIGHT, DI_PAIR_STORE_BESIDE>), dim3(rgrid), dim3(rows), 0, s, descs, hidden,
                          (const u16*)h, (const u16*)hT, num_rows, rblocks, ritems, (u16*)out, g_pair_pace);
     else if (dt == DI_BF16)
-      hipLaunchKernelGGL((k_pair_rows<u16, 0>), dim3(rgrid), dim3(rows), 0, s, descs, hidden, (const u16*)h,
+      hipLaunchKernelGGL((k_pair_rows<u16, 0, DI_PAIR_STORE>), dim3(rgrid), dim3(rows), 0, s, descs, hidden, (const u16*)h,
                          (const u16*)hT, num_rows, rblocks, ritems, (u16*)out, g_pair_pace);
     else if (bounded)
-      hipLaunchKernelGGL((k_pair_rows<float, DI_PAIR_INFLIGHT>), dim3(rgrid), dim3(rows), 0, s, descs, hidden,
+      hipLaunchKernelGGL((k_pair_rows<float, DI_PAIR_INFLIGHT, DI_PAIR_STORE_BESIDE>), dim3(rgrid), dim3(rows), 0, s, descs, hidden,
                          (const float*)h, (const float*)hT, num_rows, rblocks, ritems, (float*)out, g_pair_pace);
     else
-      hipLaunchKernelGGL((k_pair_rows<float, 0>), dim3(rgrid), dim3(rows), 0, s, descs, hidden,
+      hipLaunchKernelGGL((k_pair_rows<float, 0, DI_PAIR_STORE>), dim3(rgrid), dim3(rows), 0, s, descs, hidden,
                          (const float*)h, (const float*)hT, num_rows, rblocks, ritems, (float*)out, g_pair_pace);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? DI_OK : (int)e;
