@@ -78,6 +78,13 @@ __device__ __forceinline__ void st4(u16* p, floatx4 v) {
   u.y = pack_bf16x2(v[2], v[3]);
   *reinterpret_cast<uint2*>(p) = u;
 }
+// non-temporal forms (write-once edge rows that do not fit in L2: kept from evicting weight stages)
+__device__ __forceinline__ void st4_nt(float* p, floatx4 v) { __builtin_nontemporal_store(v, reinterpret_cast<floatx4*>(p)); }
+__device__ __forceinline__ void st4_nt(u16* p, floatx4 v) {
+  typedef unsigned int uintx2 __attribute__((ext_vector_type(2)));
+  const uintx2 u = {pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3])};
+  __builtin_nontemporal_store(u, reinterpret_cast<uintx2*>(p));
+}
 
 template <bool FAST>
 __device__ __forceinline__ float expf_(float x) {
@@ -156,6 +163,20 @@ template <int NB, typename T>
 __device__ __forceinline__ void store_row(const Act<NB>& a, T* row, int g) {
 #pragma unroll
   for (int b = 0; b < NB; ++b) st4(row + 16 * b + 4 * g, a.v[b]);
+}
+// edge-row outputs (F, Fn: 82 MB per C3 micro-batch each, re-read by the next kernel from HBM/MALL).
+// DI_EDGE_ROW_NT=1 stores them non-temporally: measured slower beside the pair stream (7108-7150 vs
+// 7438-7441 complexes/s), off
+#ifndef DI_EDGE_ROW_NT
+#define DI_EDGE_ROW_NT 0
+#endif
+template <int NB, typename T>
+__device__ __forceinline__ void store_edge_row(const Act<NB>& a, T* row, int g) {
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    if constexpr (DI_EDGE_ROW_NT) st4_nt(row + 16 * b + 4 * g, a.v[b]);
+    else st4(row + 16 * b + 4 * g, a.v[b]);
+  }
 }
 
 // A 128-feature row held in its STORAGE format (bf16: 16 VGPRs instead of 32), for prefetching

@@ -270,7 +270,7 @@ void k_init_edge(InitArgs a) {
     zero(f);
     linear<DT, 8, 1>(f, z, w + 8 * BLK, lane, PP);
   }
-  if (valid) store_row(f, reinterpret_cast<T*>(a.f_out) + (int64_t)e * HID, g);
+  if (valid) store_edge_row(f, reinterpret_cast<T*>(a.f_out) + (int64_t)e * HID, g);
   if (!with_fn) return;
   // layer-0 silu(nbr_linear(F)), applied once per edge and gathered by the conformation module
   // (silu(nbr_linear(F[ids])) == silu(nbr_linear(F))[ids], deepinteract_modules.py:386-390)
@@ -280,7 +280,7 @@ void k_init_edge(InitArgs a) {
     init_vec(fn, a.wvec + IEV_NBR, g);
     linear<DT, 8, 4>(fn, f, w, lane, PP);
     silu_<8, FAST>(fn);
-    if (valid) store_row(fn, reinterpret_cast<T*>(a.fn_out) + (int64_t)e * HID, g);
+    if (valid) store_edge_row(fn, reinterpret_cast<T*>(a.fn_out) + (int64_t)e * HID, g);
   }
 }
 
@@ -687,14 +687,14 @@ void k_edge_layer(EdgeArgs a) {
         linear<DT, 8, 4>(o, t, w, lane, st.pp());
         }
       add_(e1, o);
-      if (valid) store_row(e1, reinterpret_cast<T*>(a.f_out) + (int64_t)e * HID, g);
+      if (valid) store_edge_row(e1, reinterpret_cast<T*>(a.f_out) + (int64_t)e * HID, g);
       if constexpr (GC) continue;  // no silu(nbr_linear(F)) rows for the next layer
       w = st.next();  // next layer's silu(nbr_linear(.))
       Act<8> fn;
       init_vec_lds(fn, st.v(), g);
       linear<DT, 8, 4>(fn, e1, w, lane, st.pp());
       silu_<8, FAST>(fn);
-      if (valid) store_row(fn, reinterpret_cast<T*>(a.fn_out) + (int64_t)e * HID, g);
+      if (valid) store_edge_row(fn, reinterpret_cast<T*>(a.fn_out) + (int64_t)e * HID, g);
     }
   }
 }
@@ -1233,7 +1233,7 @@ void k_edge_lean(EdgeArgs a) {
 #pragma unroll
     for (int q = 0; q < LG; ++q) {
     DI_FENCE();
-      if (rw[q].valid) store_row(e1[q], reinterpret_cast<u16*>(a.f_out) + (int64_t)rw[q].e * HID, g);
+      if (rw[q].valid) store_edge_row(e1[q], reinterpret_cast<u16*>(a.f_out) + (int64_t)rw[q].e * HID, g);
       make_op(eop[q], e1[q]);
     }
     if constexpr (GC) return;  // the next layer gathers no silu(nbr_linear(F)) rows
@@ -1247,7 +1247,7 @@ void k_edge_lean(EdgeArgs a) {
       if constexpr (Lean::SHARED) fn = fng[q];
       else lin_op<8, 4>(fn, eop[q], w, st.v(), lane, g);
       silu_<8, true>(fn);
-      if (rw[q].valid) store_row(fn, reinterpret_cast<u16*>(a.fn_out) + (int64_t)rw[q].e * HID, g);
+      if (rw[q].valid) store_edge_row(fn, reinterpret_cast<u16*>(a.fn_out) + (int64_t)rw[q].e * HID, g);
     }
   }
 }

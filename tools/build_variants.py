@@ -37,6 +37,7 @@ VARIANTS = {
     "lean4g2ns": ["DI_LEAN_NW=4", "DI_LEAN_WPE=2", "DI_LEAN_VGPR=120", "DI_LEAN_G=2", "DI_LEAN_SHARE=0"],
     "lean4g2d4": ["DI_LEAN_NW=4", "DI_LEAN_WPE=2", "DI_LEAN_VGPR=120", "DI_LEAN_G=2", "DI_MMA_DEPTH=4"],
     "pst_plain": ["DI_PAIR_STORE_BESIDE=0"],
+    "edge_nt": ["DI_EDGE_ROW_NT=1"],
     "nt_if4": ["DI_PAIR_INFLIGHT=4"],
     "nt_if6": ["DI_PAIR_INFLIGHT=6"],
     "nt_if2": ["DI_PAIR_INFLIGHT=2"],
