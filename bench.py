@@ -282,6 +282,9 @@ def main():
                     help="node layer as di_node_aggregate + di_node_update (split; faster alone: 48 vs 68 us "
                          "per micro-batch) or one di_node_layer (fused; faster beside the pair stream: 91 vs "
                          "109 us). Default: fused when overlapped, split otherwise")
+    ap.add_argument("--embed-stream", type=int, default=None, choices=[0, 1],
+                    help="1: node embedding on a side stream, concurrent with InitEdge (default when "
+                         "overlapped: 7636-7692 vs 7431-7558 complexes/s)")
     ap.add_argument("--only", default=None, choices=["geot", "pair"],
                     help="diagnostic (not the metric): run only the GeoT stream or only the pair-tensor stream")
     ap.add_argument("--lib", default=None, help="tuning: a launch-shape variant of the HIP library "
@@ -333,6 +336,10 @@ def main():
     if args.node_kernel is None:
         args.node_kernel = "fused" if args.overlap else "split"
     eng.split_node = args.node_kernel == "split"
+    if args.embed_stream is None:
+        args.embed_stream = 1 if args.overlap else 0
+    if args.embed_stream:
+        eng.embed_stream = torch.cuda.Stream(dev)
     num_cus = torch.cuda.get_device_properties(dev).multi_processor_count
     if args.pair_cus:
         if not args.overlap:
@@ -503,6 +510,7 @@ def main():
                    + f"; pair kernel {args.pair_kernel}"
                    + (f"; DIAGNOSTIC: {args.only} stream only (not the metric)" if args.only else "")
                    + f"; node layer {args.node_kernel}"
+                   + ("; node embedding on a side stream" if args.embed_stream else "")
                    + (f", pace {args.pair_pace}" if args.pair_pace else "")
                    + f"; edge-layer kernel {['k_edge_layer', 'k_edge_lean'][edge_kernel] if args.dtype == 'bf16' else 'k_edge_layer (f32)'}"},
         "hbm_frac_of_peak": round(hbm_frac, 4),

@@ -86,6 +86,8 @@ class GeoTEngine:
         # fused di_node_layer): the segment reduction at full occupancy instead of 16 lanes per
         # node inside the MFMA kernel's one-block-per-CU grid
         self.split_node = True
+        # optional side stream for the node embedding (concurrent with InitEdge)
+        self.embed_stream = None
 
     def _check_blob_sizes(self):
         p, dt = self.packed, _DI_DT[self.dtype]
@@ -157,15 +159,31 @@ class GeoTEngine:
         if gb.geo_ref:
             fn = [None, None]
         tick = _Ticker(events)
-        tick("node_embed")
-        _lib.check(lib.di_node_embed(g, dt, gb.node_f.shape[1], _ptr(gb.node_f), _ptr(p.embed[0]), _ptr(p.embed[1]),
-                                     _ptr(h[0]), _ptr(qkv[0]), st), "di_node_embed")
+        if self.embed_stream is not None:
+            # node embedding (+ layer-0 Q/K/V) on a side stream, concurrent with InitEdge (which does
+            # not read it); the edge layer waits for both
+            cur = torch.cuda.current_stream()
+            ev0 = torch.cuda.Event()
+            ev0.record(cur)
+            with torch.cuda.stream(self.embed_stream):
+                self.embed_stream.wait_event(ev0)
+                _lib.check(lib.di_node_embed(g, dt, gb.node_f.shape[1], _ptr(gb.node_f), _ptr(p.embed[0]),
+                                             _ptr(p.embed[1]), _ptr(h[0]), _ptr(qkv[0]), _stream()), "di_node_embed")
+                ev1 = torch.cuda.Event()
+                ev1.record(self.embed_stream)
+        else:
+            tick("node_embed")
+            _lib.check(lib.di_node_embed(g, dt, gb.node_f.shape[1], _ptr(gb.node_f), _ptr(p.embed[0]),
+                                         _ptr(p.embed[1]), _ptr(h[0]), _ptr(qkv[0]), st), "di_node_embed")
+            ev1 = None
         tick("init_edge")
         _lib.check(lib.di_init_edge(g, dt, _ptr(gb.edge_f), _ptr(p.init[0]), _ptr(p.init[1]),
                                     _ptr(p.pos_src), _ptr(p.pos_dst), _ptr(f[0]), _ptr(fn[0]), st),
                    "di_init_edge")
         if after_init is not None:
             after_init.record(torch.cuda.current_stream())
+        if ev1 is not None:
+            torch.cuda.current_stream().wait_event(ev1)
         L = p.num_layers
         cur = 0
         for li in range(L):

@@ -34,8 +34,10 @@ def _oracle_graph(gb, g):
             "edge_f": gb.edge_f[e0:e1].cpu()}
 
 
-@pytest.mark.parametrize("edge_kernel,pair_kernel", [(1, "rows_bounded"), (0, "vector")])
-def test_c3_bench_path_bf16_two_slots_two_streams(edge_kernel, pair_kernel):
+@pytest.mark.parametrize("edge_kernel,pair_kernel,side", [(1, "rows_bounded", True), (0, "vector", False)])
+def test_c3_bench_path_bf16_two_slots_two_streams(edge_kernel, pair_kernel, side):
+    """side: bench.py's overlapped defaults — node embedding on a side stream beside InitEdge and the
+    fused node layer."""
     from deepinteract_amd import _lib, synth
     from deepinteract_amd.builder import build_graph_batch
     from deepinteract_amd.engine import GeoTEngine, PairTensorOp
@@ -45,6 +47,9 @@ def test_c3_bench_path_bf16_two_slots_two_streams(edge_kernel, pair_kernel):
 
     sd = seeded_state_dict(0, with_head=False)
     eng = GeoTEngine(sd, "bf16")
+    if side:
+        eng.embed_stream = torch.cuda.Stream()
+        eng.split_node = False
     n_cx = M * N_MB
     chains = [c for j in range(n_cx) for c in synth.synthetic_complex(700 + j, N_RES, N_RES)]
     pool = build_graph_batch(chains, k=K, nbr_seeds=list(range(1, 2 * n_cx + 1)))
