@@ -285,6 +285,9 @@ def main():
     ap.add_argument("--embed-stream", type=int, default=None, choices=[0, 1],
                     help="1: node embedding on a side stream, concurrent with InitEdge (default when "
                          "overlapped: 7636-7692 vs 7431-7558 complexes/s)")
+    ap.add_argument("--slots", type=int, default=2, choices=[2, 3, 4],
+                    help="GeoT workspace slots when overlapped (2: GeoT of m+1 waits for the pair tensor of m-1; "
+                         "3 / 4 measured equal within noise: 7327-7377 / 7305 vs 7292-7435)")
     ap.add_argument("--only", default=None, choices=["geot", "pair"],
                     help="diagnostic (not the metric): run only the GeoT stream or only the pair-tensor stream")
     ap.add_argument("--lib", default=None, help="tuning: a launch-shape variant of the HIP library "
@@ -394,7 +397,10 @@ def main():
         s_geot = torch.cuda.current_stream(dev)
         s_pair = torch.cuda.Stream(dev) if args.overlap else s_geot
     pair_only_inputs = {}  # --only pair: each slot's GeoT outputs, computed once in the warm-up
-    done = [None, None]  # per workspace slot: event after the pair tensor that last read it
+    # workspace slots: GeoT of micro-batch m writes slot m % slots while the pair tensor of m-1 reads
+    # slot (m-1) % slots; with 3+ slots GeoT m+1 never waits for the pair tensor of m-1 to drain
+    n_slots = args.slots if args.overlap else 1
+    done = [None] * n_slots  # per workspace slot: event after the pair tensor that last read it
 
     def launch_pair(h, hT, ready, slot, after=None, events=None):
         with torch.cuda.stream(s_pair):
@@ -414,7 +420,7 @@ def main():
         # memory-heavy node-embedding / InitEdge prologue.
         prev = None
         for m, gb in enumerate(mbs):
-            slot = m & 1 if args.overlap else 0
+            slot = m % n_slots
             after = torch.cuda.Event() if args.overlap == 2 else None
             with torch.cuda.stream(s_geot):
                 if done[slot] is not None:
@@ -511,6 +517,7 @@ def main():
                    + (f"; DIAGNOSTIC: {args.only} stream only (not the metric)" if args.only else "")
                    + f"; node layer {args.node_kernel}"
                    + ("; node embedding on a side stream" if args.embed_stream else "")
+                   + (f"; {args.slots} workspace slots" if args.overlap else "")
                    + (f", pace {args.pair_pace}" if args.pair_pace else "")
                    + f"; edge-layer kernel {['k_edge_layer', 'k_edge_lean'][edge_kernel] if args.dtype == 'bf16' else 'k_edge_layer (f32)'}"},
         "hbm_frac_of_peak": round(hbm_frac, 4),

@@ -38,6 +38,13 @@ VARIANTS = {
     "lean4g2d4": ["DI_LEAN_NW=4", "DI_LEAN_WPE=2", "DI_LEAN_VGPR=120", "DI_LEAN_G=2", "DI_MMA_DEPTH=4"],
     "pst_plain": ["DI_PAIR_STORE_BESIDE=0"],
     "edge_nt": ["DI_EDGE_ROW_NT=1"],
+    "g1s4": ["DI_LEAN_G=1", "DI_LEAN_NW=4", "DI_LEAN_WPE=4", "DI_LEAN_VGPR=64", "DI_LEAN_DBUF=0", "DI_MMA_DEPTH=5"],
+    "g1s3": ["DI_LEAN_G=1", "DI_LEAN_NW=4", "DI_LEAN_WPE=3", "DI_LEAN_VGPR=80", "DI_LEAN_DBUF=0", "DI_MMA_DEPTH=6"],
+    "g1s2": ["DI_LEAN_G=1"],
+    "gc_d3": ["DI_MMA_DEPTH=3"],
+    "gc_d6": ["DI_MMA_DEPTH=6"],
+    "gc_nofence": ["DI_LEAN_FENCE=0"],
+    "gc_holdf": ["DI_LEAN_HOLD_F=1"],
     "nt_if4": ["DI_PAIR_INFLIGHT=4"],
     "nt_if6": ["DI_PAIR_INFLIGHT=6"],
     "nt_if2": ["DI_PAIR_INFLIGHT=2"],
