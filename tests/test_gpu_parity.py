@@ -233,3 +233,37 @@ def test_geot_reference_init_weights():
             hn, en = O.geot_forward(sd, g)
         assert rel_max(hs, hn.numpy()) < F32_TOL
         assert rel_max(es, en.numpy()) < F32_TOL
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_geot_general_path_nonzero_direction_features(engines, sd, dtype):
+    """Edge features from a featuriser that is NOT the reference's (random direction /
+    orientation columns): the batch is not DI_GRAPH_GEO_REF, the neighbour-message branch is live,
+    and the whole GeoT still matches the oracle (fp32 <= 1e-4, bf16 within the stated bound)."""
+    from deepinteract_amd.graph import GraphBatch
+    from oracle import geot_oracle as O
+    z = load_case("tiny")
+    gen = torch.Generator().manual_seed(7)
+    items = []
+    for tag in ("g1", "g2"):
+        it = chain_item(z, tag)
+        ef = it["edge_f"].clone()
+        ef[:, 20:23] = torch.randn(ef.shape[0], 3, generator=gen)
+        ef[:, 23:27] = torch.nn.functional.normalize(torch.randn(ef.shape[0], 4, generator=gen), dim=-1)
+        it["edge_f"] = ef
+        items.append(it)
+    gb = GraphBatch.from_arrays(items, "cuda")
+    assert not gb.geo_ref and gb.c_graph.flags == 0
+    h, e = engines[dtype].forward(gb)
+    torch.cuda.synchronize()
+    h, e = h.float().cpu().numpy(), e.float().cpu().numpy()
+    tol = F32_TOL if dtype == "f32" else BF16_TOL
+    errs = []
+    for i, it in enumerate(items):
+        with torch.no_grad():
+            n_ref, e_ref = O.geot_forward(sd, it)
+        n0, n1 = gb.node_off[i], gb.node_off[i + 1]
+        e0, e1 = gb.edge_off[i], gb.edge_off[i + 1]
+        errs += [rel_max(h[n0:n1], n_ref.numpy()), rel_max(e[e0:e1], e_ref.numpy())]
+    print(f"tiny, random direction/orientation, {dtype}: node/edge errors", ", ".join(f"{x:.3e}" for x in errs))
+    assert max(errs) < tol
