@@ -190,12 +190,29 @@ __global__ __launch_bounds__(THREADS) void k_node_embed(EmbedArgs a) {
 // the orientation terms are the packed constants IEV_ORC / IEV_OGATE; the layer-0
 // silu(nbr_linear(F)) rows are only computed when fn_out is given (the grouped edge kernel does
 // not gather them for such batches).
+// Launch shape of the bf16 InitEdge: weights staged synchronously in one 40-KiB slot per block
+// (DI_INIT_DBUF=0), so three blocks share a CU (DI_INIT_WPE=3; the kernel holds 150 VGPRs) and
+// cover each other's stage waits. Measured (C3 micro-batch, GEO_REF): alone 109 vs 118 us with two
+// double-buffered blocks, beside the pair stream 168 vs 187 us; four blocks (128 VGPRs) spill:
+// 130 / 206 us.
+#ifndef DI_INIT_DBUF
+#define DI_INIT_DBUF 0
+#endif
+#ifndef DI_INIT_WPE
+#define DI_INIT_WPE 3
+#endif
+template <class DT>
+struct InitGeo : Geo<DT> {
+  static constexpr bool DBUF = DT::kBF16 && DI_INIT_DBUF;
+  static constexpr int WPE = DT::kBF16 ? DI_INIT_WPE : 2;
+};
 template <class DT, bool GC>
-__global__ __attribute__((amdgpu_flat_work_group_size(1, 64 * DI_GEO_NW), amdgpu_waves_per_eu(2, 2)))
+__global__ __attribute__((amdgpu_flat_work_group_size(1, 64 * DI_GEO_NW),
+                          amdgpu_waves_per_eu(InitGeo<DT>::WPE, InitGeo<DT>::WPE)))
 void k_init_edge(InitArgs a) {
   using T = typename DT::T;
   DI_GEOT_ENTRY();
-  using G = Geo<DT>;
+  using G = InitGeo<DT>;
   constexpr bool FAST = DT::kBF16;
   constexpr int CAP = G::CAP;
   __shared__ __attribute__((aligned(16))) T lds[(G::DBUF ? 2 : 1) * CAP * BLK];
