@@ -201,13 +201,19 @@ __global__ __launch_bounds__(THREADS) void k_node_embed(EmbedArgs a) {
 #ifndef DI_INIT_WPE
 #define DI_INIT_WPE 3
 #endif
+#ifndef DI_INIT_NW
+#define DI_INIT_NW 4
+#endif
 template <class DT>
 struct InitGeo : Geo<DT> {
   static constexpr bool DBUF = DT::kBF16 && DI_INIT_DBUF;
   static constexpr int WPE = DT::kBF16 ? DI_INIT_WPE : 2;
+  static constexpr int NW = DT::kBF16 ? DI_INIT_NW : Geo<DT>::NW;  // waves per block
+  static constexpr int THREADS = 64 * NW;
+  static constexpr int ROWS = ROWS_PER_WAVE * NW;
 };
 template <class DT, bool GC>
-__global__ __attribute__((amdgpu_flat_work_group_size(1, 64 * DI_GEO_NW),
+__global__ __attribute__((amdgpu_flat_work_group_size(1, 64 * (DT::kBF16 ? DI_INIT_NW : DI_GEO_NW)),
                           amdgpu_waves_per_eu(InitGeo<DT>::WPE, InitGeo<DT>::WPE)))
 void k_init_edge(InitArgs a) {
   using T = typename DT::T;
@@ -1682,8 +1688,8 @@ extern "C" int di_init_edge(const di_graph* g, di_dtype dt, const float* edge_f,
   InitArgs a{g->num_edges, edge_f, g->src, g->dst, g->node_pos, wmat, wvec, pos_src_tab, pos_dst_tab,
              f_out, fn_out};
   hipStream_t s = (hipStream_t)stream;
-  const dim3 gb(grid_rows(a.Et, Geo<BF16T>::ROWS)), bb(Geo<BF16T>::THREADS);
-  const dim3 gf(grid_rows(a.Et, Geo<F32T>::ROWS)), bf(Geo<F32T>::THREADS);
+  const dim3 gb(grid_rows(a.Et, InitGeo<BF16T>::ROWS)), bb(InitGeo<BF16T>::THREADS);
+  const dim3 gf(grid_rows(a.Et, InitGeo<F32T>::ROWS)), bf(InitGeo<F32T>::THREADS);
   if (dt == DI_BF16 && gc) hipLaunchKernelGGL((k_init_edge<BF16T, true>), gb, bb, 0, s, a);
   else if (dt == DI_BF16) hipLaunchKernelGGL((k_init_edge<BF16T, false>), gb, bb, 0, s, a);
   else if (gc) hipLaunchKernelGGL((k_init_edge<F32T, true>), gf, bf, 0, s, a);
