@@ -114,3 +114,37 @@ def test_c3_bench_path_bf16_two_slots_two_streams(edge_kernel, pair_kernel, side
         errs[f"mb{m}_c{j}_pair"] = rel_max(got.float().cpu().numpy(), pt[idx[:, 0], idx[:, 1], idx[:, 2]])
     print(f"C3 bf16 errors, edge kernel {edge_kernel}, pair kernel {pair_kernel} (max-abs / max-abs ref):", {k: f"{v:.3e}" for k, v in errs.items()})
     assert max(errs.values()) < BF16_GEOT_TOL, errs
+
+
+def test_c3_fp32_matches_oracle():
+    """The reference's precision at the metric's shape: fp32 GeoT (device builder, reference-
+    featurised batch, so the DI_GRAPH_GEO_REF kernels) on two 2x1000 complexes vs the oracle
+    within north_star's fp32 bound (1e-4 relative), and the pair tensor bit-exact to its inputs."""
+    from deepinteract_amd import synth
+    from deepinteract_amd.builder import build_graph_batch
+    from deepinteract_amd.engine import GeoTEngine, PairTensorOp
+    from deepinteract_amd.weights import seeded_state_dict
+    from oracle import geot_oracle as O
+
+    sd = seeded_state_dict(0, with_head=False)
+    eng = GeoTEngine(sd, "f32")
+    chains = [c for j in range(2) for c in synth.synthetic_complex(800 + j, N_RES, N_RES)]
+    gb = build_graph_batch(chains, k=K, nbr_seeds=[11, 12, 13, 14])
+    assert gb.geo_ref
+    h, e = eng.forward(gb)
+    _, views = PairTensorOp()(h, [gb.node_off[0], gb.node_off[2]], [gb.node_off[1], gb.node_off[3]],
+                              [N_RES, N_RES], [N_RES, N_RES], hT=eng.last_hT)
+    torch.cuda.synchronize()
+    errs = {}
+    for g in (0, 3):
+        with torch.no_grad():
+            n_ref, e_ref = O.geot_forward(sd, _oracle_graph(gb, g))
+        n0, n1 = gb.node_off[g], gb.node_off[g + 1]
+        e0, e1 = gb.edge_off[g], gb.edge_off[g + 1]
+        errs[f"g{g}_node"] = rel_max(h[n0:n1].cpu().numpy(), n_ref.numpy())
+        errs[f"g{g}_edge"] = rel_max(e[e0:e1].cpu().numpy(), e_ref.numpy())
+    a, b = h[gb.node_off[0]:gb.node_off[1]], h[gb.node_off[1]:gb.node_off[2]]
+    assert torch.equal(views[0][0, :128], a.t().unsqueeze(2).expand(128, N_RES, N_RES))
+    assert torch.equal(views[0][0, 128:], b.t().unsqueeze(1).expand(128, N_RES, N_RES))
+    print("C3 fp32 errors (max-abs / max-abs ref):", {k: f"{v:.3e}" for k, v in errs.items()})
+    assert max(errs.values()) < 1e-4, errs
