@@ -839,7 +839,12 @@ using LeanPipe = WPipe<u16, Lean::NW, DI_LEAN_DBUF != 0, EL_CAP, 128>;
 // GC (DI_GRAPH_GEO_REF batches): the sequence starts at orig_msg_linear (stages 0-1, the neighbour
 // messages, are exactly zero), which then carries the orig_msg_linear bias, and (intermediate
 // layers) ends before the next layer's nbr_linear (its gathered rows are never needed).
-template <int NS, bool GC = false>
+// DI_LEAN_F16RES: the 12 ResBlock stages read the f16 copies of their matrices (EL_R16_*) and run
+// their first two layers' SiLU in packed f16 (lean_res_block)
+#ifndef DI_LEAN_F16RES
+#define DI_LEAN_F16RES 0
+#endif
+template <int NS, bool GC = false, bool FINAL = false>
 struct LeanStages {
   LeanPipe& pipe;
   const u16* W;
@@ -848,7 +853,12 @@ struct LeanStages {
   __device__ void issue(int s) {
     const int si = GC ? s + 2 : s;
     const int vo = (GC && s == 0) ? ELV_OM : EL_VEC[si];
-    pipe.issue(W + EL_ORDER[si] * BLK, EL_SIZE[si], vo >= 0 ? V + vo : nullptr, 128);
+    int off = EL_ORDER[si];
+    if constexpr (DI_LEAN_F16RES) {
+      const int r = (si >= 3 && si <= 8) ? si - 3 : ((si >= 10 && si <= 15) ? si - 4 : -1);
+      if (r >= 0) off = (FINAL ? EL_R16_FIN : EL_R16_INT) + r * MAT128;
+    }
+    pipe.issue(W + off * BLK, EL_SIZE[si], vo >= 0 ? V + vo : nullptr, 128);
   }
   __device__ const u16* next() {
     const u16* w = pipe.next();
@@ -880,8 +890,100 @@ struct LeanRow {
   bool valid;
 };
 
-template <int NS, bool GC>
-__device__ __forceinline__ void lean_res_block(Act<8> (&x)[Lean::LG], LeanStages<NS, GC>& st, int lane, int g) {
+// ---- packed-f16 SiLU (DI_LEAN_F16RES): v_cvt_pk_f16_f32, SDWA v_exp_f16 / v_rcp_f16 per half,
+// v_pk_add_f16 / v_pk_mul_f16 (7 instructions per 2 values instead of 9 with the fp32 SiLU + bf16
+// pack); tools/diag/mfma_shape_bench.hip V4
+typedef _Float16 halfx8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ uint32_t cvt_pk_f16(float a, float b) {
+  uint32_t p;
+  asm("v_cvt_pk_f16_f32 %0, %1, %2" : "=v"(p) : "v"(a), "v"(b));
+  return p;
+}
+__device__ __forceinline__ uint32_t silu2_pk_f16(float a, float b) {  // log2-unit SiLU of (a, b) as f16x2
+  uint32_t p, e, d, r, y;
+  asm("v_cvt_pk_f16_f32 %0, %1, %2" : "=v"(p) : "v"(a), "v"(b));
+  asm("v_exp_f16_sdwa %0, -%1 dst_sel:WORD_0 dst_unused:UNUSED_PAD src0_sel:WORD_0" : "=v"(e) : "v"(p));
+  asm("v_exp_f16_sdwa %0, -%1 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1" : "+v"(e) : "v"(p));
+  asm("v_pk_add_f16 %0, %1, 1.0 op_sel_hi:[1,0]" : "=v"(d) : "v"(e));
+  asm("v_rcp_f16_sdwa %0, %1 dst_sel:WORD_0 dst_unused:UNUSED_PAD src0_sel:WORD_0" : "=v"(r) : "v"(d));
+  asm("v_rcp_f16_sdwa %0, %1 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1" : "+v"(r) : "v"(d));
+  asm("v_pk_mul_f16 %0, %1, %2" : "=v"(y) : "v"(p), "v"(r));
+  return y;
+}
+template <bool SILU>
+__device__ __forceinline__ void make_op_f16(Op<BF16T, 4>& o, const Act<8>& a) {
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    uint4 u;
+    if constexpr (SILU) {
+      u.x = silu2_pk_f16(a.v[2 * s][0], a.v[2 * s][1]);
+      u.y = silu2_pk_f16(a.v[2 * s][2], a.v[2 * s][3]);
+      u.z = silu2_pk_f16(a.v[2 * s + 1][0], a.v[2 * s + 1][1]);
+      u.w = silu2_pk_f16(a.v[2 * s + 1][2], a.v[2 * s + 1][3]);
+    } else {
+      u.x = cvt_pk_f16(a.v[2 * s][0], a.v[2 * s][1]);
+      u.y = cvt_pk_f16(a.v[2 * s][2], a.v[2 * s][3]);
+      u.z = cvt_pk_f16(a.v[2 * s + 1][0], a.v[2 * s + 1][1]);
+      u.w = cvt_pk_f16(a.v[2 * s + 1][2], a.v[2 * s + 1][3]);
+    }
+    o.f[s] = __builtin_bit_cast(bf16x8, u);  // f16 bits in the operand registers
+  }
+}
+// mma_ring2 with f16 operands (f16 bits in both the LDS fragments and the packed activations)
+template <int NBO, int NS>
+__device__ __forceinline__ void mma_ring2_f16(Act<NBO>& o0, Act<NBO>& o1, const Op<BF16T, NS>& a0,
+                                              const Op<BF16T, NS>& a1, const u16* w, int lane) {
+  constexpr int G = NBO < 2 ? NBO : 2;
+  constexpr int N = NBO * NS;
+  constexpr int D = DI_MMA_DEPTH < N ? DI_MMA_DEPTH : N;
+  auto blk = [](int i) { return (i / (G * NS)) * G + (i % G); };
+  auto kst = [](int i) { return (i % (G * NS)) / G; };
+  halfx8 fr[D];
+#pragma unroll
+  for (int i = 0; i < D; ++i)
+    fr[i] = *reinterpret_cast<const halfx8*>(w + (blk(i) * NS + kst(i)) * BLK + lane * 8);
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    __builtin_amdgcn_sched_barrier(0);
+    const int bo = blk(i), s = kst(i);
+    o0.v[bo] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fr[i % D], __builtin_bit_cast(halfx8, a0.f[s]), o0.v[bo], 0, 0, 0);
+    o1.v[bo] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fr[i % D], __builtin_bit_cast(halfx8, a1.f[s]), o1.v[bo], 0, 0, 0);
+    if (i + D < N)
+      fr[i % D] = *reinterpret_cast<const halfx8*>(w + (blk(i + D) * NS + kst(i + D)) * BLK + lane * 8);
+  }
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+template <int NS, bool GC, bool FINAL>
+__device__ __forceinline__ void lean_res_block(Act<8> (&x)[Lean::LG], LeanStages<NS, GC, FINAL>& st, int lane, int g) {
+  if constexpr (DI_LEAN_F16RES && Lean::SHARED) {
+    // ResBlock in f16 operands: x -> f16; layers 0, 1: SiLU straight into packed f16 operands;
+    // layer 2: fp32 SiLU into the fp32 residual stream
+    Op<BF16T, 4> op[Lean::LG];
+#pragma unroll
+    for (int q = 0; q < Lean::LG; ++q) make_op_f16<false>(op[q], x[q]);
+#pragma unroll 1
+    for (int l = 0; l < 3; ++l) {
+      const u16* w = st.next();
+      Act<8> t[Lean::LG];
+#pragma unroll
+      for (int q = 0; q < Lean::LG; ++q) init_vec_lds(t[q], st.v(), g);
+      mma_ring2_f16<8, 4>(t[0], t[1], op[0], op[1], w, lane);
+#pragma unroll
+      for (int q = 0; q < Lean::LG; ++q) {
+        DI_FENCE();
+        if (l < 2) {
+          make_op_f16<true>(op[q], t[q]);
+          pin(op[q]);
+        } else {
+          silu2_<8, true>(t[q]);
+          add_scaled_(x[q], t[q], silu2_unit<true>());
+          pin(x[q]);
+        }
+      }
+    }
+    return;
+  }
   Op<BF16T, 4> op[Lean::LG];
 #pragma unroll
   for (int q = 0; q < Lean::LG; ++q) make_op(op[q], x[q]);
@@ -986,7 +1088,7 @@ void k_edge_lean(EdgeArgs a) {
   }
 
   LeanPipe pipe(lds);
-  LeanStages<NS, GC> st{pipe, reinterpret_cast<const u16*>(a.wmat), a.wvec, 0};
+  LeanStages<NS, GC, FINAL> st{pipe, reinterpret_cast<const u16*>(a.wmat), a.wvec, 0};
   st.issue(0);
 
   Op<BF16T, 1> gop[LG];
