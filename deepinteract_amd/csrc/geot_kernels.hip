@@ -1602,23 +1602,16 @@ __global__ __launch_bounds__(THREADS, 1) void k_node_update_ring(NodeArgs a) {
 // consumed after a DMA issue makes the wave wait for the whole in-flight weight stage (vmcnt
 // counts in order, and the compiler cannot count a runtime-length DMA loop), which exposed the
 // DMA latency at every stage.
-// DI_NODE_NW: waves (16 nodes each) per block. A C3 micro-batch has 16k nodes, so 4-wave blocks
-// give 250 blocks -- one wave per SIMD on most CUs for a latency-bound kernel; 2-wave blocks give
-// 500 (each block still stages the whole weight set once).
-#ifndef DI_NODE_NW
-#define DI_NODE_NW 4
-#endif
-constexpr int NODE_NW = DI_NODE_NW;
 template <class DT, bool FINAL>
-__global__ __launch_bounds__(64 * NODE_NW, 2) void k_node_layer(NodeArgs a) {
+__global__ __launch_bounds__(THREADS, 2) void k_node_layer(NodeArgs a) {
   using T = typename DT::T;
   DI_GEOT_ENTRY();
   constexpr bool FAST = DT::kBF16;
   constexpr bool DB = DT::kBF16;
-  using Pipe = WPipe<T, NODE_NW, DB, MAT128, 128>;
+  using Pipe = WPipe<T, WAVES, DB, MAT128, 128>;
   __shared__ __attribute__((aligned(16))) char lds[(DB ? 2 : 1) * Pipe::SLOT_BYTES];
   const int lane = lane_id(), g = lane >> 4;
-  const int r = row_id<NODE_NW>();
+  const int r = row_id<WAVES>();
   const bool valid = r < a.Nt;
   const int v = valid ? r : a.Nt - 1;
   const T* W = reinterpret_cast<const T*>(a.wmat);
@@ -1880,7 +1873,7 @@ extern "C" int di_node_layer(const di_graph* g, di_dtype dt, int final_layer, co
   if (!final_layer && !qkv_out) return DI_EINVAL;
   NodeArgs a{g->num_nodes, nullptr, hT_out, g->src, g->in_ptr, alpha, h_in, qkv, wmat, wvec, h_out, qkv_out};
   hipStream_t s = (hipStream_t)stream;
-  dim3 grid(grid_rows(a.Nt, ROWS_PER_WAVE * NODE_NW)), block(64 * NODE_NW);
+  dim3 grid(grid_rows(a.Nt)), block(THREADS);
   if (dt == DI_BF16) {
     if (final_layer) hipLaunchKernelGGL((k_node_layer<BF16T, true>), grid, block, 0, s, a);
     else hipLaunchKernelGGL((k_node_layer<BF16T, false>), grid, block, 0, s, a);

@@ -39,8 +39,6 @@ VARIANTS = {
     "pst_plain": ["DI_PAIR_STORE_BESIDE=0"],
     "edge_nt": ["DI_EDGE_ROW_NT=1"],
     "f16res": ["DI_LEAN_F16RES=1"],
-    "node_nw2": ["DI_NODE_NW=2"],
-    "node_nw1": ["DI_NODE_NW=1"],
     "init_d2": ["DI_INIT_DBUF=1", "DI_INIT_WPE=2"],
     "init_nw8d": ["DI_INIT_NW=8", "DI_INIT_DBUF=1", "DI_INIT_WPE=2"],
     "init_nw8s": ["DI_INIT_NW=8", "DI_INIT_DBUF=0", "DI_INIT_WPE=3"],
