@@ -201,19 +201,13 @@ __global__ __launch_bounds__(THREADS) void k_node_embed(EmbedArgs a) {
 #ifndef DI_INIT_WPE
 #define DI_INIT_WPE 3
 #endif
-#ifndef DI_INIT_NW
-#define DI_INIT_NW 4
-#endif
 template <class DT>
 struct InitGeo : Geo<DT> {
   static constexpr bool DBUF = DT::kBF16 && DI_INIT_DBUF;
   static constexpr int WPE = DT::kBF16 ? DI_INIT_WPE : 2;
-  static constexpr int NW = DT::kBF16 ? DI_INIT_NW : Geo<DT>::NW;  // waves per block
-  static constexpr int THREADS = 64 * NW;
-  static constexpr int ROWS = ROWS_PER_WAVE * NW;
 };
 template <class DT, bool GC>
-__global__ __attribute__((amdgpu_flat_work_group_size(1, 64 * (DT::kBF16 ? DI_INIT_NW : DI_GEO_NW)),
+__global__ __attribute__((amdgpu_flat_work_group_size(1, 64 * DI_GEO_NW),
                           amdgpu_waves_per_eu(InitGeo<DT>::WPE, InitGeo<DT>::WPE)))
 void k_init_edge(InitArgs a) {
   using T = typename DT::T;

@@ -40,9 +40,6 @@ VARIANTS = {
     "edge_nt": ["DI_EDGE_ROW_NT=1"],
     "f16res": ["DI_LEAN_F16RES=1"],
     "init_d2": ["DI_INIT_DBUF=1", "DI_INIT_WPE=2"],
-    "init_nw8d": ["DI_INIT_NW=8", "DI_INIT_DBUF=1", "DI_INIT_WPE=2"],
-    "init_nw8s": ["DI_INIT_NW=8", "DI_INIT_DBUF=0", "DI_INIT_WPE=3"],
-    "init_nw12s": ["DI_INIT_NW=12", "DI_INIT_DBUF=0", "DI_INIT_WPE=3"],
     "init_s4": ["DI_INIT_DBUF=0", "DI_INIT_WPE=4"],
     "g1s4": ["DI_LEAN_G=1", "DI_LEAN_NW=4", "DI_LEAN_WPE=4", "DI_LEAN_VGPR=64", "DI_LEAN_DBUF=0", "DI_MMA_DEPTH=5"],
     "g1s3": ["DI_LEAN_G=1", "DI_LEAN_NW=4", "DI_LEAN_WPE=3", "DI_LEAN_VGPR=80", "DI_LEAN_DBUF=0", "DI_MMA_DEPTH=6"],
