@@ -288,6 +288,8 @@ def main():
     ap.add_argument("--kernel-events", default="all", choices=["all", "dominant"],
                     help="HIP events around every launch in the timed region (all) or only around the "
                          "pair-tensor kernel, the GeoT kernels timed in one untimed step after it")
+    ap.add_argument("--geot-streams", type=int, default=1, choices=[1, 2],
+                    help="GeoT streams (2: micro-batches alternate, needs --slots >= 3)")
     ap.add_argument("--slots", type=int, default=2, choices=[2, 3, 4],
                     help="GeoT workspace slots when overlapped (2: GeoT of m+1 waits for the pair tensor of m-1; "
                          "3 / 4 measured equal within noise: 7327-7377 / 7305 vs 7292-7435)")
@@ -399,10 +401,17 @@ def main():
     else:
         s_geot = torch.cuda.current_stream(dev)
         s_pair = torch.cuda.Stream(dev) if args.overlap else s_geot
+    # --geot-streams 2: micro-batches alternate between two GeoT streams, so the kernels of m+1 fill
+    # the tails, launch gaps and latency-bound node layers of m (independent micro-batches)
+    geot_streams = [s_geot] + [torch.cuda.Stream(dev) for _ in range(args.geot_streams - 1)]
+    embed_streams = [eng.embed_stream] + [torch.cuda.Stream(dev) if eng.embed_stream is not None else None
+                                          for _ in range(args.geot_streams - 1)]
     pair_only_inputs = {}  # --only pair: each slot's GeoT outputs, computed once in the warm-up
     # workspace slots: GeoT of micro-batch m writes slot m % slots while the pair tensor of m-1 reads
     # slot (m-1) % slots; with 3+ slots GeoT m+1 never waits for the pair tensor of m-1 to drain
     n_slots = args.slots if args.overlap else 1
+    if args.geot_streams > 1 and n_slots < 4:
+        raise SystemExit("--geot-streams 2 needs --slots 4 (two GeoT micro-batches + the pair tensor's in flight)")
     done = [None] * n_slots  # per workspace slot: event after the pair tensor that last read it
 
     def launch_pair(h, hT, ready, slot, after=None, events=None):
@@ -427,9 +436,11 @@ def main():
         for m, gb in enumerate(mbs):
             slot = m % n_slots
             after = torch.cuda.Event() if args.overlap == 2 else None
-            with torch.cuda.stream(s_geot):
+            sg = geot_streams[m % len(geot_streams)]
+            eng.embed_stream = embed_streams[m % len(geot_streams)]
+            with torch.cuda.stream(sg):
                 if done[slot] is not None:
-                    s_geot.wait_event(done[slot])
+                    sg.wait_event(done[slot])
                 if args.only == "pair" and slot in pair_only_inputs:
                     h, hT = pair_only_inputs[slot]
                 else:
@@ -438,7 +449,7 @@ def main():
                     if args.only == "pair":
                         pair_only_inputs[slot] = (h, hT)
                 ready = torch.cuda.Event()
-                ready.record(s_geot)
+                ready.record(sg)
             if args.only == "geot":
                 continue
             if args.overlap == 2:
@@ -529,6 +540,7 @@ def main():
                    + f"; node layer {args.node_kernel}"
                    + ("; node embedding on a side stream" if args.embed_stream else "")
                    + (f"; {args.slots} workspace slots" if args.overlap else "")
+                   + (f"; {args.geot_streams} GeoT streams" if args.geot_streams > 1 else "")
                    + ("" if args.kernel_events == "all" else "; GeoT kernel events from an untimed step")
                    + (f", pace {args.pair_pace}" if args.pair_pace else "")
                    + f"; edge-layer kernel {['k_edge_layer', 'k_edge_lean'][edge_kernel] if args.dtype == 'bf16' else 'k_edge_layer (f32)'}"},
