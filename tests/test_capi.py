@@ -45,6 +45,20 @@ def test_invalid_arguments_rejected_without_gpu():
                                 None, None, None) == -1
 
 
+def test_geo_ref_fn_contract_without_gpu():
+    """Fn rows may be omitted (NULL) only for DI_GRAPH_GEO_REF batches: without the flag the
+    kernels need them and the entry points refuse NULL before any launch (dummy non-NULL
+    pointers are never dereferenced on these paths)."""
+    import ctypes
+    lib = _lib.load()
+    p = ctypes.c_void_p(16)
+    g = _lib.DiGraph(8, 16, 16, 16, 16, 16, 16, 0)
+    assert lib.di_init_edge(ctypes.byref(g), _lib.DI_BF16, p, p, p, p, p, p, None, None) == -1
+    assert lib.di_edge_layer(ctypes.byref(g), _lib.DI_BF16, 0, p, p, None, p, p, p, p, p, p, None) == -1
+    assert lib.di_edge_layer(ctypes.byref(g), _lib.DI_BF16, 0, p, p, p, p, p, p, p, p, None, None) == -1
+    assert _lib.DI_GRAPH_GEO_REF == 1
+
+
 def test_head_prologue_work_bytes():
     lib = _lib.load()
     # per (complex, channel): a', b', e^a', e^b' fp32 tables + one int32 flag
