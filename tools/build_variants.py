@@ -37,6 +37,7 @@ VARIANTS = {
     "lean4g2ns": ["DI_LEAN_NW=4", "DI_LEAN_WPE=2", "DI_LEAN_VGPR=120", "DI_LEAN_G=2", "DI_LEAN_SHARE=0"],
     "lean4g2d4": ["DI_LEAN_NW=4", "DI_LEAN_WPE=2", "DI_LEAN_VGPR=120", "DI_LEAN_G=2", "DI_MMA_DEPTH=4"],
     "pst_plain": ["DI_PAIR_STORE_BESIDE=0"],
+    "pst_ntsc0": ["DI_PAIR_STORE_BESIDE=3"],
     "edge_nt": ["DI_EDGE_ROW_NT=1"],
     "f16res": ["DI_LEAN_F16RES=1"],
     "init_d2": ["DI_INIT_DBUF=1", "DI_INIT_WPE=2"],
