@@ -38,12 +38,15 @@ EDGE_MAC = {"init_edge": 129_024, "edge_layer": 456_656, "edge_layer_final": 374
 H = 128
 
 
-# MACs the bf16 grouped kernels actually issue on MFMA per edge (16x16x32 MFMAs per 16-edge tile x
-# 8192 / 16), by DI_GRAPH_GEO_REF: the reference-equivalent rates above count the reference's work
-# (incl. the neighbour-message branch that is exactly zero for reference-featurised batches and the
-# nbr_linear the reference applies to 4 gathered rows per edge); these count what runs
+# MACs the GeoT kernels actually issue on MFMA per edge (packed 16x32 weight blocks x 16 rows per
+# 16-edge tile / 16 = 512 MAC per block and edge; the same stage sequence in bf16 k_edge_lean and
+# fp32 k_edge_layer), by DI_GRAPH_GEO_REF: the reference-equivalent rates above count the
+# reference's work (incl. the neighbour-message branch that is exactly zero for reference-featurised
+# batches and the nbr_linear the reference applies to 4 gathered rows per edge); these count what runs
 EXEC_EDGE_MAC = {True: {"init_edge": 65_536, "edge_layer": 348_160, "edge_layer_final": 266_240},
                  False: {"init_edge": 131_072, "edge_layer": 428_032, "edge_layer_final": 329_728}}
+# node kernels issue the node_in_embedding on 128 (113 zero-padded) input columns
+EXEC_NODE_EMBED_MAC = 128 * 128 + 3 * 128 * 128
 
 
 def node_mac(kind):
@@ -73,6 +76,18 @@ def algorithmic_flops_per_complex(n1, n2, k, layers=2):
     for n in (n1, n2):
         e = n * k
         f += e * (129_024 + (layers - 1) * 456_656 + 374_736) + n * (113 * H + layers * (3 * H * H + H * H + 2 * H * 2 * H))
+    return 2.0 * f
+
+
+def executed_flops_per_complex(n1, n2, k, layers=2, geo_ref=True):
+    """FLOPs the kernels issue on MFMA per complex (EXEC_EDGE_MAC / EXEC_NODE_EMBED_MAC; node layers
+    as node_mac): the executed counterpart of algorithmic_flops_per_complex."""
+    m = EXEC_EDGE_MAC[bool(geo_ref)]
+    f = 0
+    for n in (n1, n2):
+        e = n * k
+        f += e * (m["init_edge"] + (layers - 1) * m["edge_layer"] + m["edge_layer_final"])
+        f += n * (EXEC_NODE_EMBED_MAC + (layers - 1) * node_mac("node_layer") + node_mac("node_layer_final"))
     return 2.0 * f
 
 
@@ -242,6 +257,181 @@ def allgather_record(ws, rank, complexes, n_res, k, dev, reps=3):
             "collective": "all_gather_into_tensor (RCCL), real contact maps tiled to the metric's size"}
 
 
+class Schedule:
+    """The timed unit's schedule over resident micro-batches: GeoT of micro-batch m (compute-bound,
+    stream A) overlapped with the pair-tensor stores of m-1 (HBM-bound, stream B); workspace slots
+    carry the node features between them (slot m % slots).
+
+    overlap 0: one stream; 1: pair tensor of m-1 beside GeoT of m; 2: as 1, the pair tensor started
+    once InitEdge of m has been issued."""
+
+    def __init__(self, eng, pair, mbs, h1r, h2r, l1, l2, pair_buf, s_geot, s_pair, overlap, slots=2,
+                 geot_streams=1, only=None):
+        self.eng, self.pair, self.mbs = eng, pair, mbs
+        self.h1r, self.h2r, self.l1, self.l2, self.pair_buf = h1r, h2r, l1, l2, pair_buf
+        self.s_pair, self.overlap, self.only = s_pair, overlap, only
+        self.n_slots = slots if overlap else 1
+        dev = eng.device
+        self.geot_streams = [s_geot] + [torch.cuda.Stream(dev) for _ in range(geot_streams - 1)]
+        self.embed_streams = [eng.embed_stream] + [torch.cuda.Stream(dev) if eng.embed_stream is not None else None
+                                                   for _ in range(geot_streams - 1)]
+        if geot_streams > 1 and self.n_slots < 4:
+            raise SystemExit("--geot-streams 2 needs --slots 4 (two GeoT micro-batches + the pair tensor's in flight)")
+        self.done = [None] * self.n_slots  # per slot: event after the pair tensor that last read it
+        self.pair_only_inputs = {}         # --only pair: each slot's GeoT outputs, computed in the warm-up
+
+    def _launch_pair(self, h, hT, ready, slot, after=None, events=None):
+        with torch.cuda.stream(self.s_pair):
+            self.s_pair.wait_event(ready)
+            if after is not None:
+                self.s_pair.wait_event(after)
+            self.pair(h, self.h1r, self.h2r, self.l1, self.l2, out=self.pair_buf, events=events, hT=hT)
+            ev = torch.cuda.Event()
+            ev.record(self.s_pair)
+            self.done[slot] = ev
+
+    def step(self, events=None, geot_events="same"):
+        if geot_events == "same":
+            geot_events = events
+        eng, prev = self.eng, None
+        for m, gb in enumerate(self.mbs):
+            slot = m % self.n_slots
+            after = torch.cuda.Event() if self.overlap == 2 else None
+            sg = self.geot_streams[m % len(self.geot_streams)]
+            eng.embed_stream = self.embed_streams[m % len(self.geot_streams)]
+            with torch.cuda.stream(sg):
+                if self.done[slot] is not None:
+                    sg.wait_event(self.done[slot])
+                if self.only == "pair" and slot in self.pair_only_inputs:
+                    h, hT = self.pair_only_inputs[slot]
+                else:
+                    h, _ = eng.forward(gb, clone=False, events=geot_events, slot=slot, after_init=after)
+                    hT = eng.last_hT
+                    if self.only == "pair":
+                        self.pair_only_inputs[slot] = (h, hT)
+                ready = torch.cuda.Event()
+                ready.record(sg)
+            if self.only == "geot":
+                continue
+            if self.overlap == 2:
+                if prev is not None:
+                    self._launch_pair(*prev, after=after, events=events)
+                prev = (h, hT, ready, slot)
+            else:
+                self._launch_pair(h, hT, ready, slot, events=events)
+        if prev is not None:
+            self._launch_pair(*prev, events=events)
+
+    def timed(self, steps, warmup, ws=1, kernel_events="all"):
+        """(elapsed seconds of `steps` steps, bracketed by barrier + synchronize, max over ranks;
+        per-kernel HIP event pairs recorded inside the timed region)."""
+        for _ in range(warmup):
+            self.step()
+        events = {}
+        barrier(ws)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            # kernel_events "dominant": only the pair-tensor kernel is bracketed by HIP events inside
+            # the timed region; the GeoT kernels' event pairs are collected in one untimed step after
+            self.step(events, events if kernel_events == "all" else None)
+        torch.cuda.synchronize()
+        barrier(ws)
+        elapsed = max_over_ranks(ws, time.perf_counter() - t0)
+        if kernel_events != "all":
+            self.step(None, events)
+            torch.cuda.synchronize()
+        return elapsed, events
+
+
+def kernel_table(events, nodes, edges, l1l2, esz, dtype, geo_ref):
+    """Per-kernel average duration (HIP events on the launch stream), reference-equivalent TFLOP/s
+    (SURVEY §8d MACs), executed TFLOP/s (EXEC_EDGE_MAC) and GB/s of the byte-bound kernels."""
+    kern = {}
+    for name, pairs in events.items():
+        ms = [s.elapsed_time(e) for s, e in pairs]
+        avg_s = float(np.mean(ms)) / 1e3
+        flops, byts = kernel_units(name, nodes, edges, l1l2, esz)
+        rec = {"launches": len(ms), "avg_us": avg_s * 1e6, "total_ms": float(np.sum(ms))}
+        if flops is not None:
+            rec["tflops"] = flops / avg_s / 1e12
+            if name in EXEC_EDGE_MAC[True]:
+                rec["exec_tflops"] = 2.0 * EXEC_EDGE_MAC[bool(geo_ref)][name] * edges / avg_s / 1e12
+                rec["exec_frac_of_peak"] = rec["exec_tflops"] / MFMA_PEAK_TFLOPS[dtype]
+        if byts is not None:
+            rec["gbs"] = byts / avg_s / 1e9
+        kern[name] = rec
+    return kern
+
+
+def roofline_of(kern, dtype, traffic=None, mfma_only=False):
+    """Roofline of the dominant kernel (largest total time; mfma_only: among the GeoT kernels).
+    MFMA-bound kernels report executed FLOPs (what the MFMA pipe runs) with the reference-equivalent
+    rate beside it."""
+    cands = {n: r for n, r in kern.items() if not mfma_only or "tflops" in r}
+    dom = max(cands, key=lambda n: cands[n]["total_ms"])
+    d = kern[dom]
+    if "tflops" in d:
+        ach = d.get("exec_tflops", d["tflops"])
+        roof = {"kernel": dom, "bound": "mfma", "achieved": round(ach, 2), "peak": MFMA_PEAK_TFLOPS[dtype],
+                "unit": "TFLOP/s", "flops": "executed" if "exec_tflops" in d else "reference-equivalent",
+                "reference_equivalent_tflops": round(d["tflops"], 2)}
+    else:
+        roof = {"kernel": dom, "bound": "hbm", "achieved": round(d["gbs"], 1), "peak": HBM_PEAK_GBS, "unit": "GB/s"}
+    roof["frac"] = round(roof["achieved"] / roof["peak"], 4)
+    roof["traffic"] = traffic
+    return roof
+
+
+def rounded(kern):
+    return {n: {kk: round(v, 4) if isinstance(v, float) else v for kk, v in r.items()} for n, r in kern.items()}
+
+
+def make_pair(dev, args):
+    from deepinteract_amd.engine import PairTensorOp
+    if args.pair_cus:
+        return PairTensorOp(dev, kernel=args.pair_kernel, blocks=args.pair_cus, waves_per_block=8)
+    return PairTensorOp(dev, kernel=args.pair_kernel, blocks=args.pair_blocks, waves_per_block=args.pair_waves,
+                        beside=bool(args.pair_beside))
+
+
+def sub_record(what, dtype, geo_ref, complexes, pool_gb, P, M, n_res, k, args, dev, sd, cfg, s_geot, s_pair,
+               steps=3, warmup=1):
+    """Supplementary C3 line outside the metric: the same overlapped schedule on `complexes`
+    complexes in `dtype`, with DI_GRAPH_GEO_REF set or cleared on every batch."""
+    from deepinteract_amd.engine import GeoTEngine
+    from deepinteract_amd.graph import select_graphs
+    eng = GeoTEngine(sd, dtype, cfg, device=dev)
+    eng.split_node = args.node_kernel == "split"
+    eng.embed_stream = torch.cuda.Stream(dev) if args.embed_stream else None
+    mbs = [select_graphs(pool_gb, [2 * ((m * M + j) % P) + s for j in range(M) for s in (0, 1)]).with_geo_ref(geo_ref)
+           for m in range(complexes // M)]
+    gb0 = mbs[0]
+    h1r = [gb0.node_off[2 * j] for j in range(M)]
+    h2r = [gb0.node_off[2 * j + 1] for j in range(M)]
+    tdt = torch.bfloat16 if dtype == "bf16" else torch.float32
+    esz = 2 if dtype == "bf16" else 4
+    pair_buf = torch.empty(M * 2 * H * n_res * n_res, dtype=tdt, device=dev)
+    sch = Schedule(eng, make_pair(dev, args), mbs, h1r, h2r, [n_res] * M, [n_res] * M, pair_buf, s_geot, s_pair,
+                   args.overlap, args.slots)
+    elapsed, events = sch.timed(steps, warmup)
+    value = complexes * steps / elapsed
+    kern = kernel_table(events, gb0.num_nodes, gb0.num_edges, M * 2 * H * n_res * n_res * esz, esz, dtype, geo_ref)
+    flops_c = algorithmic_flops_per_complex(n_res, n_res, k, args.layers)
+    xflops_c = executed_flops_per_complex(n_res, n_res, k, args.layers, geo_ref)
+    out = {"what": what, "value": round(value, 2), "unit": "complexes/s", "dtype": dtype,
+           "geo_ref": bool(geo_ref), "complexes_per_step": complexes, "steps": steps, "warmup": warmup,
+           "ms_per_step": round(elapsed / steps * 1e3, 3),
+           "mfma_frac_of_peak": round(flops_c * value / (MFMA_PEAK_TFLOPS[dtype] * 1e12), 4),
+           "mfma_frac_of_peak_executed": round(xflops_c * value / (MFMA_PEAK_TFLOPS[dtype] * 1e12), 4),
+           "hbm_frac_of_peak": round(algorithmic_bytes_per_complex(n_res, n_res, k, esz) * value / (HBM_PEAK_GBS * 1e9), 4),
+           "roofline": roofline_of(kern, dtype), "roofline_geot": roofline_of(kern, dtype, mfma_only=True),
+           "kernels": rounded(kern)}
+    del pair_buf, mbs, sch, eng
+    torch.cuda.empty_cache()
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -256,17 +446,18 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=20)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-prologue", action="store_true", help="skip the supplementary fused-head-prologue line")
+    ap.add_argument("--no-sub", action="store_true",
+                    help="skip the supplementary fp32 and general-path (geo_ref off) C3 sub-records")
     ap.add_argument("--pair-cus", type=int, default=0,
                     help="K > 0: pair tensor on a CU-masked stream of K dedicated CUs (K blocks x 8 waves), "
                          "GeoT on the other CUs (needs --overlap 1)")
     ap.add_argument("--cu-layout", default="stride", choices=["stride", "contig"])
-    ap.add_argument("--pair-kernel", default=None, choices=["rows", "vector", "rows_bounded"],
-                    help="aligned pair-tensor kernel (default: rows alone, rows_bounded in 2-wave blocks "
-                         "beside GeoT)")
+    ap.add_argument("--pair-kernel", default="auto", choices=["auto", "lines", "rows", "vector"],
+                    help="pair-tensor kernel (auto: whole-line stores for 128-B aligned planes)")
     ap.add_argument("--pair-blocks", type=int, default=0)
-    ap.add_argument("--pair-waves", type=int, default=0)
-    ap.add_argument("--pair-pace", type=int, default=None,
-                    help="store-rate pacing of the pair kernel: s_sleep(1) per row / vector trip")
+    ap.add_argument("--pair-waves", type=int, default=0, help="waves per pair block (default: 2 beside GeoT, 4 alone)")
+    ap.add_argument("--pair-beside", type=int, default=None, choices=[0, 1],
+                    help="bounded store queue + non-temporal stores (default: 1 when overlapped)")
     ap.add_argument("--overlap", type=int, default=1, choices=[0, 1, 2],
                     help="0: one stream; 1: pair tensor of micro-batch m-1 on its own stream beside GeoT of m; "
                          "2: as 1, started after InitEdge of m")
@@ -276,26 +467,22 @@ def main():
     ap.add_argument("--layers", type=int, default=None, help="GeoT layers (default 2; c5: 4)")
     ap.add_argument("--node-limit", type=int, default=None,
                     help="max_num_graph_nodes of the synthetic model (default 2304; c5: 4096)")
-    ap.add_argument("--edge-kernel", type=int, default=None, choices=[0, 1],
-                    help="bf16 edge-layer kernel (di_edge_config): 0 two 4-wave blocks per CU, 1 grouped/lean form")
     ap.add_argument("--node-kernel", default=None, choices=["split", "fused"],
-                    help="node layer as di_node_aggregate + di_node_update (split; faster alone: 48 vs 68 us "
-                         "per micro-batch) or one di_node_layer (fused; faster beside the pair stream: 91 vs "
-                         "109 us). Default: fused when overlapped, split otherwise")
+                    help="node layer as di_node_aggregate + di_node_update (split) or one di_node_layer (fused). "
+                         "Default: fused when overlapped, split otherwise")
     ap.add_argument("--embed-stream", type=int, default=None, choices=[0, 1],
-                    help="1: node embedding on a side stream, concurrent with InitEdge (default when "
-                         "overlapped: 7636-7692 vs 7431-7558 complexes/s)")
+                    help="1: node embedding on a side stream, concurrent with InitEdge (default when overlapped)")
     ap.add_argument("--kernel-events", default="all", choices=["all", "dominant"],
                     help="HIP events around every launch in the timed region (all) or only around the "
                          "pair-tensor kernel, the GeoT kernels timed in one untimed step after it")
     ap.add_argument("--geot-streams", type=int, default=1, choices=[1, 2],
-                    help="GeoT streams (2: micro-batches alternate, needs --slots >= 3)")
-    ap.add_argument("--slots", type=int, default=2, choices=[2, 3, 4],
-                    help="GeoT workspace slots when overlapped (2: GeoT of m+1 waits for the pair tensor of m-1; "
-                         "3 / 4 measured equal within noise: 7327-7377 / 7305 vs 7292-7435)")
+                    help="GeoT streams (2: micro-batches alternate, needs --slots 4)")
+    ap.add_argument("--slots", type=int, default=2, choices=[2, 3, 4], help="GeoT workspace slots when overlapped")
     ap.add_argument("--only", default=None, choices=["geot", "pair"],
                     help="diagnostic (not the metric): run only the GeoT stream or only the pair-tensor stream")
-    ap.add_argument("--lib", default=None, help="tuning: a launch-shape variant of the HIP library "
+    ap.add_argument("--geo-ref", type=int, default=1, choices=[0, 1],
+                    help="0: clear DI_GRAPH_GEO_REF on every batch (the general path; diagnostic)")
+    ap.add_argument("--lib", default=None, help="tuning: a variant build of the HIP library "
                                                  "(deepinteract_amd.build.build_variant)")
     args = ap.parse_args()
     if args.lib:
@@ -314,48 +501,38 @@ def main():
         if args.micro_batch == ap.get_default("micro_batch"):
             args.micro_batch = 2
         args.pool = min(args.pool, 2)
-        args.no_cpu = args.no_prologue = True
+        args.no_cpu = args.no_prologue = args.no_sub = True
     args.layers = args.layers or 2
     args.node_limit = args.node_limit or 2304
-
-    if args.pair_kernel is None:
-        args.pair_kernel = "rows_bounded" if args.overlap and not args.pair_cus else "rows"
-    if args.pair_kernel == "rows_bounded" and not args.pair_waves:
-        args.pair_waves = 2  # one 2-wave block per CU beside GeoT (4-wave blocks starve InitEdge)
+    if args.pair_beside is None:
+        args.pair_beside = 1 if args.overlap and not args.pair_cus else 0
+    if not args.pair_waves:
+        args.pair_waves = 2 if args.pair_beside else 4  # 4-wave blocks beside GeoT starve InitEdge
+    if args.node_kernel is None:
+        args.node_kernel = "fused" if args.overlap else "split"
+    if args.embed_stream is None:
+        args.embed_stream = 1 if args.overlap else 0
     ws, rank, local = dist_setup()
     dev = torch.device("cuda", local)
     from deepinteract_amd import synth
     from deepinteract_amd.builder import build_graph_batch
-    from deepinteract_amd.engine import GeoTEngine, PairTensorOp
+    from deepinteract_amd.config import GeoTConfig
+    from deepinteract_amd.engine import GeoTEngine
     from deepinteract_amd.graph import select_graphs
     from deepinteract_amd.weights import seeded_state_dict
 
     n_res, k, M = args.residues, args.knn, args.micro_batch
     assert args.complexes % M == 0
-    from deepinteract_amd.config import GeoTConfig
     cfg = GeoTConfig(num_gnn_layers=args.layers, knn=k, node_count_limit=args.node_limit)
     sd = seeded_state_dict(0, cfg, with_head=False)
     eng = GeoTEngine(sd, args.dtype, cfg, device=dev)
-    if args.edge_kernel is not None:
-        _lib_check = eng.lib.di_edge_config(args.edge_kernel)
-        if _lib_check < 0:
-            raise SystemExit(f"di_edge_config({args.edge_kernel}) failed")
-    edge_kernel = eng.lib.di_edge_config(-1)
-    if args.node_kernel is None:
-        args.node_kernel = "fused" if args.overlap else "split"
     eng.split_node = args.node_kernel == "split"
-    if args.embed_stream is None:
-        args.embed_stream = 1 if args.overlap else 0
     if args.embed_stream:
         eng.embed_stream = torch.cuda.Stream(dev)
     num_cus = torch.cuda.get_device_properties(dev).multi_processor_count
-    if args.pair_cus:
-        if not args.overlap:
-            raise SystemExit("--pair-cus needs --overlap 1 or 2")
-        pair = PairTensorOp(dev, blocks=args.pair_cus, waves_per_block=8, kernel=args.pair_kernel)
-    else:
-        pair = PairTensorOp(dev, blocks=args.pair_blocks, waves_per_block=args.pair_waves, kernel=args.pair_kernel,
-                            pace=args.pair_pace)
+    if args.pair_cus and not args.overlap:
+        raise SystemExit("--pair-cus needs --overlap 1 or 2")
+    pair = make_pair(dev, args)
 
     # ---- inputs: a pool of distinct complexes built on the device (kNN + features + ids) ----
     P = min(args.pool, args.complexes)
@@ -373,7 +550,7 @@ def main():
     for _ in range(2):
         torch.cuda.synchronize()
         tb = time.perf_counter()
-        pool_gb = build_graph_batch([ch for pair in pool for ch in pair], k=k, device=dev,
+        pool_gb = build_graph_batch([ch for pair_ in pool for ch in pair_], k=k, device=dev,
                                     node_count_limit=args.node_limit,
                                     nbr_seeds=[2 * (1000 * rank + c) + s + 1 for c in range(P) for s in (0, 1)])
         torch.cuda.synchronize()
@@ -383,7 +560,8 @@ def main():
     n_mb = args.complexes // M
     mbs = [select_graphs(pool_gb, [2 * ((m * M + j) % P) + s for j in range(M) for s in (0, 1)])
            for m in range(n_mb)]
-    del pool_gb
+    if not args.geo_ref:
+        mbs = [gb.with_geo_ref(False) for gb in mbs]
     gb0 = mbs[0]
     h1r = [gb0.node_off[2 * j] for j in range(M)]
     h2r = [gb0.node_off[2 * j + 1] for j in range(M)]
@@ -401,124 +579,30 @@ def main():
     else:
         s_geot = torch.cuda.current_stream(dev)
         s_pair = torch.cuda.Stream(dev) if args.overlap else s_geot
-    # --geot-streams 2: micro-batches alternate between two GeoT streams, so the kernels of m+1 fill
-    # the tails, launch gaps and latency-bound node layers of m (independent micro-batches)
-    geot_streams = [s_geot] + [torch.cuda.Stream(dev) for _ in range(args.geot_streams - 1)]
-    embed_streams = [eng.embed_stream] + [torch.cuda.Stream(dev) if eng.embed_stream is not None else None
-                                          for _ in range(args.geot_streams - 1)]
-    pair_only_inputs = {}  # --only pair: each slot's GeoT outputs, computed once in the warm-up
-    # workspace slots: GeoT of micro-batch m writes slot m % slots while the pair tensor of m-1 reads
-    # slot (m-1) % slots; with 3+ slots GeoT m+1 never waits for the pair tensor of m-1 to drain
-    n_slots = args.slots if args.overlap else 1
-    if args.geot_streams > 1 and n_slots < 4:
-        raise SystemExit("--geot-streams 2 needs --slots 4 (two GeoT micro-batches + the pair tensor's in flight)")
-    done = [None] * n_slots  # per workspace slot: event after the pair tensor that last read it
-
-    def launch_pair(h, hT, ready, slot, after=None, events=None):
-        with torch.cuda.stream(s_pair):
-            s_pair.wait_event(ready)
-            if after is not None:
-                s_pair.wait_event(after)
-            pair(h, h1r, h2r, l1, l2, out=pair_buf, events=events, hT=hT)
-            ev = torch.cuda.Event()
-            ev.record(s_pair)
-            done[slot] = ev
-
-    def step(events=None, geot_events="same"):
-        if geot_events == "same":
-            geot_events = events
-        # GeoT of micro-batch m (compute-bound, stream A) overlaps the pair-tensor stores of
-        # micro-batch m-1 (HBM-bound, stream B); two workspace slots carry the node features.
-        # overlap 2: the pair tensor of m-1 starts once InitEdge of m has been issued, so the
-        # store stream runs beside the edge layers (MFMA/VALU-bound), not beside the
-        # memory-heavy node-embedding / InitEdge prologue.
-        prev = None
-        for m, gb in enumerate(mbs):
-            slot = m % n_slots
-            after = torch.cuda.Event() if args.overlap == 2 else None
-            sg = geot_streams[m % len(geot_streams)]
-            eng.embed_stream = embed_streams[m % len(geot_streams)]
-            with torch.cuda.stream(sg):
-                if done[slot] is not None:
-                    sg.wait_event(done[slot])
-                if args.only == "pair" and slot in pair_only_inputs:
-                    h, hT = pair_only_inputs[slot]
-                else:
-                    h, _ = eng.forward(gb, clone=False, events=geot_events, slot=slot, after_init=after)
-                    hT = eng.last_hT
-                    if args.only == "pair":
-                        pair_only_inputs[slot] = (h, hT)
-                ready = torch.cuda.Event()
-                ready.record(sg)
-            if args.only == "geot":
-                continue
-            if args.overlap == 2:
-                if prev is not None:
-                    launch_pair(*prev, after=after, events=events)
-                prev = (h, hT, ready, slot)
-            else:
-                launch_pair(h, hT, ready, slot, events=events)
-        if prev is not None:
-            launch_pair(*prev, events=events)
-
-    for _ in range(args.warmup):
-        step()
-    events = {}
-    barrier(ws)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        # --kernel-events dominant: only the dominant (pair-tensor) kernel is bracketed by HIP
-        # events inside the timed region; the GeoT kernels' event pairs (two marker packets per
-        # launch on the GeoT stream) are collected in one untimed step after it
-        step(events, events if args.kernel_events == "all" else None)
-    torch.cuda.synchronize()
-    barrier(ws)
-    elapsed = time.perf_counter() - t0
-    elapsed = max_over_ranks(ws, elapsed)
+    sch = Schedule(eng, pair, mbs, h1r, h2r, l1, l2, pair_buf, s_geot, s_pair, args.overlap, args.slots,
+                   args.geot_streams, args.only)
+    elapsed, events = sch.timed(args.steps, args.warmup, ws, args.kernel_events)
     total = args.complexes * args.steps * ws
-    if args.kernel_events != "all":
-        step(None, events)
-        torch.cuda.synchronize()
-
-    # ---- supplementary (outside the metric): fused head prologue, contact-map all-gather ----
-    prologue = head_prologue_record(h1r, h2r, l1, l2, mbs[-1], eng, dev, tdt) if not args.no_prologue else None
-    gather = allgather_record(ws, rank, args.complexes, n_res, k, dev) if ws > 1 and args.config == "c3" else None
     value = total / elapsed
 
-    # ---- per-kernel timing (HIP events on the launch stream, inside the timed region) -------
+    # ---- supplementary (outside the metric) ------------------------------------------------
+    prologue = head_prologue_record(h1r, h2r, l1, l2, mbs[-1], eng, dev, tdt) if not args.no_prologue else None
+    gather = allgather_record(ws, rank, args.complexes, n_res, k, dev) if ws > 1 and args.config == "c3" else None
     nodes, edges = gb0.num_nodes, gb0.num_edges
     l1l2 = sum(2 * H * a * b * esz for a, b in zip(l1, l2))
-    kern = {}
-    for name, pairs in events.items():
-        ms = [s.elapsed_time(e) for s, e in pairs]
-        avg_s = float(np.mean(ms)) / 1e3
-        flops, byts = kernel_units(name, nodes, edges, l1l2, esz)
-        rec = {"launches": len(ms), "avg_us": avg_s * 1e6, "total_ms": float(np.sum(ms))}
-        if flops is not None:
-            rec["tflops"] = flops / avg_s / 1e12  # reference-equivalent (SURVEY §8d MACs)
-            if args.dtype == "bf16" and edge_kernel == 1 and name in EXEC_EDGE_MAC[True]:
-                rec["exec_tflops"] = 2.0 * EXEC_EDGE_MAC[bool(gb0.geo_ref)][name] * edges / avg_s / 1e12
-        if byts is not None:
-            rec["gbs"] = byts / avg_s / 1e9
-        kern[name] = rec
-    dom = max(kern, key=lambda n: kern[n]["total_ms"])
-    d = kern[dom]
-    if "tflops" in d:
-        roof = {"kernel": dom, "bound": "mfma", "achieved": round(d["tflops"], 2),
-                "peak": MFMA_PEAK_TFLOPS[args.dtype], "unit": "TFLOP/s"}
-    else:
-        roof = {"kernel": dom, "bound": "hbm", "achieved": round(d["gbs"], 1), "peak": HBM_PEAK_GBS, "unit": "GB/s"}
-    roof["frac"] = round(roof["achieved"] / roof["peak"], 4)
-    # the committed PMC summary was collected on the default workload (C3, micro-batch 8, bf16):
-    # any other shape reports traffic null rather than borrowing those per-launch bytes
-    pmc_shape = (args.config, M, n_res, k, args.layers, args.dtype) == ("c3", 8, 1000, 20, 2, "bf16")
-    traffic = load_pmc_traffic(dom) if pmc_shape else None
-    roof["traffic"] = traffic
+    kern = kernel_table(events, nodes, edges, l1l2, esz, args.dtype, gb0.geo_ref)
+    # the committed PMC summary was collected on the default workload (C3, micro-batch 8, bf16, the
+    # default kernels): any other shape reports traffic null rather than borrowing those bytes
+    pmc_shape = (args.config, M, n_res, k, args.layers, args.dtype, args.pair_kernel, args.geo_ref) == \
+        ("c3", 8, 1000, 20, 2, "bf16", "auto", 1)
+    roof = roofline_of(kern, args.dtype)
+    roof["traffic"] = load_pmc_traffic(roof["kernel"]) if pmc_shape else None
     bytes_c = algorithmic_bytes_per_complex(n_res, n_res, k, esz)
     hbm_frac = bytes_c * value / ws / (HBM_PEAK_GBS * 1e9)
     flops_c = algorithmic_flops_per_complex(n_res, n_res, k, args.layers)
+    xflops_c = executed_flops_per_complex(n_res, n_res, k, args.layers, gb0.geo_ref)
     mfma_frac = flops_c * value / ws / (MFMA_PEAK_TFLOPS[args.dtype] * 1e12)
+    xmfma_frac = xflops_c * value / ws / (MFMA_PEAK_TFLOPS[args.dtype] * 1e12)
 
     out = {
         "metric": METRIC if args.config == "c3" else METRIC_C5, "value": round(value, 2), "unit": "complexes/s", "n_gpus": ws,
@@ -535,21 +619,24 @@ def main():
                                "GeoT || pair-tensor (2 HIP streams, pair after InitEdge)"][args.overlap]
                    + (f"; pair on {args.pair_cus} dedicated CUs ({args.cu_layout}), GeoT on "
                       f"{num_cus - args.pair_cus}" if args.pair_cus else "")
-                   + f"; pair kernel {args.pair_kernel}"
+                   + f"; pair kernel {args.pair_kernel} ({args.pair_waves}-wave blocks"
+                   + (", bounded store queue, nt stores)" if args.pair_beside else ")")
                    + (f"; DIAGNOSTIC: {args.only} stream only (not the metric)" if args.only else "")
+                   + ("" if args.geo_ref else "; DI_GRAPH_GEO_REF cleared (general path)")
                    + f"; node layer {args.node_kernel}"
                    + ("; node embedding on a side stream" if args.embed_stream else "")
                    + (f"; {args.slots} workspace slots" if args.overlap else "")
                    + (f"; {args.geot_streams} GeoT streams" if args.geot_streams > 1 else "")
                    + ("" if args.kernel_events == "all" else "; GeoT kernel events from an untimed step")
-                   + (f", pace {args.pair_pace}" if args.pair_pace else "")
-                   + f"; edge-layer kernel {['k_edge_layer', 'k_edge_lean'][edge_kernel] if args.dtype == 'bf16' else 'k_edge_layer (f32)'}"},
+                   + f"; edge-layer kernel {'k_edge_lean' if args.dtype == 'bf16' else 'k_edge_layer (f32)'}"},
         "hbm_frac_of_peak": round(hbm_frac, 4),
         "mfma_frac_of_peak": round(mfma_frac, 4),
-        "algorithmic_per_complex": {"bytes": bytes_c, "flops": flops_c,
+        "mfma_frac_of_peak_executed": round(xmfma_frac, 4),
+        "algorithmic_per_complex": {"bytes": bytes_c, "flops": flops_c, "executed_mfma_flops": xflops_c,
                                     "mfma_peak_tflops": MFMA_PEAK_TFLOPS[args.dtype], "hbm_peak_gbs": HBM_PEAK_GBS},
         "roofline": roof,
-        "kernels": {n: {kk: round(v, 3) if isinstance(v, float) else v for kk, v in r.items()} for n, r in kern.items()},
+        "roofline_geot": roofline_of(kern, args.dtype, mfma_only=True) if any("tflops" in r for r in kern.values()) else None,
+        "kernels": rounded(kern),
         "builder": {"complexes": P, "build_s": round(t_build, 4), "ms_per_complex": round(t_build / P * 1e3, 3),
                     "cold_build_s": round(t_builds[0], 4),
                     "synth_host_s": round(t_synth, 3),
@@ -559,21 +646,37 @@ def main():
         out["head_prologue"] = prologue
     if gather is not None:
         out["contact_map_allgather"] = gather
+    if not args.no_sub and args.config == "c3" and not args.only and not args.pair_cus:
+        # supplementary C3 lines outside the metric (same schedule and kernels): the reference's
+        # precision (fp32, deepinteract_utils.py:1088) and the general path with the neighbour-edge
+        # gathers live (DI_GRAPH_GEO_REF cleared, deepinteract_modules.py:384-418)
+        del pair_buf, sch
+        torch.cuda.empty_cache()
+        out["sub_records"] = [
+            sub_record("fp32 C3 (the reference's precision), same schedule", "f32", True, 128, pool_gb, P, M,
+                       n_res, k, args, dev, sd, cfg, s_geot, s_pair),
+            sub_record("bf16 C3, general path (DI_GRAPH_GEO_REF cleared: neighbour gathers live)", "bf16", False,
+                       256, pool_gb, P, M, n_res, k, args, dev, sd, cfg, s_geot, s_pair),
+        ]
     if rank == 0 and ws == 1 and not args.no_cpu:
-        threads, logical = physical_cores()
+        # the headline at the threads this job is given on the box (OMP_NUM_THREADS: its CPU share),
+        # the protocol's one-thread-per-physical-core figure beside it (on a shared host the op-by-op
+        # DGL-style path loses to oversubscription there: 0.32 vs 1.19 complexes/s in round 2)
+        phys, logical = physical_cores()
+        omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+        threads = omp if 0 < omp < phys else phys
         cps, dt = cpu_baseline(n_res, k, args.cpu_sample, threads)
         out["cpu_baseline"] = {"value": round(cps, 4), "unit": "complexes/s", "cores": threads, "kind": "port",
                                "sample": f"{args.cpu_sample} C3 complexes (2x{n_res} res, k={k}) after 3 warm-ups, "
                                          f"oracle fp32 (DGL-style op-for-op) GeoT both chains + pair tensor, "
-                                         f"torch.inference_mode, {threads} threads = physical cores of the "
-                                         f"{logical} logical CPUs this process may use, {dt:.1f}s"}
-        omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
-        if 0 < omp < threads:
-            # the host's per-job CPU share (OMP_NUM_THREADS) on a shared box: more threads than the
-            # share can be slower; reported beside the protocol's number, not instead of it
-            cps2, dt2 = cpu_baseline(n_res, k, 5, omp, warmup=1)
-            out["cpu_baseline"]["at_job_cpu_share"] = {"threads": omp, "value": round(cps2, 4),
-                                                       "sample": f"5 complexes after 1 warm-up, {dt2:.1f}s"}
+                                         f"torch.inference_mode, {threads} threads "
+                                         + ("(OMP_NUM_THREADS, the job's CPU share)" if threads == omp else
+                                            f"= physical cores of the {logical} logical CPUs this process may use")
+                                         + f", {dt:.1f}s"}
+        if threads != phys:
+            cps2, dt2 = cpu_baseline(n_res, k, 5, phys, warmup=1)
+            out["cpu_baseline"]["at_physical_cores"] = {"threads": phys, "value": round(cps2, 4),
+                                                        "sample": f"5 complexes after 1 warm-up, {dt2:.1f}s"}
     if rank == 0:
         print(json.dumps(out), flush=True)
     if ws > 1:

@@ -33,6 +33,15 @@ class DiPairDesc(ctypes.Structure):
                 ("l1", ctypes.c_int32), ("l2", ctypes.c_int32)]
 
 
+class DiPairLaunch(ctypes.Structure):
+    _fields_ = [("kernel", ctypes.c_int32), ("blocks", ctypes.c_int32), ("waves_per_block", ctypes.c_int32),
+                ("beside", ctypes.c_int32)]
+
+
+DI_PAIR_AUTO, DI_PAIR_ROWS, DI_PAIR_VECTOR, DI_PAIR_LINES = 0, 1, 2, 3
+ABI_VERSION = 3
+
+
 _P = ctypes.c_void_p
 _I = ctypes.c_int32
 _SIGS = {
@@ -42,13 +51,11 @@ _SIGS = {
     "di_init_edge": ([ctypes.POINTER(DiGraph), _I, _P, _P, _P, _P, _P, _P, _P, _P], ctypes.c_int),
     "di_edge_layer": ([ctypes.POINTER(DiGraph), _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
                       ctypes.c_int),
-    "di_edge_config": ([_I], ctypes.c_int),
     "di_node_layer": ([ctypes.POINTER(DiGraph), _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P], ctypes.c_int),
     "di_node_aggregate": ([ctypes.POINTER(DiGraph), _I, _P, _P, _P, _P], ctypes.c_int),
     "di_node_update": ([ctypes.POINTER(DiGraph), _I, _I, _P, _P, _P, _P, _P, _P, _P, _P], ctypes.c_int),
-    "di_pair_tensor": ([_I, _P, _I, _I, _I, _I, _I, _P, _P, _I, _P, _P], ctypes.c_int),
-    "di_pair_config": ([_I, _I, _I], ctypes.c_int),
-    "di_pair_pace": ([_I], ctypes.c_int),
+    "di_pair_tensor": ([_I, _P, _I, _I, _I, _I, _I, _P, _P, _I, ctypes.POINTER(DiPairLaunch), _P, _P], ctypes.c_int),
+    "di_pair_tensor_check": ([_I, _I, _I, _I, _I, ctypes.POINTER(DiPairLaunch)], ctypes.c_int),
     "di_head_prologue": ([_I, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, ctypes.c_float, _P, _P, _P],
                          ctypes.c_int),
     "di_head_prologue_work_bytes": ([_I, _I, _I, _I], ctypes.c_int64),
@@ -79,7 +86,7 @@ def _bind(path: str):
         fn = getattr(lib, name)
         fn.argtypes = argtypes
         fn.restype = restype
-    if lib.di_abi_version() != 2:
+    if lib.di_abi_version() != ABI_VERSION:
         raise RuntimeError("deepinteract_amd ABI version mismatch")
     return lib
 

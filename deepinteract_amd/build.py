@@ -38,7 +38,31 @@ def up_to_date() -> bool:
     return all(os.path.getmtime(p) <= t for p in _deps())
 
 
-def build(force: bool = False, verbose: bool = True, defines=(), out: str | None = None) -> str:
+# Host-side AddressSanitizer + UndefinedBehaviorSanitizer build of the C ABI (argument validation,
+# descriptor / size arithmetic, launch-shape selection): every -fsanitize flag applies to the host
+# compilation only (-Xarch_host); device code is unchanged and GPU sanitizers are not used. Loaded in
+# a child process with the shared ASan runtime preloaded (tests/test_host_sanitizers.py).
+SAN_FLAGS = ["-O1", "-g", "-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fsanitize=undefined",
+             "-Xarch_host", "-fno-sanitize-recover=undefined", "-Xarch_host", "-fno-omit-frame-pointer"]
+SAN_LIB = os.path.join(LIBDIR, "asan", "libdeepinteract_amd.so")
+
+
+def asan_runtime() -> str:
+    """The shared ASan runtime of the ROCm LLVM the library is built with."""
+    cands = sorted(glob.glob("/opt/rocm/lib/llvm/lib/clang/*/lib/linux/libclang_rt.asan-x86_64.so"))
+    if not cands:
+        raise RuntimeError("libclang_rt.asan-x86_64.so not found under /opt/rocm/lib/llvm")
+    return cands[-1]
+
+
+def build_host_sanitized(force: bool = False) -> str:
+    if not force and os.path.exists(SAN_LIB) and all(os.path.getmtime(p) <= os.path.getmtime(SAN_LIB) for p in _deps()):
+        return SAN_LIB
+    return build(force=True, defines=SAN_FLAGS, out=SAN_LIB,
+                 link_flags=["-fsanitize=address", "-fsanitize=undefined", "-shared-libsan"])
+
+
+def build(force: bool = False, verbose: bool = True, defines=(), out: str | None = None, link_flags=()) -> str:
     """Build the library. ``defines``/``out`` build a tuning variant (extra -D defines, or raw
     compiler flags when an entry starts with '-') into its
     own directory, loaded with bench.py --lib <path> (launch-shape knobs compared in one GPU session)."""
@@ -59,7 +83,7 @@ def build(force: bool = False, verbose: bool = True, defines=(), out: str | None
 
     with cf.ThreadPoolExecutor(max_workers=min(8, len(_sources()))) as ex:
         objs = list(ex.map(compile_one, _sources()))
-    cmd = [HIPCC, "-shared", f"--offload-arch={ARCH}", "-o", lib_path, *objs]
+    cmd = [HIPCC, "-shared", f"--offload-arch={ARCH}", *link_flags, "-o", lib_path, *objs]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed:\n{r.stderr}")

@@ -42,6 +42,9 @@ def _node_off(sizes, device):
 _stage = {"buf": None, "event": None}
 
 
+BUILDER_MAX_NODES = 4096  # csrc/graph_builder.hip KNN_MAX_N: one chain's Cα rows staged in LDS
+
+
 def _pinned(words):
     """Reusable pinned host staging buffer of at least `words` 4-byte words (float32 view)."""
     st = _stage
@@ -85,12 +88,15 @@ def build_graph_batch(chains, k=KNN, nb=GEO_NBRHD_SIZE, seed=0, device="cuda", r
     if nb != 2:
         raise NotImplementedError("geo_nbrhd_size=2 (the reference's setting, lit_model_predict.py:156)")
     from .engine import gpu_device
-    device = gpu_device(device)
-    lib = _lib.load()
     sizes = [int(np.asarray(c["backbone"]).shape[0]) for c in chains]
     for n in sizes:
         if n > node_count_limit:
             raise IndexError(f"chain of {n} residues exceeds NODE_COUNT_LIMIT={node_count_limit}")
+        if n > BUILDER_MAX_NODES:
+            raise NotImplementedError(f"chain of {n} residues: the on-device kNN handles chains of at most "
+                                      f"{BUILDER_MAX_NODES} residues (di_knn_topk)")
+    device = gpu_device(device)
+    lib = _lib.load()
     if nbr_seeds is not None and len(nbr_seeds) != len(sizes):
         raise ValueError(f"{len(nbr_seeds)} neighbour seeds for {len(sizes)} chains")
     nt, G = int(sum(sizes)), len(sizes)
@@ -145,7 +151,7 @@ def build_graph_batch(chains, k=KNN, nb=GEO_NBRHD_SIZE, seed=0, device="cuda", r
     # k_geo_feats writes the featuriser's constant direction / orientation columns (0,0,0,0,0,0,1)
     # for every edge, so the batch carries DI_GRAPH_GEO_REF by construction (no device check)
     gb = GraphBatch(src, dst, nbr, node_f, edge_f, sizes, [n * k for n in sizes], node_count_limit=node_count_limit,
-                    in_ptr=in_ptr, node_pos=node_pos, geo_ref=True)
+                    in_ptr=in_ptr, node_pos=node_pos, _trusted_geo_ref=True)
     gb._keep = (d_all,)  # inputs referenced by in-flight launches
     if return_aux:
         return gb, {"knn_idx": idx, "knn_d2": d2}

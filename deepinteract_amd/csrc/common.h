@@ -164,19 +164,12 @@ __device__ __forceinline__ void store_row(const Act<NB>& a, T* row, int g) {
 #pragma unroll
   for (int b = 0; b < NB; ++b) st4(row + 16 * b + 4 * g, a.v[b]);
 }
-// edge-row outputs (F, Fn: 82 MB per C3 micro-batch each, re-read by the next kernel from HBM/MALL).
-// DI_EDGE_ROW_NT=1 stores them non-temporally: measured slower beside the pair stream (7108-7150 vs
-// 7438-7441 complexes/s), off
-#ifndef DI_EDGE_ROW_NT
-#define DI_EDGE_ROW_NT 0
-#endif
+// edge-row outputs (F, Fn: 82 MB per C3 micro-batch each, re-read by the next kernel from HBM/MALL)
+// keep the default store policy: non-temporal row stores measured slower beside the pair stream
+// (7108-7150 vs 7438-7441 complexes/s, round 2)
 template <int NB, typename T>
 __device__ __forceinline__ void store_edge_row(const Act<NB>& a, T* row, int g) {
-#pragma unroll
-  for (int b = 0; b < NB; ++b) {
-    if constexpr (DI_EDGE_ROW_NT) st4_nt(row + 16 * b + 4 * g, a.v[b]);
-    else st4(row + 16 * b + 4 * g, a.v[b]);
-  }
+  store_row(a, row, g);
 }
 
 // A 128-feature row held in its STORAGE format (bf16: 16 VGPRs instead of 32), for prefetching
@@ -326,49 +319,22 @@ __device__ __forceinline__ void unpack_op(Act<2 * NS>& a, const Op<BF16T, NS>& o
   }
 }
 
-// out (NBO 16-row blocks) += W (NBO x NS packed blocks, in LDS) . op (NS 32-feature k-steps)
-#ifndef DI_MMA_ORDER
-#define DI_MMA_ORDER 3
-#endif
-// DMA pump: with a weight pipe passed in, one pending LDS-DMA piece of the NEXT stage is issued
-// after every DI_DMA_PUMP MFMAs (0: the stage's pieces are issued in one burst at stage start),
-// so the issue cost of the weight stream hides between this wave's MFMAs. Measured (C3 edge
-// layer, bf16): burst 503 us, pump every 1/2/4 MFMAs 576/575/559 us (extra spills) -> off.
-#ifndef DI_DMA_PUMP
-#define DI_DMA_PUMP 0
-#endif
 constexpr int BUF_RSRC_W3 = 0x00020000;  // gfx9 raw buffer: DATA_FORMAT 32, no swizzle / stride
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* g) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(g), 0, 0x7fffffff, BUF_RSRC_W3);
 }
 
-// Pending LDS-DMA pieces of the next weight stage: 1-KiB pieces [pi, pk) of src -> dst, stepping
-// by the block's wave count (wave-uniform state).
-struct DmaPump {
-  const char* src = nullptr;
-  char* dst = nullptr;
-  int pi = 0, pk = 0, step = 1;
-  __device__ __forceinline__ void pump() {
-    if (pi < pk) {
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(buf_rsrc(src),
-                                               (__attribute__((address_space(3))) void*)(dst + pi * 1024), 16,
-                                               (threadIdx.x & 63) * 16, pi * 1024, 0, 0);
-      pi += step;
-    }
-  }
-};
-// Explicitly pipelined form (DI_MMA_ORDER 4): A fragments read DI_MMA_DEPTH MFMAs ahead of their
-// use through a register ring, with scheduling fences between steps, so at most DEPTH fragments
-// (4 VGPRs each) are live: bounds register pressure for the 4-waves-per-SIMD kernels.
-#ifndef DI_MMA_DEPTH
-#define DI_MMA_DEPTH 4
-#endif
+// A fragments read MMA_DEPTH MFMAs ahead of their use through a register ring, with scheduling
+// fences between steps, so at most MMA_DEPTH fragments (4 VGPRs each) are live: bounds register
+// pressure for the two-waves-per-SIMD kernels (the compiler otherwise hoists most of a layer's
+// ds_reads). Measured depth 3 / 6 vs 4 (C3, overlapped): 7330 / 7286 vs 7307 complexes/s (noise).
+constexpr int MMA_DEPTH = 4;
 template <int NBO, int NS>
 __device__ __forceinline__ void mma_ring(Act<NBO>& out, const Op<BF16T, NS>& op, const u16* w, int lane) {
   constexpr int G = NBO < 2 ? NBO : 2;
   constexpr int N = NBO * NS;
-  constexpr int D = DI_MMA_DEPTH < N ? DI_MMA_DEPTH : N;
+  constexpr int D = MMA_DEPTH < N ? MMA_DEPTH : N;
   // step i -> (output block, k-step), output-block-pair major
   auto blk = [](int i) { return (i / (G * NS)) * G + (i % G); };
   auto kst = [](int i) { return (i % (G * NS)) / G; };
@@ -387,43 +353,25 @@ __device__ __forceinline__ void mma_ring(Act<NBO>& out, const Op<BF16T, NS>& op,
   __builtin_amdgcn_sched_barrier(0);
 }
 
+// out (NBO 16-row blocks) += W (NBO x NS packed blocks, in LDS) . op (NS 32-feature k-steps),
+// output-block-pair major (a pair of output blocks completes early, so its epilogue can overlap)
 template <int NBO, int NS>
-__device__ __forceinline__ void mma(Act<NBO>& out, const Op<BF16T, NS>& op, const u16* w, int lane,
-                                    DmaPump* pp = nullptr) {
-  if constexpr (DI_MMA_ORDER == 4) {
-    mma_ring<NBO, NS>(out, op, w, lane);
-  } else if constexpr (DI_MMA_ORDER == 0 || DI_MMA_ORDER == 2) {  // k-step major
+__device__ __forceinline__ void mma(Act<NBO>& out, const Op<BF16T, NS>& op, const u16* w, int lane) {
+  constexpr int G = NBO < 2 ? NBO : 2;
+#pragma unroll
+  for (int b0 = 0; b0 < NBO; b0 += G) {
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
 #pragma unroll
-      for (int bo = 0; bo < NBO; ++bo) {
+      for (int bo = b0; bo < b0 + G; ++bo) {
         const bf16x8 af = *reinterpret_cast<const bf16x8*>(w + (bo * NS + s) * BLK + lane * 8);
         out.v[bo] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, op.f[s], out.v[bo], 0, 0, 0);
       }
-      if constexpr (DI_MMA_ORDER == 0)
-        __builtin_amdgcn_sched_barrier(0);  // bound the LDS fragments in flight (register pressure)
-    }
-  } else {  // output-block-pair major: blocks complete early (their epilogue can overlap)
-    constexpr int G = NBO < 2 ? NBO : 2;
-#pragma unroll
-    for (int b0 = 0; b0 < NBO; b0 += G) {
-#pragma unroll
-      for (int s = 0; s < NS; ++s) {
-#pragma unroll
-        for (int bo = b0; bo < b0 + G; ++bo) {
-          const bf16x8 af = *reinterpret_cast<const bf16x8*>(w + (bo * NS + s) * BLK + lane * 8);
-          out.v[bo] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, op.f[s], out.v[bo], 0, 0, 0);
-        }
-        if constexpr (DI_DMA_PUMP > 0)
-          if (pp && ((b0 / G) * NS + s) % (DI_DMA_PUMP < G ? 1 : DI_DMA_PUMP / G) == 0) pp->pump();
-      }
-      if constexpr (DI_MMA_ORDER == 1) __builtin_amdgcn_sched_barrier(0);
     }
   }
 }
 template <int NBO, int NS>
-__device__ __forceinline__ void mma(Act<NBO>& out, const Op<F32T, NS>& op, const float* w, int lane,
-                                    DmaPump* = nullptr) {
+__device__ __forceinline__ void mma(Act<NBO>& out, const Op<F32T, NS>& op, const float* w, int lane) {
 #pragma unroll
   for (int s = 0; s < NS; ++s)
 #pragma unroll
@@ -441,11 +389,10 @@ __device__ __forceinline__ void mma(Act<NBO>& out, const Op<F32T, NS>& op, const
 
 // convenience: out += W . a   (a has 2*NS blocks)
 template <class DT, int NBO, int NS>
-__device__ __forceinline__ void linear(Act<NBO>& out, const Act<2 * NS>& a, const typename DT::T* w, int lane,
-                                       DmaPump* pp = nullptr) {
+__device__ __forceinline__ void linear(Act<NBO>& out, const Act<2 * NS>& a, const typename DT::T* w, int lane) {
   Op<DT, NS> op;
   make_op(op, a);
-  mma<NBO, NS>(out, op, w, lane, pp);
+  mma<NBO, NS>(out, op, w, lane);
 }
 
 // ------------------------------------------------------------------ weight staging
@@ -486,15 +433,21 @@ __device__ __forceinline__ void dma_vec(float* lds, const float* g, int n512) {
 }
 
 // Weight pipeline over one (DBUF=false) or two (DBUF=true) LDS slots, each holding CAP packed
-// weight blocks plus VCAP fp32 vector elements (the stage's biases).
+// weight blocks plus VCAP fp32 vector elements (the stage's biases), for a block of NW waves.
 //   issue(W_next, n, V_next, nv) starts the DMA of the NEXT layer's weights and biases; next()
-//   waits for it (barrier, which also drains this wave's DMA: s_waitcnt vmcnt(0)) and makes it
-//   the current slot (w(), v()).
+//   waits for it (this wave's LDS-DMA via s_waitcnt vmcnt(0), every wave's via the barrier) and
+//   makes it the current slot (w(), v()).
 // With DBUF the DMA of layer i+1 runs under layer i's MFMAs; the slot it overwrites was last read
 // in layer i-1, before the barrier inside next(). Call pattern per layer:
 //     pipe.next(); pipe.issue(next layer); compute(pipe.w(), pipe.v());
+// The DMA pieces of a stage are split over the NW waves by wave index: a block launched with a
+// different wave count than NW would leave pieces unwritten (fewer waves) -- the kernels take NW
+// and their launch shape from one geometry struct (KernelGeo below), never from two constants.
 template <typename T, int NW, bool DBUF, int CAP, int VCAP = 0>
 struct WPipe {
+  static_assert(NW >= 1 && NW <= 16, "waves per block");
+  static_assert((CAP * BLK * (int)sizeof(T)) % 1024 == 0, "a stage is whole 1-KiB LDS-DMA pieces");
+  static_assert(VCAP % 128 == 0, "bias vectors are whole 512-B pieces");
   static constexpr int SLOT_BYTES = CAP * BLK * (int)sizeof(T) + VCAP * 4;
   char* base;
   int cur;
@@ -508,18 +461,8 @@ struct WPipe {
   __device__ __forceinline__ float* slot_v(int s) const {
     return reinterpret_cast<float*>(base + (DBUF ? s : 0) * SLOT_BYTES + CAP * BLK * (int)sizeof(T));
   }
-  // pumped DMA (DBUF and DI_DMA_PUMP): the next stage's pieces, issued between MFMAs
-  DmaPump dp;
-  __device__ __forceinline__ DmaPump* pump_ptr() { return (DBUF && DI_DMA_PUMP > 0) ? &dp : nullptr; }
   __device__ __forceinline__ void issue(const T* g, int nblk, const float* gv = nullptr, int nvec = 0) {
-    if constexpr (DBUF && DI_DMA_PUMP > 0) {
-      dp.src = reinterpret_cast<const char*>(g);
-      dp.dst = reinterpret_cast<char*>(slot_w(cur ^ 1));
-      dp.pi = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-      dp.pk = nblk * BLK * (int)sizeof(T) / 1024;
-      dp.step = NW;
-      if (gv) dma_vec<NW>(slot_v(cur ^ 1), gv, nvec / 128);
-    } else if constexpr (DBUF) {
+    if constexpr (DBUF) {
       dma_blocks<NW>(slot_w(cur ^ 1), g, nblk);
       if (gv) dma_vec<NW>(slot_v(cur ^ 1), gv, nvec / 128);
     } else {
@@ -531,8 +474,6 @@ struct WPipe {
   }
   __device__ __forceinline__ const T* next() {
     if constexpr (DBUF) {
-      if constexpr (DI_DMA_PUMP > 0)
-        while (dp.pi < dp.pk) dp.pump();  // pieces the stage's MFMAs did not carry
       lds_dma_wait();
       __syncthreads();
       cur ^= 1;
@@ -545,154 +486,19 @@ struct WPipe {
     }
     return slot_w(cur);
   }
-  __device__ __forceinline__ void mid() const {}
   __device__ __forceinline__ const T* w() const { return slot_w(cur); }
   __device__ __forceinline__ const float* v() const { return slot_v(cur); }
 };
 
-// Ping-pong ring for 8-wave blocks: waves 0-3 (group 0) and 4-7 (group 1) run the same layer
-// sequence half a stage apart, so on every SIMD one wave is in a layer's MFMA half while its
-// partner is in the previous layer's SiLU/VALU half (the two waves of a SIMD come from the two
-// groups). Every wave calls next() (stage barrier, full wait) and mid() (bare s_barrier) once per
-// stage; group 1 starts and group 0 ends with one extra mid(), so their barrier counts match and
-// group 1's stage boundaries fall on group 0's mid-points. Only group 0 issues the LDS-DMA, at its
-// stage start, into the slot of stage i-2 (NSLOT = 3): group 1 finished that stage one barrier
-// earlier, and the DMA lands before group 0's next stage barrier (its own vmcnt(0) there).
-template <typename T, int CAP, int VCAP>
-struct RingPipe {
-  static constexpr int NSLOT = 3;
-  static constexpr int SLOT_BYTES = CAP * BLK * (int)sizeof(T) + VCAP * 4;
-  char* base;
-  int cur;
-  bool loader;
-  __device__ explicit RingPipe(void* lds) : base(reinterpret_cast<char*>(lds)), cur(NSLOT - 1) {
-    loader = __builtin_amdgcn_readfirstlane(threadIdx.x >> 8) == 0;
-  }
-  __device__ __forceinline__ T* slot_w(int s) const { return reinterpret_cast<T*>(base + s * SLOT_BYTES); }
-  __device__ __forceinline__ float* slot_v(int s) const {
-    return reinterpret_cast<float*>(base + s * SLOT_BYTES + CAP * BLK * (int)sizeof(T));
-  }
-  __device__ __forceinline__ int nxt(int s) const { return s == NSLOT - 1 ? 0 : s + 1; }
-  __device__ __forceinline__ DmaPump* pump_ptr() { return nullptr; }
-  // DMA of the stage AFTER the current one (group 0 only)
-  __device__ __forceinline__ void issue(const T* g, int nblk, const float* gv = nullptr, int nvec = 0) {
-    if (loader) {
-      const int s = nxt(cur);
-      dma_blocks<4>(slot_w(s), g, nblk);
-      if (gv) dma_vec<4>(slot_v(s), gv, nvec / 128);
-    }
-  }
-  __device__ __forceinline__ const T* next() {
-    lds_dma_wait();
-    __syncthreads();
-    cur = nxt(cur);
-    return slot_w(cur);
-  }
-  __device__ __forceinline__ void mid() const {
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-  }
-  __device__ __forceinline__ const T* w() const { return slot_w(cur); }
-  __device__ __forceinline__ const float* v() const { return slot_v(cur); }
-};
-
-// Decoupled weight ring for one 8-wave block per CU (128 rows per weight pass): NSLOT = 4 LDS
-// slots, every stage's pieces split over all 8 waves, and NO workgroup barrier per stage. Stage i
-// lives in slot i % 4; per slot one monotone LDS counter FULL counts the waves whose pieces of the
-// slot's current stage have landed (generation g = i / 4 is complete at 8 (g + 1)). A wave
-// entering stage i:
-//   1. drains its own vector memory (s_waitcnt vmcnt(0): its pieces of stage i+1, issued when it
-//      entered stage i-1, have landed) and its LDS reads (lgkmcnt(0): nothing of stage i-1 is read
-//      later), then adds 1 to FULL[(i+1) % 4];
-//   2. waits (s_sleep poll) until FULL[i % 4] is complete, i.e. every wave has entered stage i-1;
-//   3. issues its share of stage i+2 into slot (i+2) % 4 = the slot of stage i-2, which every wave
-//      finished before entering stage i-1 (step 2), so no further check is needed.
-// So a weight piece has two stages of compute to land, and a wave can run up to one stage ahead of
-// the slowest wave of its block (the two waves of a SIMD drift out of phase instead of meeting at
-// a barrier 25 times per tile). Call order: init(); issue(0); issue(1); then per stage i:
-// enter(i); if (i + 2 < total) issue(i + 2, ...); compute with w(i) / v(i).
-template <typename T, int CAP, int VCAP, int NW_ = 8>
-struct FullRing {
-  static constexpr int NW = NW_, NSLOT = 4;
-  static constexpr int SLOT_BYTES = CAP * BLK * (int)sizeof(T) + VCAP * 4;
-  static constexpr int LDS_BYTES = NSLOT * SLOT_BYTES + 16;  // + 4 FULL counters
-  char* base;
-  uint32_t* full;
-  int wave;
-  __device__ explicit FullRing(void* lds)
-      : base(reinterpret_cast<char*>(lds)),
-        full(reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(lds) + NSLOT * SLOT_BYTES)) {
-    wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  }
-  __device__ __forceinline__ void init() {
-    if (threadIdx.x < NSLOT) full[threadIdx.x] = 0u;
-    __syncthreads();
-  }
-  __device__ __forceinline__ T* slot_w(int i) const { return reinterpret_cast<T*>(base + (i & 3) * SLOT_BYTES); }
-  __device__ __forceinline__ float* slot_v(int i) const {
-    return reinterpret_cast<float*>(base + (i & 3) * SLOT_BYTES + CAP * BLK * (int)sizeof(T));
-  }
-  // this wave's share of stage i: 1-KiB pieces wave, wave + 8, ...; the 512-B bias vector by the
-  // wave whose turn it is (i % 8), as one half-wave piece
-  __device__ __forceinline__ void issue(int i, const T* g, int nblk, const float* gv) {
-    const int loff = (threadIdx.x & 63) * 16;
-    const int nkib = nblk * BLK * (int)sizeof(T) / 1024;
-    const __amdgpu_buffer_rsrc_t r = buf_rsrc(g);
-    char* dst = reinterpret_cast<char*>(slot_w(i));
-    for (int p = wave; p < nkib; p += NW)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)(dst + p * 1024), 16,
-                                               loff, p * 1024, 0, 0);
-    if (gv != nullptr && wave == i % NW && (threadIdx.x & 63) < 32)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(buf_rsrc(gv),
-                                               (__attribute__((address_space(3))) void*)slot_v(i), 16,
-                                               (threadIdx.x & 63) * 16, 0, 0, 0);
-  }
-  // pumped form (DI_DMA_PUMP > 0): defer() records this wave's pieces of stage i, mma() issues
-  // one of them every DI_DMA_PUMP MFMAs (so the CU's LDS-DMA path is not flooded by 8 waves
-  // issuing a whole stage at once), flush() issues what the stage's MFMAs did not carry
-  DmaPump dp;
-  __device__ __forceinline__ DmaPump* pump_ptr() { return DI_DMA_PUMP > 0 ? &dp : nullptr; }
-  __device__ __forceinline__ void defer(int i, const T* g, int nblk, const float* gv) {
-    dp.src = reinterpret_cast<const char*>(g);
-    dp.dst = reinterpret_cast<char*>(slot_w(i));
-    dp.pi = wave;
-    dp.pk = nblk * BLK * (int)sizeof(T) / 1024;
-    dp.step = NW;
-    if (gv != nullptr && wave == i % NW && (threadIdx.x & 63) < 32)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(buf_rsrc(gv),
-                                               (__attribute__((address_space(3))) void*)slot_v(i), 16,
-                                               (threadIdx.x & 63) * 16, 0, 0, 0);
-  }
-  __device__ __forceinline__ void flush() {
-    while (dp.pi < dp.pk) dp.pump();
-  }
-  __device__ __forceinline__ void signal(int i) {  // my pieces of stage i have landed
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    if ((threadIdx.x & 63) == 0)
-      __hip_atomic_fetch_add(full + (i & 3), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  }
-  __device__ __forceinline__ void wait(int i) {  // every wave's pieces of stage i have landed
-    const uint32_t target = (uint32_t)NW * (uint32_t)((i >> 2) + 1);
-    while (__builtin_amdgcn_readfirstlane(
-               __hip_atomic_load(full + (i & 3), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) < target)
-      __builtin_amdgcn_s_sleep(1);
-    asm volatile("" ::: "memory");
-  }
-  // prologue: stages 0 and 1 issued by every wave; signal both, wait for stage 0
-  __device__ __forceinline__ void start() {
-    signal(0);
-    signal(1);
-    wait(0);
-  }
-  // entering stage i >= 1: signal stage i+1 (own pieces issued at stage i-1), wait stage i
-  __device__ __forceinline__ void enter(int i, bool has_next) {
-    if (has_next) signal(i + 1);
-    else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    wait(i);
-  }
-  __device__ __forceinline__ const T* w(int i) const { return slot_w(i); }
-  __device__ __forceinline__ const float* v(int i) const { return slot_v(i); }
+// Launch geometry of a kernel: NW waves per block, ROWS_PER_WAVE rows per wave. The kernel's
+// __launch_bounds__ / flat-work-group-size, its WPipe, its row index and the host launch all read
+// THREADS / ROWS from the same struct.
+template <int NW_>
+struct KernelGeo {
+  static_assert(NW_ >= 1 && NW_ <= 16, "waves per block");
+  static constexpr int NW = NW_;
+  static constexpr int THREADS = 64 * NW_;
+  static constexpr int ROWS = ROWS_PER_WAVE * NW_;
 };
 
 // Single synchronous stage (kept for simple kernels).

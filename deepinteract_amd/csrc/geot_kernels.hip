@@ -76,16 +76,6 @@ struct NodeArgs {
   void* qkv_out;
 };
 
-// Wave priority of the GeoT kernels (s_setprio at entry; 0 = hardware default, no instruction):
-// beside the pair-tensor store stream (priority 0) the GeoT waves win every issue tie.
-#ifndef DI_GEOT_PRIO
-#define DI_GEOT_PRIO 0
-#endif
-#define DI_GEOT_ENTRY() \
-  do {                                                              \
-    if (DI_GEOT_PRIO > 0) __builtin_amdgcn_s_setprio(DI_GEOT_PRIO); \
-  } while (0)
-
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 template <int NW>
 __device__ __forceinline__ int row_id() {
@@ -96,18 +86,14 @@ __device__ __forceinline__ int row_id() {
 // (2 x 80 KiB of LDS, <=256 VGPRs), each double-buffering its weight stages so the LDS-DMA of
 // layer i+1 runs under layer i's MFMAs. Two independent blocks per CU matter: the waves of ONE
 // block meet at every stage barrier in lockstep, so only waves of the other block can fill a
-// SIMD's MFMA pipe while these run their SiLU VALU work (and vice versa).
+// SIMD's MFMA pipe while these run their SiLU VALU work (and vice versa). Measured alternatives
+// (round 1-2): one 8-wave block per CU with or without a decoupled ring, persistent
+// tiles, XCD-aware tile order, static wave priority, pumped DMA pieces -- all slower.
 // fp32 (parity path; stages twice as large): same geometry, synchronous single-buffered stages.
 template <class DT>
-#ifndef DI_GEO_NW
-#define DI_GEO_NW 4
-#endif
-struct Geo {
-  static constexpr int NW = DI_GEO_NW;  // waves per block (2 waves per SIMD either way)
+struct Geo : KernelGeo<4> {
   static constexpr bool DBUF = DT::kBF16;
   static constexpr int CAP = 40;  // blocks per weight stage buffer
-  static constexpr int THREADS = 64 * NW;
-  static constexpr int ROWS = ROWS_PER_WAVE * NW;
 };
 
 // The edge's own input row F: bf16 path keeps it in registers as a packed MFMA operand (its
@@ -145,17 +131,17 @@ struct FRow<F32T> {
 };
 
 // ================================================================ node embedding (+ Q/K/V of layer 0)
+using EmbedGeo = KernelGeo<4>;
 template <class DT>
-__global__ __launch_bounds__(THREADS) void k_node_embed(EmbedArgs a) {
+__global__ __launch_bounds__(EmbedGeo::THREADS) void k_node_embed(EmbedArgs a) {
   using T = typename DT::T;
-  DI_GEOT_ENTRY();
   __shared__ __attribute__((aligned(16))) T lds[2 * MAT128 * BLK];
   const int lane = lane_id(), g = lane >> 4;
-  const int r = row_id<WAVES>();
+  const int r = row_id<EmbedGeo::NW>();
   const bool valid = r < a.Nt;
   const int v = valid ? r : a.Nt - 1;
   const T* W = reinterpret_cast<const T*>(a.wmat);
-  WPipe<T, WAVES, true, MAT128> pipe(lds);
+  WPipe<T, EmbedGeo::NW, true, MAT128> pipe(lds);
   pipe.issue(W + EM_EMB * BLK, MAT128);
 
   Act<8> x;  // in_dim (113 raw DIPS-Plus + geometric features) input columns, zero padded to 128
@@ -190,28 +176,20 @@ __global__ __launch_bounds__(THREADS) void k_node_embed(EmbedArgs a) {
 // the orientation terms are the packed constants IEV_ORC / IEV_OGATE; the layer-0
 // silu(nbr_linear(F)) rows are only computed when fn_out is given (the grouped edge kernel does
 // not gather them for such batches).
-// Launch shape of the bf16 InitEdge: weights staged synchronously in one 40-KiB slot per block
-// (DI_INIT_DBUF=0), so three blocks share a CU (DI_INIT_WPE=3; the kernel holds 150 VGPRs) and
-// cover each other's stage waits. Measured (C3 micro-batch, GEO_REF): alone 109 vs 118 us with two
-// double-buffered blocks, beside the pair stream 168 vs 187 us; four blocks (128 VGPRs) spill:
-// 130 / 206 us.
-#ifndef DI_INIT_DBUF
-#define DI_INIT_DBUF 0
-#endif
-#ifndef DI_INIT_WPE
-#define DI_INIT_WPE 3
-#endif
+// Launch shape of the bf16 InitEdge: weights staged synchronously in one 40-KiB slot per block,
+// so three blocks share a CU (the kernel holds 150 VGPRs) and cover each other's stage waits.
+// Measured (C3 micro-batch, GEO_REF): alone 109 vs 118 us with two double-buffered blocks, beside
+// the pair stream 168 vs 187 us; four blocks (128 VGPRs) spill: 130 / 206 us.
 template <class DT>
 struct InitGeo : Geo<DT> {
-  static constexpr bool DBUF = DT::kBF16 && DI_INIT_DBUF;
-  static constexpr int WPE = DT::kBF16 ? DI_INIT_WPE : 2;
+  static constexpr bool DBUF = false;
+  static constexpr int WPE = DT::kBF16 ? 3 : 2;  // blocks (waves per SIMD) per CU
 };
 template <class DT, bool GC>
-__global__ __attribute__((amdgpu_flat_work_group_size(1, 64 * DI_GEO_NW),
+__global__ __attribute__((amdgpu_flat_work_group_size(1, InitGeo<DT>::THREADS),
                           amdgpu_waves_per_eu(InitGeo<DT>::WPE, InitGeo<DT>::WPE)))
 void k_init_edge(InitArgs a) {
   using T = typename DT::T;
-  DI_GEOT_ENTRY();
   using G = InitGeo<DT>;
   constexpr bool FAST = DT::kBF16;
   constexpr int CAP = G::CAP;
@@ -222,7 +200,6 @@ void k_init_edge(InitArgs a) {
   const int e = valid ? r : a.Et - 1;
   const T* W = reinterpret_cast<const T*>(a.wmat);
   WPipe<T, G::NW, G::DBUF, CAP> pipe(lds);
-  DmaPump* PP = pipe.pump_ptr();
   pipe.issue(W + IE_T0 * BLK, 8);  // stage 0: the collapsed edge-message map (8 blocks)
 
   Act<2> geo;
@@ -243,7 +220,7 @@ void k_init_edge(InitArgs a) {
     // [128, 2] map of the message columns (no activation between them, :237-241)
     const T* w = pipe.next();
     pipe.issue(W + (IE_T0 + 40 * geo_t(0)) * BLK, 40);
-    mma<8, 1>(acc, gop, w, lane, PP);
+    mma<8, 1>(acc, gop, w, lane);
   }
 #pragma unroll 1
   for (int i = 0; i < NT; ++i) {
@@ -252,9 +229,9 @@ void k_init_edge(InitArgs a) {
     else pipe.issue(W + IE_GEO1 * BLK, 40);
     Act<8> y;
     zero(y);
-    mma<8, 1>(y, gop, w, lane, PP);
+    mma<8, 1>(y, gop, w, lane);
     silu2_<8, FAST>(y);
-    linear<DT, 8, 4>(acc, y, w + 8 * BLK, lane, PP);
+    linear<DT, 8, 4>(acc, y, w + 8 * BLK, lane);
   }
   silu2_<8, FAST>(acc);  // combined_edge_logits (log2 units: feeds the gate product -> linear)
   // gating: (em1 + silu(d1) + silu(r1) + silu(o1) + silu(a1)) * c
@@ -269,7 +246,7 @@ void k_init_edge(InitArgs a) {
       if (GC && (t == 2 || t == 3)) continue;
       Act<8> y;
       zero(y);
-      mma<8, 1>(y, gop, w + 8 * t * BLK, lane, PP);
+      mma<8, 1>(y, gop, w + 8 * t * BLK, lane);
       if (t > 0) silu2_<8, FAST>(y);
       add_(gs, y);
     }
@@ -283,9 +260,9 @@ void k_init_edge(InitArgs a) {
     if (with_fn) pipe.issue(W + IE_NBR * BLK, MAT128);
     Act<2> z;
     zero(z);
-    linear<DT, 2, 4>(z, acc, w, lane, PP);
+    linear<DT, 2, 4>(z, acc, w, lane);
     zero(f);
-    linear<DT, 8, 1>(f, z, w + 8 * BLK, lane, PP);
+    linear<DT, 8, 1>(f, z, w + 8 * BLK, lane);
   }
   if (valid) store_edge_row(f, reinterpret_cast<T*>(a.f_out) + (int64_t)e * HID, g);
   if (!with_fn) return;
@@ -295,7 +272,7 @@ void k_init_edge(InitArgs a) {
     const T* w = pipe.next();
     Act<8> fn;
     init_vec(fn, a.wvec + IEV_NBR, g);
-    linear<DT, 8, 4>(fn, f, w, lane, PP);
+    linear<DT, 8, 4>(fn, f, w, lane);
     silu_<8, FAST>(fn);
     if (valid) store_edge_row(fn, reinterpret_cast<T*>(a.fn_out) + (int64_t)e * HID, g);
   }
@@ -326,47 +303,18 @@ __constant__ int EL_VEC[25] = {-1, ELV_OM, -1,
 constexpr int EL_NSTAGE_CONF = 18, EL_NSTAGE_FINAL = 19, EL_NSTAGE = 25;
 constexpr int EL_CAP = 36;
 
-// bf16 (the benchmark path): two independent 4-wave blocks per CU, each double-buffering its
-// weight stages (WPipe). DI_EDGE_RING=1 instead runs one 8-wave block per CU (128 rows per weight
-// pass, half the LDS-DMA bytes per CU) on the decoupled 4-slot FullRing (common.h: no per-stage
-// barrier, two stages of DMA lead). Measured (C3 micro-batch, serial, rocprof-consistent HIP
-// events): ring 518-533 us vs 501-504 us for the two 4-wave blocks, ring + pumped pieces
-// (DI_DMA_PUMP 2/4/8) 523-556 us: the two waves of a SIMD from two independent blocks keep more
-// phase diversity than the halved weight stream buys.
-// fp32 parity path: 4-wave blocks with synchronous stages (WPipe).
-#ifndef DI_EDGE_RING
-#define DI_EDGE_RING 0
-#endif
-#ifndef DI_RING_PRIO
-#define DI_RING_PRIO 0
-#endif
-#ifndef DI_RING_STAGGER
-#define DI_RING_STAGGER 0  // x 512 clocks of start delay for waves 4-7
-#endif
+// k_edge_layer: 16 rows per wave, 4-wave blocks, two blocks per CU: the fp32 edge layers (the
+// reference's precision; double-buffered bf16 is k_edge_lean below) and the conformation module
+// alone (di_conformation, both dtypes).
 template <class DT>
-struct EdgeGeo {
-  static constexpr bool RING = DT::kBF16 && DI_EDGE_RING;
-  static constexpr int NW = RING ? 8 : Geo<DT>::NW;
-  static constexpr int THREADS = 64 * NW;
-  static constexpr int ROWS = ROWS_PER_WAVE * NW;
-};
-template <class DT>
-using EdgePipe = std::conditional_t<EdgeGeo<DT>::RING, FullRing<typename DT::T, EL_CAP, 128>,
-                                    WPipe<typename DT::T, Geo<DT>::NW, Geo<DT>::DBUF, EL_CAP, 128>>;
-template <class DT>
-constexpr int edge_lds_bytes() {
-  if constexpr (EdgeGeo<DT>::RING) return EdgePipe<DT>::LDS_BYTES;
-  else return (Geo<DT>::DBUF ? 2 : 1) * EdgePipe<DT>::SLOT_BYTES;
-}
+using EdgePipe = WPipe<typename DT::T, Geo<DT>::NW, Geo<DT>::DBUF, EL_CAP, 128>;
 
 // MODE: 0 intermediate layer, 1 final layer, 2 conformation module alone (di_conformation)
 template <int MODE>
 constexpr int edge_nstage() { return MODE == 2 ? EL_NSTAGE_CONF : (MODE == 1 ? EL_NSTAGE_FINAL : EL_NSTAGE); }
 
-// The weight-stage sequence of a block's tiles: next() makes the next stage current (its weights
-// w(), its bias vector v()) and keeps the DMA stream ahead of it (ring: two stages, barrier pipe:
-// one); the sequence runs on across the block's tiles (stage 0 of tile t+1 follows the last stage
-// of tile t).
+// The weight-stage sequence of one tile: next() makes the next stage current (its weights w(),
+// its bias vector v()) and issues the DMA of the one after it.
 // GC (DI_GRAPH_GEO_REF batches, layer modes 0/1): the sequence starts at orig_msg_linear, which
 // then carries the orig_msg_linear bias, and (intermediate layers) ends before nbr_linear
 template <class DT, int MODE, bool GC = false>
@@ -376,56 +324,20 @@ struct EdgeStages {
   EdgePipe<DT>& pipe;
   const T* W;
   const float* V;
-  int gi;     // global index of the next stage to make current
-  int total;  // stages this block runs (tiles x NS)
-  const float* vcur;
-  __device__ void issue(int i, bool pumped = false) {
-    const int s0 = i % NS;
+  int gi;  // index of the next stage to make current
+  __device__ void issue(int s0) {
     const int s = GC ? s0 + 2 : s0;
     const int vo = (GC && s0 == 0) ? ELV_OM : EL_VEC[s];
-    if constexpr (EdgeGeo<DT>::RING) {
-      if (pumped) pipe.defer(i, W + EL_ORDER[s] * BLK, EL_SIZE[s], vo >= 0 ? V + vo : nullptr);
-      else pipe.issue(i, W + EL_ORDER[s] * BLK, EL_SIZE[s], vo >= 0 ? V + vo : nullptr);
-    } else {
-      pipe.issue(W + EL_ORDER[s] * BLK, EL_SIZE[s], vo >= 0 ? V + vo : nullptr, 128);
-    }
+    pipe.issue(W + EL_ORDER[s] * BLK, EL_SIZE[s], vo >= 0 ? V + vo : nullptr, 128);
   }
-  // weight-piece pump handed to the MFMA loops (nullptr: pieces were issued in one burst)
-  __device__ DmaPump* pp() {
-    if constexpr (EdgeGeo<DT>::RING) return pipe.pump_ptr();
-    else return nullptr;
-  }
-  __device__ void begin() {  // before the first next()
-    if constexpr (EdgeGeo<DT>::RING) {
-      pipe.init();
-      issue(0);
-      if (total > 1) issue(1);
-    } else {
-      issue(0);
-    }
-  }
+  __device__ void begin() { issue(0); }
   __device__ const T* next() {
     const int i = gi++;
-    if constexpr (EdgeGeo<DT>::RING) {
-      if (i == 0) {
-        pipe.signal(0);
-        if (total > 1) pipe.signal(1);
-        pipe.wait(0);
-      } else {
-        if constexpr (DI_DMA_PUMP > 0) pipe.flush();  // pieces of stage i+1 the last stage did not carry
-        pipe.enter(i, i + 1 < total);
-      }
-      if (i + 2 < total) issue(i + 2, DI_DMA_PUMP > 0);
-      vcur = pipe.v(i);
-      return pipe.w(i);
-    } else {
-      const T* w = pipe.next();
-      if (i + 1 < total) issue(i + 1);
-      vcur = pipe.v();
-      return w;
-    }
+    const T* w = pipe.next();
+    if (i + 1 < NS) issue(i + 1);
+    return w;
   }
-  __device__ const float* v() const { return vcur; }
+  __device__ const float* v() const { return pipe.v(); }
 };
 
 template <class DT, int MODE, bool GC>
@@ -437,229 +349,159 @@ __device__ __forceinline__ void res_block(Act<8>& x, EdgeStages<DT, MODE, GC>& s
     const typename DT::T* w = st.next();
     Act<8> t;
     init_vec_lds(t, st.v(), g);
-    linear<DT, 8, 4>(t, y, w, lane, st.pp());
+    linear<DT, 8, 4>(t, y, w, lane);
     silu2_<8, FAST>(t);  // log2 units: folded into the next linear / the residual fma
     y = t;
   }
   add_scaled_(x, y, silu2_unit<FAST>());
 }
 
-// One tile's per-row inputs, loaded a tile ahead (persistent blocks): neighbour ids, the 28 edge
-// features, the edge's own row F (bf16: raw, it IS the packed MFMA operand) and the first
-// neighbour row. The loads are issued during the previous tile's last stages.
-template <class DT, bool GC = false>
-struct EdgeIn {
-  using T = typename DT::T;
-  int4 nb;
-  Act<2> geo;
-  RawRow<T> fraw;
-  RawRow<T> xn;
-  __device__ __forceinline__ void load_ids(const EdgeArgs& a, int e) {
-    if constexpr (!GC) nb = *reinterpret_cast<const int4*>(a.nbr + (int64_t)e * 4);
-  }
-  __device__ __forceinline__ void load_rest(const EdgeArgs& a, int e, int g) {
-    load_edge_geo(geo, a.edge_f + (int64_t)e * NFEAT_E, g);
-    if constexpr (DT::kBF16) fraw.load(reinterpret_cast<const T*>(a.f_in) + (int64_t)e * HID, g);
-    if constexpr (!GC) xn.load(reinterpret_cast<const T*>(a.fn_in) + (int64_t)nb.x * HID, g);
-  }
-};
-
-template <class DT>
-__device__ __forceinline__ int tile_edge(int tile, int Et, bool& valid) {
-  const int r = tile * EdgeGeo<DT>::ROWS + (threadIdx.x >> 6) * ROWS_PER_WAVE + (threadIdx.x & 15);
-  valid = r < Et;
-  return valid ? r : Et - 1;
-}
-
-// XCD-aware tile order for the one-tile-per-block grid (8 * ceil(T/8) blocks). The dispatcher
-// deals workgroups round-robin over the 8 XCDs (block b -> XCD b % 8), each with its own L2, so
-// block b takes tile (b % 8) * ceil(T/8) + b / 8: every XCD walks one contiguous eighth of the
-// edge array, and the neighbour-edge rows a tile gathers (Fn rows of sequence/space-near nodes,
-// the dst node's own rows in the adjacent tile) are mostly already in that XCD's L2.
-#ifndef DI_XCD_TILES
-#define DI_XCD_TILES 0
-#endif
-__host__ __device__ inline int xcd_grid(int ntiles) { return DI_XCD_TILES ? 8 * ((ntiles + 7) / 8) : ntiles; }
-__device__ __forceinline__ int xcd_tile(int b, int ntiles) {
-  if (!DI_XCD_TILES) return b;
-  const int q = (ntiles + 7) >> 3;
-  return (b & 7) * q + (b >> 3);
-}
-
 // Two 4-wave blocks per CU, each wave capped at 240 VGPRs (amdgpu_num_vgpr counts the unified
 // VGPR+AGPR file in pairs on gfx950): 2 x 240 + 32 = 512 leaves one pair-tensor wave per SIMD
-// co-resident, so the HBM-bound pair stores run under the MFMA/VALU-bound edge layers.
-// Persistent: each block walks tiles blockIdx.x, +gridDim.x, ...; the weight-stage stream runs on
-// across tiles (the last stage's DMA slot fetches stage 0 of the next tile) and the next tile's
-// inputs are prefetched under the current tile's last stages, so no tile pays a cold prologue.
+// co-resident. One 64-row tile per block.
 // GC (DI_GRAPH_GEO_REF, modes 0/1): the neighbour-message stages are skipped (exactly zero) and no
 // silu(nbr_linear(F)) rows are gathered or written.
 template <class DT, int MODE, bool GC = false>
-#ifndef DI_EDGE_NUM_VGPR
-#define DI_EDGE_NUM_VGPR 120
-#endif
-__global__ __attribute__((amdgpu_flat_work_group_size(1, 512), amdgpu_waves_per_eu(2, 2),
-                          amdgpu_num_vgpr(DI_EDGE_NUM_VGPR)))
+__global__ __attribute__((amdgpu_flat_work_group_size(1, Geo<DT>::THREADS), amdgpu_waves_per_eu(2, 2),
+                          amdgpu_num_vgpr(120)))
 void k_edge_layer(EdgeArgs a) {
   constexpr bool FINAL = MODE == 1, CONF = MODE == 2;
-  DI_GEOT_ENTRY();
   using T = typename DT::T;
-  using G = EdgeGeo<DT>;
+  using G = Geo<DT>;
   constexpr bool FAST = DT::kBF16;
-  __shared__ __attribute__((aligned(16))) char lds[edge_lds_bytes<DT>()];
+  __shared__ __attribute__((aligned(16))) char lds[(G::DBUF ? 2 : 1) * EdgePipe<DT>::SLOT_BYTES];
   const int lane = lane_id(), g = lane >> 4;
-  const int ntiles = (a.Et + G::ROWS - 1) / G::ROWS;
+  const int r = row_id<G::NW>();
+  const bool valid = r < a.Et;
+  const int e = valid ? r : a.Et - 1;
   const T* W = reinterpret_cast<const T*>(a.wmat);
   const T* fn_in = reinterpret_cast<const T*>(a.fn_in);
   const T* qkv = reinterpret_cast<const T*>(a.qkv);
-
-  // first tile: XCD-aware when every block owns one tile; persistent grids stride by gridDim.x
-  const int first = (int)gridDim.x >= ntiles ? xcd_tile(blockIdx.x, ntiles) : (int)blockIdx.x;
-  if (first >= ntiles) return;  // padding block of the XCD-aware grid (uniform, before any DMA)
-  const int my_tiles = (ntiles - first + (int)gridDim.x - 1) / (int)gridDim.x;
+  const T* f_row = reinterpret_cast<const T*>(a.f_in) + (int64_t)e * HID;
 
   EdgePipe<DT> pipe(lds);
-  EdgeStages<DT, MODE, GC> st{pipe, W, a.wvec, 0, my_tiles * EdgeStages<DT, MODE, GC>::NS, nullptr};
+  EdgeStages<DT, MODE, GC> st{pipe, W, a.wvec, 0};
   st.begin();
-  if constexpr (G::RING) {
-    // the younger half (waves 4-7) of the block: static priority and/or a start delay, so the two
-    // waves of a SIMD run out of phase (MI355X_MICROARCH.md "Two waves per SIMD", items 4 and 9)
-    const bool young = __builtin_amdgcn_readfirstlane(threadIdx.x) >= 256;
-    if (DI_RING_PRIO && young) __builtin_amdgcn_s_setprio(1);
-    if (DI_RING_STAGGER > 0 && young)
-      for (int t = 0; t < DI_RING_STAGGER; ++t) __builtin_amdgcn_s_sleep(8);
-  }
-  EdgeIn<DT, GC> in;
+  int4 nb = {0, 0, 0, 0};
+  if constexpr (!GC) nb = *reinterpret_cast<const int4*>(a.nbr + (int64_t)e * 4);
+  Op<DT, 1> gop;
   {
-    bool v0;
-    const int e0 = tile_edge<DT>(first, a.Et, v0);
-    in.load_ids(a, e0);
-    in.load_rest(a, e0, g);
+    Act<2> geo;
+    load_edge_geo(geo, a.edge_f + (int64_t)e * NFEAT_E, g);
+    make_op(gop, geo);
+  }
+  FRow<DT> fr;
+  if constexpr (DT::kBF16) {
+    RawRow<T> fraw;
+    fraw.load(f_row, g);
+    fr.set_raw(fraw);
   }
 
-#pragma unroll 1
-  for (int tile = first; tile < ntiles; tile += gridDim.x) {
-    bool valid;
-    const int e = tile_edge<DT>(tile, a.Et, valid);
-    const bool more = tile + (int)gridDim.x < ntiles;
-    bool vn;
-    const int en = tile_edge<DT>(more ? tile + gridDim.x : tile, a.Et, vn);
-    const T* f_row = reinterpret_cast<const T*>(a.f_in) + (int64_t)e * HID;
-
-    const int4 nb = in.nb;
-    Op<DT, 1> gop;
-    make_op(gop, in.geo);
-    FRow<DT> fr;
-    if constexpr (DT::kBF16) fr.set_raw(in.fraw);
-
-    const T* w;
-    Act<8> x;
-    if constexpr (GC) {
-      // DI_GRAPH_GEO_REF: the neighbour messages are multiplied by dir_linear_1(dir_linear_0(0)) = 0
-      // (:408): x = orig_msg_linear(F) + b exactly
-      w = st.next();  // orig_msg_linear (+ its bias)
-      init_vec_lds(x, st.v(), g);
-    } else {
-      // ---- neighbour-edge messages (conformation_module_message_func :384-418)
-      w = st.next();  // stage 0: geometric gates + downward_proj
-      Act<4> gate;              // dir . orient . amide embeddings (64)
-      {
-        Act<4> t1;
-        zero(gate);
-        mma<4, 1>(gate, gop, w + 8 * BLK, lane, st.pp());
-        zero(t1);
-        mma<4, 1>(t1, gop, w + 12 * BLK, lane, st.pp());
-        mul_(gate, t1);
-        zero(t1);
-        mma<4, 1>(t1, gop, w + 16 * BLK, lane, st.pp());
-        mul_(gate, t1);
-      }
-      Act<4> s;
-      zero(s);
-      RawRow<T> xn = in.xn;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        Act<8> x;
-        xn.to_act(x);
-        if (j < 3) {  // prefetch the next neighbour row under this one's MFMAs
-          const int nx = j == 0 ? nb.y : (j == 1 ? nb.z : nb.w);
-          xn.load(fn_in + (int64_t)nx * HID, g);
-        }
-        // dist_linear_1(dist_linear_0(dist)), recomputed per neighbour (8 MFMAs) rather than held
-        // live across the loop: the memory clobber stops the compiler from hoisting it (32 VGPRs)
-        asm volatile("" ::: "memory");
-        Act<8> dg;
-        zero(dg);
-        mma<8, 1>(dg, gop, w, lane, st.pp());
-#pragma unroll
-        for (int b = 0; b < 8; ++b)
-#pragma unroll
-          for (int q = 0; q < 4; ++q) x.v[b][q] *= dg.v[b][q];  // gathered rows are silu(nbr_linear(F))
-        Act<4> y;
-        zero(y);
-        linear<DT, 4, 4>(y, x, w + 20 * BLK, lane, st.pp());  // downward_proj
-#pragma unroll
-        for (int b = 0; b < 4; ++b)
-#pragma unroll
-          for (int q = 0; q < 4; ++q) s.v[b][q] += silu2<FAST>(y.v[b][q]) * gate.v[b][q];
-      }
-      w = st.next();  // stage 1: upward_proj (+ orig_msg_linear bias)
-      zero(x);
-      linear<DT, 8, 2>(x, s, w, lane, st.pp());
-      silu2_<8, FAST>(x);
-      {
-        Act<8> bo;
-        init_vec_lds(bo, st.v(), g);
-#pragma unroll
-        for (int b = 0; b < 8; ++b) x.v[b] = silu2_unit<FAST>() * x.v[b] + bo.v[b];
-      }
-      w = st.next();  // stage 2: orig_msg_linear(res) + nbr
-    }
-    mma<8, 4>(x, fr.operand(f_row, g), w, lane, st.pp());
-    res_block<DT, MODE, GC>(x, st, lane, g);
-    res_block<DT, MODE, GC>(x, st, lane, g);
+  const T* w;
+  Act<8> x;
+  if constexpr (GC) {
+    // DI_GRAPH_GEO_REF: the neighbour messages are multiplied by dir_linear_1(dir_linear_0(0)) = 0
+    // (:408): x = orig_msg_linear(F) + b exactly
+    w = st.next();  // orig_msg_linear (+ its bias)
+    init_vec_lds(x, st.v(), g);
+  } else {
+    // ---- neighbour-edge messages (conformation_module_message_func :384-418)
+    RawRow<T> xn;
+    xn.load(fn_in + (int64_t)nb.x * HID, g);
+    w = st.next();  // stage 0: geometric gates + downward_proj
+    Act<4> gate;    // dir . orient . amide embeddings (64)
     {
-      w = st.next();  // res_connect_linear
-      Act<8> y;
-      init_vec_lds(y, st.v(), g);
-      linear<DT, 8, 4>(y, x, w, lane, st.pp());
-      silu2_<8, FAST>(y);
-      fr.act(x, f_row, g);
-      add_scaled_(x, y, silu2_unit<FAST>());
+      Act<4> t1;
+      zero(gate);
+      mma<4, 1>(gate, gop, w + 8 * BLK, lane);
+      zero(t1);
+      mma<4, 1>(t1, gop, w + 12 * BLK, lane);
+      mul_(gate, t1);
+      zero(t1);
+      mma<4, 1>(t1, gop, w + 16 * BLK, lane);
+      mul_(gate, t1);
     }
-    res_block<DT, MODE, GC>(x, st, lane, g);
-    res_block<DT, MODE, GC>(x, st, lane, g);
+    Act<4> s;
+    zero(s);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      Act<8> xa;
+      xn.to_act(xa);
+      if (j < 3) {  // prefetch the next neighbour row under this one's MFMAs
+        const int nx = j == 0 ? nb.y : (j == 1 ? nb.z : nb.w);
+        xn.load(fn_in + (int64_t)nx * HID, g);
+      }
+      // dist_linear_1(dist_linear_0(dist)), recomputed per neighbour (8 MFMAs) rather than held
+      // live across the loop: the memory clobber stops the compiler from hoisting it (32 VGPRs)
+      asm volatile("" ::: "memory");
+      Act<8> dg;
+      zero(dg);
+      mma<8, 1>(dg, gop, w, lane);
+#pragma unroll
+      for (int b = 0; b < 8; ++b)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) xa.v[b][q] *= dg.v[b][q];  // gathered rows are silu(nbr_linear(F))
+      Act<4> y;
+      zero(y);
+      linear<DT, 4, 4>(y, xa, w + 20 * BLK, lane);  // downward_proj
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) s.v[b][q] += silu2<FAST>(y.v[b][q]) * gate.v[b][q];
+    }
+    w = st.next();  // stage 1: upward_proj (+ orig_msg_linear bias)
+    zero(x);
+    linear<DT, 8, 2>(x, s, w, lane);
+    silu2_<8, FAST>(x);
     {
-      w = st.next();  // final geometric gate
-      if ((FINAL || CONF) && more) in.load_ids(a, en);
-      Act<8> fg;
-      zero(fg);
-      mma<8, 1>(fg, gop, w, lane, st.pp());
-      mul_(x, fg);
-      w = st.next();  // final_linear
-      Act<8> y;
-      init_vec_lds(y, st.v(), g);
-      linear<DT, 8, 4>(y, x, w, lane, st.pp());
-      silu2_<8, FAST>(y);
-      fr.act(x, f_row, g);
-      add_scaled_(x, y, silu2_unit<FAST>());  // conformation output
+      Act<8> bo;
+      init_vec_lds(bo, st.v(), g);
+#pragma unroll
+      for (int b = 0; b < 8; ++b) x.v[b] = silu2_unit<FAST>() * x.v[b] + bo.v[b];
     }
-    if constexpr (CONF) {
-      if (more) in.load_rest(a, en, g);
-      if (valid) store_row(x, reinterpret_cast<T*>(a.f_out) + (int64_t)e * HID, g);
-      continue;
-    }
+    w = st.next();  // stage 2: orig_msg_linear(res) + nbr
+  }
+  mma<8, 4>(x, fr.operand(f_row, g), w, lane);
+  res_block<DT, MODE, GC>(x, st, lane, g);
+  res_block<DT, MODE, GC>(x, st, lane, g);
+  {
+    w = st.next();  // res_connect_linear
+    Act<8> y;
+    init_vec_lds(y, st.v(), g);
+    linear<DT, 8, 4>(y, x, w, lane);
+    silu2_<8, FAST>(y);
+    fr.act(x, f_row, g);
+    add_scaled_(x, y, silu2_unit<FAST>());
+  }
+  res_block<DT, MODE, GC>(x, st, lane, g);
+  res_block<DT, MODE, GC>(x, st, lane, g);
+  {
+    w = st.next();  // final geometric gate
+    Act<8> fg;
+    zero(fg);
+    mma<8, 1>(fg, gop, w, lane);
+    mul_(x, fg);
+    w = st.next();  // final_linear
+    Act<8> y;
+    init_vec_lds(y, st.v(), g);
+    linear<DT, 8, 4>(y, x, w, lane);
+    silu2_<8, FAST>(y);
+    fr.act(x, f_row, g);
+    add_scaled_(x, y, silu2_unit<FAST>());  // conformation output
+  }
+  if constexpr (CONF) {
+    if (valid) store_row(x, reinterpret_cast<T*>(a.f_out) + (int64_t)e * HID, g);
+    return;
+  } else {
     // ---- attention scores (propagate_attention :76-91)
     const int sn = a.src[e], dn = a.dst[e];
     RawRow<T> kr, qr;  // K[src], Q[dst] in flight under the projection's MFMAs
     kr.load(qkv + (int64_t)sn * 3 * HID + HID, g);
     qr.load(qkv + (int64_t)dn * 3 * HID, g);
     w = st.next();  // edge_feats_projection(BN1e(conf))
-    if (FINAL && more) in.load_rest(a, en, g);  // F of this tile is dead from here on
-    if (!FINAL && more) in.load_ids(a, en);
     Act<8> p;
     init_vec_lds(p, st.v(), g);
-    linear<DT, 8, 4>(p, x, w, lane, st.pp());
+    linear<DT, 8, 4>(p, x, w, lane);
     {
       Act<8> kq, qd;
       kr.to_act(kq);
@@ -684,7 +526,7 @@ void k_edge_layer(EdgeArgs a) {
       w = st.next();  // O_edge_feats
       Act<8> e1;
       init_vec_lds(e1, st.v(), g);
-      linear<DT, 8, 4>(e1, p, w, lane, st.pp());
+      linear<DT, 8, 4>(e1, p, w, lane);
       {
         Act<8> fa;
         fr.act(fa, f_row, g);
@@ -695,21 +537,20 @@ void k_edge_layer(EdgeArgs a) {
 #pragma unroll 1
       for (int half = 0; half < 2; ++half) {
         w = st.next();  // edge_feats_MLP.0 (BN2e folded), hidden half
-        if (half == 0 && more) in.load_rest(a, en, g);  // F of this tile is dead from here on
         Act<8> t;
         init_vec_lds(t, st.v(), g);
-        linear<DT, 8, 4>(t, e1, w, lane, st.pp());
-          silu2_<8, FAST>(t);
+        linear<DT, 8, 4>(t, e1, w, lane);
+        silu2_<8, FAST>(t);
         w = st.next();  // edge_feats_MLP.3, input half
-        linear<DT, 8, 4>(o, t, w, lane, st.pp());
-        }
+        linear<DT, 8, 4>(o, t, w, lane);
+      }
       add_(e1, o);
       if (valid) store_edge_row(e1, reinterpret_cast<T*>(a.f_out) + (int64_t)e * HID, g);
-      if constexpr (GC) continue;  // no silu(nbr_linear(F)) rows for the next layer
+      if constexpr (GC) return;  // no silu(nbr_linear(F)) rows for the next layer
       w = st.next();  // next layer's silu(nbr_linear(.))
       Act<8> fn;
       init_vec_lds(fn, st.v(), g);
-      linear<DT, 8, 4>(fn, e1, w, lane, st.pp());
+      linear<DT, 8, 4>(fn, e1, w, lane);
       silu_<8, FAST>(fn);
       if (valid) store_edge_row(fn, reinterpret_cast<T*>(a.fn_out) + (int64_t)e * HID, g);
     }
@@ -718,64 +559,39 @@ void k_edge_layer(EdgeArgs a) {
 
 // ================================================================ fused edge layer, grouped form (bf16)
 // The same stage sequence and arithmetic as k_edge_layer<BF16T, 0/1>, with each wave carrying
-// LG independent 16-row groups through every weight stage (LG = 2: 128 rows per 4-wave block and
-// weight pass, so every LDS-DMA'd stage and every stage barrier serves twice the rows of
-// k_edge_layer; two blocks per CU as before). Within a stage the groups are computed one after
-// the other from the same LDS slot: their chains are independent, so one group's SiLU VALU work
-// can issue beside the other group's MFMAs.
-// Register diet (two waves per SIMD at 240 registers): one tile per block (no next-tile prefetch
-// state); the edge's own row F is re-read (L2-hot) for each of its uses instead of being held;
-// the dist gate is computed k-step by k-step and multiplied straight into the packed
-// downward_proj operand; the edge FFN accumulates into the residual e1.
-#ifndef DI_LEAN_NW
-#define DI_LEAN_NW 4
-#endif
-#ifndef DI_LEAN_G
-#define DI_LEAN_G 2
-#endif
-#ifndef DI_LEAN_VGPR
-#define DI_LEAN_VGPR 120  // x2 on gfx950 (unified file counted in pairs): 240 registers
-#endif
-#ifndef DI_LEAN_WPE
-#define DI_LEAN_WPE 2
-#endif
+// TWO independent 16-row groups through every weight stage (128 rows per 4-wave block and weight
+// pass, so every LDS-DMA'd stage and every stage barrier serves twice the rows of k_edge_layer;
+// two blocks per CU as before). Every LDS A fragment feeds one MFMA per group (mma_ring2: half
+// the ds_reads per row; tools/diag/mfma_shape_bench.hip V1 vs V0: 336 vs 375 us on the bare
+// compute core).
+// Register diet (two waves per SIMD at 240 registers): one tile per block; the edge's own row F
+// is re-read (L2-hot) for each of its uses instead of being held; the dist gate is computed
+// k-step by k-step and multiplied straight into the packed downward_proj operand; the edge FFN
+// accumulates into the residual e1.
+// Measured alternatives (round 2): one group per wave at 2-4 waves per SIMD, 8-wave
+// blocks, single-slot stages at 3-4 blocks per CU, the ResBlocks in packed f16, F held in
+// registers, fragment depth 3 / 6, no scheduling fences -- all slower or equal.
+struct Lean : KernelGeo<4> {
+  static constexpr int LG = 2;  // 16-row groups per wave
+  static constexpr int GROUP_ROWS = ROWS;
+  static constexpr int ROWS_ALL = GROUP_ROWS * LG;
+};
 // scheduling fence between row groups / phases (keeps the compiler from interleaving, and so
-// doubling the live state of, independent groups)
-#ifndef DI_LEAN_FENCE
-#define DI_LEAN_FENCE 1
-#endif
-// The memory clobber also keeps the groups' reads of the same LDS slot (A fragments, biases)
-// from being merged into one live copy shared by both groups.
-#define DI_FENCE()                                \
-  do {                                            \
-    if (DI_LEAN_FENCE) {                          \
-      asm volatile("" ::: "memory");              \
-      __builtin_amdgcn_sched_barrier(0);          \
-    }                                             \
-  } while (0)
-// MFMA chains of the lean kernel: the explicitly pipelined fragment ring (common.h mma_ring) by
-// default, which bounds the live A fragments (the compiler otherwise hoists most of a layer's
-// ds_reads and needs ~40 more registers)
-#ifndef DI_LEAN_RING
-#define DI_LEAN_RING 1
-#endif
-template <int NBO, int NS>
-__device__ __forceinline__ void lmma(Act<NBO>& out, const Op<BF16T, NS>& op, const u16* w, int lane) {
-  if constexpr (DI_LEAN_RING) mma_ring<NBO, NS>(out, op, w, lane);
-  else mma<NBO, NS>(out, op, w, lane);
+// doubling the live state of, independent groups). The memory clobber also keeps the groups'
+// reads of the same LDS slot (A fragments, biases) from being merged into one live copy shared by
+// both groups.
+__device__ __forceinline__ void lean_fence() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
 }
 // Both row groups through one pass over the stage's A fragments: every LDS fragment read feeds
-// one MFMA per group (half the ds_reads per row; tools/diag/mfma_shape_bench.hip V1 vs V0:
-// 336 vs 375 us on the bare compute core). Both groups' accumulators are live across the loop.
-#ifndef DI_LEAN_SHARE
-#define DI_LEAN_SHARE 1
-#endif
+// one MFMA per group. Both groups' accumulators are live across the loop.
 template <int NBO, int NS>
 __device__ __forceinline__ void mma_ring2(Act<NBO>& o0, Act<NBO>& o1, const Op<BF16T, NS>& a0, const Op<BF16T, NS>& a1,
                                           const u16* w, int lane) {
   constexpr int G = NBO < 2 ? NBO : 2;
   constexpr int N = NBO * NS;
-  constexpr int D = DI_MMA_DEPTH < N ? DI_MMA_DEPTH : N;
+  constexpr int D = MMA_DEPTH < N ? MMA_DEPTH : N;
   auto blk = [](int i) { return (i / (G * NS)) * G + (i % G); };
   auto kst = [](int i) { return (i % (G * NS)) / G; };
   bf16x8 fr[D];
@@ -793,52 +609,24 @@ __device__ __forceinline__ void mma_ring2(Act<NBO>& o0, Act<NBO>& o1, const Op<B
   }
   __builtin_amdgcn_sched_barrier(0);
 }
-// out[q] (= bias or 0) += W . op[q] for every row group
-template <int LG, int NBO, int NS>
-__device__ __forceinline__ void lin_groups(Act<NBO> (&out)[LG], const Op<BF16T, NS> (&op)[LG], const u16* w,
-                                           const float* bias, int lane, int g) {
+// out[q] (= bias or 0) += W . op[q] for both row groups
+template <int NBO, int NS>
+__device__ __forceinline__ void lin_groups(Act<NBO> (&out)[Lean::LG], const Op<BF16T, NS> (&op)[Lean::LG],
+                                           const u16* w, const float* bias, int lane, int g) {
 #pragma unroll
-  for (int q = 0; q < LG; ++q) {
+  for (int q = 0; q < Lean::LG; ++q) {
     if (bias) init_vec_lds(out[q], bias, g);
     else zero(out[q]);
   }
-  if constexpr (LG == 2 && DI_LEAN_SHARE) {
-    mma_ring2<NBO, NS>(out[0], out[1], op[0], op[1], w, lane);
-  } else {
-#pragma unroll
-    for (int q = 0; q < LG; ++q) lmma<NBO, NS>(out[q], op[q], w, lane);
-  }
+  mma_ring2<NBO, NS>(out[0], out[1], op[0], op[1], w, lane);
 }
-// DI_LEAN_HOLD_F=1: the edge's own F rows stay in registers (16 per group) from stage 2 through
-// final_linear (three uses, one read) instead of being re-read (L2 / HBM) for each use
-#ifndef DI_LEAN_HOLD_F
-#define DI_LEAN_HOLD_F 0
-#endif
-struct Lean {
-  static constexpr int NW = DI_LEAN_NW;
-  static constexpr int LG = DI_LEAN_G;
-  static constexpr int THREADS = 64 * NW;
-  static constexpr int GROUP_ROWS = ROWS_PER_WAVE * NW;
-  static constexpr int ROWS = GROUP_ROWS * LG;
-  static constexpr bool SHARED = LG == 2 && DI_LEAN_SHARE;  // groups share each A fragment
-};
-// DI_LEAN_DBUF=0: one synchronous stage slot per block (36.5 KiB), so three or four blocks fit in
-// a CU's LDS; each block's DMA wait is then covered by the other blocks' compute
-#ifndef DI_LEAN_DBUF
-#define DI_LEAN_DBUF 1
-#endif
-using LeanPipe = WPipe<u16, Lean::NW, DI_LEAN_DBUF != 0, EL_CAP, 128>;
+using LeanPipe = WPipe<u16, Lean::NW, true, EL_CAP, 128>;
 
 // stage sequencer of one tile: next() publishes stage i and issues the DMA of stage i + 1.
 // GC (DI_GRAPH_GEO_REF batches): the sequence starts at orig_msg_linear (stages 0-1, the neighbour
 // messages, are exactly zero), which then carries the orig_msg_linear bias, and (intermediate
 // layers) ends before the next layer's nbr_linear (its gathered rows are never needed).
-// DI_LEAN_F16RES: the 12 ResBlock stages read the f16 copies of their matrices (EL_R16_*) and run
-// their first two layers' SiLU in packed f16 (lean_res_block)
-#ifndef DI_LEAN_F16RES
-#define DI_LEAN_F16RES 0
-#endif
-template <int NS, bool GC = false, bool FINAL = false>
+template <int NS, bool GC = false>
 struct LeanStages {
   LeanPipe& pipe;
   const u16* W;
@@ -847,12 +635,7 @@ struct LeanStages {
   __device__ void issue(int s) {
     const int si = GC ? s + 2 : s;
     const int vo = (GC && s == 0) ? ELV_OM : EL_VEC[si];
-    int off = EL_ORDER[si];
-    if constexpr (DI_LEAN_F16RES) {
-      const int r = (si >= 3 && si <= 8) ? si - 3 : ((si >= 10 && si <= 15) ? si - 4 : -1);
-      if (r >= 0) off = (FINAL ? EL_R16_FIN : EL_R16_INT) + r * MAT128;
-    }
-    pipe.issue(W + off * BLK, EL_SIZE[si], vo >= 0 ? V + vo : nullptr, 128);
+    pipe.issue(W + EL_ORDER[si] * BLK, EL_SIZE[si], vo >= 0 ? V + vo : nullptr, 128);
   }
   __device__ const u16* next() {
     const u16* w = pipe.next();
@@ -869,7 +652,7 @@ __device__ __forceinline__ void lin_op(Act<NBO>& y, const Op<BF16T, NS>& x, cons
                                        int g) {
   if (bias) init_vec_lds(y, bias, g);
   else zero(y);
-  lmma<NBO, NS>(y, x, w, lane);
+  mma_ring<NBO, NS>(y, x, w, lane);
 }
 
 __device__ __forceinline__ void raw_op(Op<BF16T, 4>& o, const RawRow<u16>& r) {
@@ -884,135 +667,26 @@ struct LeanRow {
   bool valid;
 };
 
-// ---- packed-f16 SiLU (DI_LEAN_F16RES): v_cvt_pk_f16_f32, SDWA v_exp_f16 / v_rcp_f16 per half,
-// v_pk_add_f16 / v_pk_mul_f16 (7 instructions per 2 values instead of 9 with the fp32 SiLU + bf16
-// pack); tools/diag/mfma_shape_bench.hip V4
-typedef _Float16 halfx8 __attribute__((ext_vector_type(8)));
-__device__ __forceinline__ uint32_t cvt_pk_f16(float a, float b) {
-  uint32_t p;
-  asm("v_cvt_pk_f16_f32 %0, %1, %2" : "=v"(p) : "v"(a), "v"(b));
-  return p;
-}
-__device__ __forceinline__ uint32_t silu2_pk_f16(float a, float b) {  // log2-unit SiLU of (a, b) as f16x2
-  uint32_t p, e, d, r, y;
-  asm("v_cvt_pk_f16_f32 %0, %1, %2" : "=v"(p) : "v"(a), "v"(b));
-  asm("v_exp_f16_sdwa %0, -%1 dst_sel:WORD_0 dst_unused:UNUSED_PAD src0_sel:WORD_0" : "=v"(e) : "v"(p));
-  asm("v_exp_f16_sdwa %0, -%1 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1" : "+v"(e) : "v"(p));
-  asm("v_pk_add_f16 %0, %1, 1.0 op_sel_hi:[1,0]" : "=v"(d) : "v"(e));
-  asm("v_rcp_f16_sdwa %0, %1 dst_sel:WORD_0 dst_unused:UNUSED_PAD src0_sel:WORD_0" : "=v"(r) : "v"(d));
-  asm("v_rcp_f16_sdwa %0, %1 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1" : "+v"(r) : "v"(d));
-  asm("v_pk_mul_f16 %0, %1, %2" : "=v"(y) : "v"(p), "v"(r));
-  return y;
-}
-template <bool SILU>
-__device__ __forceinline__ void make_op_f16(Op<BF16T, 4>& o, const Act<8>& a) {
-#pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    uint4 u;
-    if constexpr (SILU) {
-      u.x = silu2_pk_f16(a.v[2 * s][0], a.v[2 * s][1]);
-      u.y = silu2_pk_f16(a.v[2 * s][2], a.v[2 * s][3]);
-      u.z = silu2_pk_f16(a.v[2 * s + 1][0], a.v[2 * s + 1][1]);
-      u.w = silu2_pk_f16(a.v[2 * s + 1][2], a.v[2 * s + 1][3]);
-    } else {
-      u.x = cvt_pk_f16(a.v[2 * s][0], a.v[2 * s][1]);
-      u.y = cvt_pk_f16(a.v[2 * s][2], a.v[2 * s][3]);
-      u.z = cvt_pk_f16(a.v[2 * s + 1][0], a.v[2 * s + 1][1]);
-      u.w = cvt_pk_f16(a.v[2 * s + 1][2], a.v[2 * s + 1][3]);
-    }
-    o.f[s] = __builtin_bit_cast(bf16x8, u);  // f16 bits in the operand registers
-  }
-}
-// mma_ring2 with f16 operands (f16 bits in both the LDS fragments and the packed activations)
-template <int NBO, int NS>
-__device__ __forceinline__ void mma_ring2_f16(Act<NBO>& o0, Act<NBO>& o1, const Op<BF16T, NS>& a0,
-                                              const Op<BF16T, NS>& a1, const u16* w, int lane) {
-  constexpr int G = NBO < 2 ? NBO : 2;
-  constexpr int N = NBO * NS;
-  constexpr int D = DI_MMA_DEPTH < N ? DI_MMA_DEPTH : N;
-  auto blk = [](int i) { return (i / (G * NS)) * G + (i % G); };
-  auto kst = [](int i) { return (i % (G * NS)) / G; };
-  halfx8 fr[D];
-#pragma unroll
-  for (int i = 0; i < D; ++i)
-    fr[i] = *reinterpret_cast<const halfx8*>(w + (blk(i) * NS + kst(i)) * BLK + lane * 8);
-#pragma unroll
-  for (int i = 0; i < N; ++i) {
-    __builtin_amdgcn_sched_barrier(0);
-    const int bo = blk(i), s = kst(i);
-    o0.v[bo] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fr[i % D], __builtin_bit_cast(halfx8, a0.f[s]), o0.v[bo], 0, 0, 0);
-    o1.v[bo] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fr[i % D], __builtin_bit_cast(halfx8, a1.f[s]), o1.v[bo], 0, 0, 0);
-    if (i + D < N)
-      fr[i % D] = *reinterpret_cast<const halfx8*>(w + (blk(i + D) * NS + kst(i + D)) * BLK + lane * 8);
-  }
-  __builtin_amdgcn_sched_barrier(0);
-}
-
-template <int NS, bool GC, bool FINAL>
-__device__ __forceinline__ void lean_res_block(Act<8> (&x)[Lean::LG], LeanStages<NS, GC, FINAL>& st, int lane, int g) {
-  if constexpr (DI_LEAN_F16RES && Lean::SHARED) {
-    // ResBlock in f16 operands: x -> f16; layers 0, 1: SiLU straight into packed f16 operands;
-    // layer 2: fp32 SiLU into the fp32 residual stream
-    Op<BF16T, 4> op[Lean::LG];
-#pragma unroll
-    for (int q = 0; q < Lean::LG; ++q) make_op_f16<false>(op[q], x[q]);
-#pragma unroll 1
-    for (int l = 0; l < 3; ++l) {
-      const u16* w = st.next();
-      Act<8> t[Lean::LG];
-#pragma unroll
-      for (int q = 0; q < Lean::LG; ++q) init_vec_lds(t[q], st.v(), g);
-      mma_ring2_f16<8, 4>(t[0], t[1], op[0], op[1], w, lane);
-#pragma unroll
-      for (int q = 0; q < Lean::LG; ++q) {
-        DI_FENCE();
-        if (l < 2) {
-          make_op_f16<true>(op[q], t[q]);
-          pin(op[q]);
-        } else {
-          silu2_<8, true>(t[q]);
-          add_scaled_(x[q], t[q], silu2_unit<true>());
-          pin(x[q]);
-        }
-      }
-    }
-    return;
-  }
+template <int NS, bool GC>
+__device__ __forceinline__ void lean_res_block(Act<8> (&x)[Lean::LG], LeanStages<NS, GC>& st, int lane, int g) {
   Op<BF16T, 4> op[Lean::LG];
 #pragma unroll
   for (int q = 0; q < Lean::LG; ++q) make_op(op[q], x[q]);
 #pragma unroll 1
   for (int l = 0; l < 3; ++l) {
     const u16* w = st.next();
-    if constexpr (Lean::SHARED) {
-      Act<8> t[Lean::LG];
-      lin_groups<Lean::LG, 8, 4>(t, op, w, st.v(), lane, g);
+    Act<8> t[Lean::LG];
+    lin_groups<8, 4>(t, op, w, st.v(), lane, g);
 #pragma unroll
-      for (int q = 0; q < Lean::LG; ++q) {
-        DI_FENCE();
-        silu2_<8, true>(t[q]);
-        if (l < 2) {
-          make_op(op[q], t[q]);
-          pin(op[q]);
-        } else {
-          add_scaled_(x[q], t[q], silu2_unit<true>());
-          pin(x[q]);
-        }
-      }
-    } else {
-#pragma unroll
-      for (int q = 0; q < Lean::LG; ++q) {
-        DI_FENCE();
-        Act<8> t;
-        lin_op<8, 4>(t, op[q], w, st.v(), lane, g);
-        silu2_<8, true>(t);  // log2 units: folded into the next linear / the residual fma
-        if (l < 2) {
-          make_op(op[q], t);
-          pin(op[q]);
-        } else {
-          add_scaled_(x[q], t, silu2_unit<true>());
-          pin(x[q]);
-        }
+    for (int q = 0; q < Lean::LG; ++q) {
+      lean_fence();
+      silu2_<8, true>(t[q]);  // log2 units: folded into the next linear / the residual fma
+      if (l < 2) {
+        make_op(op[q], t[q]);
+        pin(op[q]);
+      } else {
+        add_scaled_(x[q], t[q], silu2_unit<true>());
+        pin(x[q]);
       }
     }
   }
@@ -1028,45 +702,29 @@ __device__ __forceinline__ void load_f(RawRow<u16> (&fr)[Lean::LG], const u16* c
 
 __device__ __forceinline__ void lean_f_residual(Act<8> (&x)[Lean::LG], const u16* w, const float* v,
                                                 const RawRow<u16> (&fr)[Lean::LG], int lane, int g) {
-  if constexpr (Lean::SHARED) {
-    Op<BF16T, 4> op[Lean::LG];
+  Op<BF16T, 4> op[Lean::LG];
 #pragma unroll
-    for (int q = 0; q < Lean::LG; ++q) make_op(op[q], x[q]);
-    Act<8> y[Lean::LG];
-    lin_groups<Lean::LG, 8, 4>(y, op, w, v, lane, g);
-#pragma unroll
-    for (int q = 0; q < Lean::LG; ++q) {
-      DI_FENCE();
-      silu2_<8, true>(y[q]);
-      fr[q].to_act(x[q]);
-      add_scaled_(x[q], y[q], silu2_unit<true>());
-      pin(x[q]);
-    }
-    return;
-  }
+  for (int q = 0; q < Lean::LG; ++q) make_op(op[q], x[q]);
+  Act<8> y[Lean::LG];
+  lin_groups<8, 4>(y, op, w, v, lane, g);
 #pragma unroll
   for (int q = 0; q < Lean::LG; ++q) {
-    DI_FENCE();
-    Op<BF16T, 4> op;
-    make_op(op, x[q]);
-    Act<8> y;
-    lin_op<8, 4>(y, op, w, v, lane, g);
-    silu2_<8, true>(y);
+    lean_fence();
+    silu2_<8, true>(y[q]);
     fr[q].to_act(x[q]);
-    add_scaled_(x[q], y, silu2_unit<true>());
+    add_scaled_(x[q], y[q], silu2_unit<true>());
     pin(x[q]);
   }
 }
 
 template <int MODE, bool GC>
-__global__ __attribute__((amdgpu_flat_work_group_size(1, 64 * DI_LEAN_NW), amdgpu_waves_per_eu(DI_LEAN_WPE, DI_LEAN_WPE),
-                          amdgpu_num_vgpr(DI_LEAN_VGPR)))
+__global__ __attribute__((amdgpu_flat_work_group_size(1, Lean::THREADS), amdgpu_waves_per_eu(2, 2),
+                          amdgpu_num_vgpr(120)))
 void k_edge_lean(EdgeArgs a) {
   constexpr bool FINAL = MODE == 1;
   constexpr int NS = (FINAL ? EL_NSTAGE_FINAL : EL_NSTAGE) - (GC ? (FINAL ? 2 : 3) : 0);
   constexpr int LG = Lean::LG;
-  DI_GEOT_ENTRY();
-  __shared__ __attribute__((aligned(16))) char lds[(DI_LEAN_DBUF ? 2 : 1) * LeanPipe::SLOT_BYTES];
+  __shared__ __attribute__((aligned(16))) char lds[2 * LeanPipe::SLOT_BYTES];
   const int lane = lane_id(), g = lane >> 4;
   const u16* fn_in = reinterpret_cast<const u16*>(a.fn_in);
   const u16* qkv = reinterpret_cast<const u16*>(a.qkv);
@@ -1074,21 +732,21 @@ void k_edge_lean(EdgeArgs a) {
   const u16* f_row[LG];
 #pragma unroll
   for (int q = 0; q < LG; ++q) {
-    DI_FENCE();
-    const int r = blockIdx.x * Lean::ROWS + q * Lean::GROUP_ROWS + (threadIdx.x >> 6) * ROWS_PER_WAVE + (threadIdx.x & 15);
+    lean_fence();
+    const int r = blockIdx.x * Lean::ROWS_ALL + q * Lean::GROUP_ROWS + (threadIdx.x >> 6) * ROWS_PER_WAVE + (threadIdx.x & 15);
     rw[q].valid = r < a.Et;
     rw[q].e = rw[q].valid ? r : a.Et - 1;
     f_row[q] = reinterpret_cast<const u16*>(a.f_in) + (int64_t)rw[q].e * HID;
   }
 
   LeanPipe pipe(lds);
-  LeanStages<NS, GC, FINAL> st{pipe, reinterpret_cast<const u16*>(a.wmat), a.wvec, 0};
+  LeanStages<NS, GC> st{pipe, reinterpret_cast<const u16*>(a.wmat), a.wvec, 0};
   st.issue(0);
 
   Op<BF16T, 1> gop[LG];
 #pragma unroll
   for (int q = 0; q < LG; ++q) {
-    DI_FENCE();
+    lean_fence();
     Act<2> geo;
     load_edge_geo(geo, a.edge_f + (int64_t)rw[q].e * NFEAT_E, g);
     make_op(gop[q], geo);
@@ -1111,39 +769,38 @@ void k_edge_lean(EdgeArgs a) {
     // ---- neighbour-edge messages (conformation_module_message_func :384-418)
     w = st.next();  // stage 0: geometric gates + downward_proj
     Act<4> s[LG];
-  #pragma unroll
+#pragma unroll
     for (int q = 0; q < LG; ++q) {
-      DI_FENCE();
+      lean_fence();
       Act<4> gate;
       {
         Act<4> t1;
         zero(gate);
-        lmma<4, 1>(gate, gop[q], w + 8 * BLK, lane);
+        mma_ring<4, 1>(gate, gop[q], w + 8 * BLK, lane);
         zero(t1);
-        lmma<4, 1>(t1, gop[q], w + 12 * BLK, lane);
+        mma_ring<4, 1>(t1, gop[q], w + 12 * BLK, lane);
         mul_(gate, t1);
         zero(t1);
-        lmma<4, 1>(t1, gop[q], w + 16 * BLK, lane);
+        mma_ring<4, 1>(t1, gop[q], w + 16 * BLK, lane);
         mul_(gate, t1);
         pin(gate);
       }
       zero(s[q]);
       const int4 nbq = nb;
       if (q + 1 < LG) nb = *reinterpret_cast<const int4*>(a.nbr + (int64_t)rw[q + 1].e * 4);
-  #pragma unroll
+#pragma unroll
       for (int j = 0; j < 4; ++j) {
-        DI_FENCE();
+        lean_fence();
         // x = silu(nbr_linear(F))[nbr_j] * dist gate, packed k-step by k-step
         Op<BF16T, 4> xop;
-  #pragma unroll
+#pragma unroll
         for (int ks = 0; ks < 4; ++ks) {
           // recomputed per neighbour (2 MFMAs per k-step) rather than held live across the loop:
           // the memory clobber stops the compiler from merging the neighbours' copies (32 VGPRs)
-          asm volatile("" ::: "memory");
-          DI_FENCE();
+          lean_fence();
           Act<2> dg;
           zero(dg);
-          lmma<2, 1>(dg, gop[q], w + 2 * ks * BLK, lane);
+          mma_ring<2, 1>(dg, gop[q], w + 2 * ks * BLK, lane);
           // opaque until here: keeps the compiler from unpacking the whole gathered row to fp32 as
           // soon as it lands (32 registers instead of 16)
           asm volatile("" : "+v"(xn.u[2 * ks]), "+v"(xn.u[2 * ks + 1]));
@@ -1166,29 +823,29 @@ void k_edge_lean(EdgeArgs a) {
         } else if (q + 1 < LG) {
           xn.load(fn_in + (int64_t)nb.x * HID, g);
         }
-        DI_FENCE();
+        lean_fence();
         Act<4> y;
         zero(y);
-        lmma<4, 4>(y, xop, w + 20 * BLK, lane);  // downward_proj
-  #pragma unroll
+        mma_ring<4, 4>(y, xop, w + 20 * BLK, lane);  // downward_proj
+#pragma unroll
         for (int b = 0; b < 4; ++b)
-  #pragma unroll
+#pragma unroll
           for (int r = 0; r < 4; ++r) s[q].v[b][r] += silu2<true>(y.v[b][r]) * gate.v[b][r];
         pin(s[q]);
       }
     }
     {
       w = st.next();  // stage 1: upward_proj (+ orig_msg_linear bias)
-  #pragma unroll
+#pragma unroll
       for (int q = 0; q < LG; ++q) {
-      DI_FENCE();
+        lean_fence();
         Op<BF16T, 2> sop;
         make_op(sop, s[q]);
         lin_op<8, 2>(x[q], sop, w, nullptr, lane, g);
         silu2_<8, true>(x[q]);
         Act<8> bo;
         init_vec_lds(bo, st.v(), g);
-  #pragma unroll
+#pragma unroll
         for (int b = 0; b < 8; ++b) x[q].v[b] = silu2_unit<true>() * x[q].v[b] + bo.v[b];
         pin(x[q]);
       }
@@ -1197,27 +854,16 @@ void k_edge_lean(EdgeArgs a) {
     w = st.next();  // stage 2: orig_msg_linear(res) + nbr
   }
   {
-    if constexpr (Lean::SHARED) {
-      Op<BF16T, 4> fop[LG];
+    Op<BF16T, 4> fop[LG];
 #pragma unroll
-      for (int q = 0; q < LG; ++q) raw_op(fop[q], fr[q]);
-      mma_ring2<8, 4>(x[0], x[1], fop[0], fop[1], w, lane);
+    for (int q = 0; q < LG; ++q) raw_op(fop[q], fr[q]);
+    mma_ring2<8, 4>(x[0], x[1], fop[0], fop[1], w, lane);
 #pragma unroll
-      for (int q = 0; q < LG; ++q) pin(x[q]);
-    } else {
-#pragma unroll
-      for (int q = 0; q < LG; ++q) {
-        DI_FENCE();
-        Op<BF16T, 4> fop;
-        raw_op(fop, fr[q]);
-        lmma<8, 4>(x[q], fop, w, lane);
-        pin(x[q]);
-      }
-    }
+    for (int q = 0; q < LG; ++q) pin(x[q]);
   }
   lean_res_block(x, st, lane, g);
   lean_res_block(x, st, lane, g);
-  if (!DI_LEAN_HOLD_F) load_f(fr, f_row, g);
+  load_f(fr, f_row, g);
   w = st.next();  // res_connect_linear: x = F + silu(rc(x))
   lean_f_residual(x, w, st.v(), fr, lane, g);
   lean_res_block(x, st, lane, g);
@@ -1225,14 +871,14 @@ void k_edge_lean(EdgeArgs a) {
   w = st.next();  // final geometric gate
 #pragma unroll
   for (int q = 0; q < LG; ++q) {
-    DI_FENCE();
+    lean_fence();
     Act<8> fg;
     zero(fg);
-    lmma<8, 1>(fg, gop[q], w, lane);
+    mma_ring<8, 1>(fg, gop[q], w, lane);
     mul_(x[q], fg);
     pin(x[q]);
   }
-  if (!DI_LEAN_HOLD_F) load_f(fr, f_row, g);
+  load_f(fr, f_row, g);
   w = st.next();  // final_linear: x = F + silu(final(x)) = conformation output
   lean_f_residual(x, w, st.v(), fr, lane, g);
 
@@ -1240,32 +886,25 @@ void k_edge_lean(EdgeArgs a) {
   RawRow<u16> kr[LG], qr[LG];  // K[src], Q[dst]: issued before the stage barrier
 #pragma unroll
   for (int q = 0; q < LG; ++q) {
-    DI_FENCE();
+    lean_fence();
     const int e = rw[q].e;
     kr[q].load(qkv + (int64_t)a.src[e] * 3 * HID + HID, g);
     qr[q].load(qkv + (int64_t)a.dst[e] * 3 * HID, g);
   }
   w = st.next();  // edge_feats_projection(BN1e(conf))
   Op<BF16T, 4> pop[LG];
-  Act<8> pg[Lean::SHARED ? LG : 1];
-  if constexpr (Lean::SHARED) {
+  Act<8> pg[LG];
+  {
     Op<BF16T, 4> xop[LG];
 #pragma unroll
     for (int q = 0; q < LG; ++q) make_op(xop[q], x[q]);
-    lin_groups<LG, 8, 4>(pg, xop, w, st.v(), lane, g);
+    lin_groups<8, 4>(pg, xop, w, st.v(), lane, g);
   }
 #pragma unroll
   for (int q = 0; q < LG; ++q) {
-    DI_FENCE();
+    lean_fence();
     const int e = rw[q].e;
-    Act<8> p;
-    if constexpr (Lean::SHARED) {
-      p = pg[q];
-    } else {
-      Op<BF16T, 4> op;
-      make_op(op, x[q]);
-      lin_op<8, 4>(p, op, w, st.v(), lane, g);
-    }
+    Act<8> p = pg[q];
     Act<8> kq, qd;
     kr[q].to_act(kq);
     qr[q].to_act(qd);
@@ -1291,14 +930,10 @@ void k_edge_lean(EdgeArgs a) {
     load_f(fr, f_row, g);  // O_edge: re-read (the attention stage has no room for it)
     w = st.next();  // O_edge_feats
     Act<8> e1[LG];
-    if constexpr (Lean::SHARED) lin_groups<LG, 8, 4>(e1, pop, w, st.v(), lane, g);
+    lin_groups<8, 4>(e1, pop, w, st.v(), lane, g);
 #pragma unroll
     for (int q = 0; q < LG; ++q) {
-      DI_FENCE();
-      if constexpr (!Lean::SHARED) {
-        init_vec_lds(e1[q], st.v(), g);
-        lmma<8, 4>(e1[q], pop[q], w, lane);
-      }
+      lean_fence();
       Act<8> fa;
       fr[q].to_act(fa);
       add_(e1[q], fa);
@@ -1314,68 +949,38 @@ void k_edge_lean(EdgeArgs a) {
     for (int half = 0; half < 2; ++half) {
       w = st.next();  // edge_feats_MLP.0 (BN2e folded), hidden half
       Op<BF16T, 4> top[LG];
-      if constexpr (Lean::SHARED) {
-        Act<8> t[LG];
-        lin_groups<LG, 8, 4>(t, eop, w, st.v(), lane, g);
+      Act<8> t[LG];
+      lin_groups<8, 4>(t, eop, w, st.v(), lane, g);
 #pragma unroll
-        for (int q = 0; q < LG; ++q) {
-          DI_FENCE();
-          silu2_<8, true>(t[q]);
-          make_op(top[q], t[q]);
-          pin(top[q]);
-        }
-      } else {
-#pragma unroll
-        for (int q = 0; q < LG; ++q) {
-          DI_FENCE();
-          Act<8> t;
-          lin_op<8, 4>(t, eop[q], w, st.v(), lane, g);
-          silu2_<8, true>(t);
-          make_op(top[q], t);
-          pin(top[q]);
-        }
+      for (int q = 0; q < LG; ++q) {
+        lean_fence();
+        silu2_<8, true>(t[q]);
+        make_op(top[q], t[q]);
+        pin(top[q]);
       }
       w = st.next();  // edge_feats_MLP.3, input half: accumulated into the residual
-      if constexpr (Lean::SHARED) {
-        mma_ring2<8, 4>(e1[0], e1[1], top[0], top[1], w, lane);
+      mma_ring2<8, 4>(e1[0], e1[1], top[0], top[1], w, lane);
 #pragma unroll
-        for (int q = 0; q < LG; ++q) pin(e1[q]);
-      } else {
-#pragma unroll
-        for (int q = 0; q < LG; ++q) {
-          DI_FENCE();
-          lmma<8, 4>(e1[q], top[q], w, lane);
-          pin(e1[q]);
-        }
-      }
+      for (int q = 0; q < LG; ++q) pin(e1[q]);
     }
 #pragma unroll
     for (int q = 0; q < LG; ++q) {
-    DI_FENCE();
+      lean_fence();
       if (rw[q].valid) store_edge_row(e1[q], reinterpret_cast<u16*>(a.f_out) + (int64_t)rw[q].e * HID, g);
       make_op(eop[q], e1[q]);
     }
     if constexpr (GC) return;  // the next layer gathers no silu(nbr_linear(F)) rows
     w = st.next();  // next layer's silu(nbr_linear(.))
-    Act<8> fng[Lean::SHARED ? LG : 1];
-    if constexpr (Lean::SHARED) lin_groups<LG, 8, 4>(fng, eop, w, st.v(), lane, g);
+    Act<8> fng[LG];
+    lin_groups<8, 4>(fng, eop, w, st.v(), lane, g);
 #pragma unroll
     for (int q = 0; q < LG; ++q) {
-      DI_FENCE();
-      Act<8> fn;
-      if constexpr (Lean::SHARED) fn = fng[q];
-      else lin_op<8, 4>(fn, eop[q], w, st.v(), lane, g);
-      silu_<8, true>(fn);
-      if (rw[q].valid) store_edge_row(fn, reinterpret_cast<u16*>(a.fn_out) + (int64_t)rw[q].e * HID, g);
+      lean_fence();
+      silu_<8, true>(fng[q]);
+      if (rw[q].valid) store_edge_row(fng[q], reinterpret_cast<u16*>(a.fn_out) + (int64_t)rw[q].e * HID, g);
     }
   }
 }
-
-// edge-layer kernel choice (di_edge_config): 0 = k_edge_layer (two 4-wave blocks per CU, 16 rows
-// per wave), 1 = k_edge_lean (two 4-wave blocks per CU, Lean::LG = 2 16-row groups per wave sharing
-// every A fragment; default: C3 micro-batch alone 446 vs 496 us, final 350 vs 383 us, overlapped
-// 5.3-5.4 k vs 5.2 k complexes/s)
-static int g_edge_kernel = 1;
 
 // ================================================================ node aggregation (CSR segment sum)
 // h_attn[v] = sum_{e in in(v)} alpha[e, head] * V[src e]  /  (sum_e alpha[e, head] + 1e-6)
@@ -1486,8 +1091,12 @@ __device__ __forceinline__ void nu_wait_younger(int n_stages_younger) {
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+// each of the 4 waves issues exactly NU_STAGE * BLK * 2 / 1024 / 4 = 8 one-KiB pieces per stage:
+// the vmcnt immediates of nu_wait_younger assume that split
+using NodeRingGeo = KernelGeo<4>;
+static_assert(NU_STAGE * BLK * 2 / 1024 / NodeRingGeo::NW == 8, "nu_wait_younger counts 8 pieces per wave");
 template <bool FINAL>
-__global__ __launch_bounds__(THREADS, 1) void k_node_update_ring(NodeArgs a) {
+__global__ __launch_bounds__(NodeRingGeo::THREADS, 1) void k_node_update_ring(NodeArgs a) {
   constexpr int NS = FINAL ? 5 : 8;
   constexpr int NVEC = FINAL ? NLV_N_FINAL : NLV_N;
   // one LDS object: [4 ring slots | all biases]
@@ -1495,7 +1104,7 @@ __global__ __launch_bounds__(THREADS, 1) void k_node_update_ring(NodeArgs a) {
   u16* wring = reinterpret_cast<u16*>(lds);
   float* vlds = reinterpret_cast<float*>(lds + NU_SLOTS * NU_STAGE * BLK * 2);
   const int lane = lane_id(), g = lane >> 4;
-  const int r = row_id<WAVES>();
+  const int r = row_id<NodeRingGeo::NW>();
   const bool valid = r < a.Nt;
   const int v = valid ? r : a.Nt - 1;
   const u16* W = reinterpret_cast<const u16*>(a.wmat);
@@ -1503,10 +1112,10 @@ __global__ __launch_bounds__(THREADS, 1) void k_node_update_ring(NodeArgs a) {
   auto stage_blk = [](int s) {
     return s == 0 ? NL_ON : (s == 1 ? NL_F1 : (s == 2 ? NL_F2 : (s == 3 ? NL_F1 + MAT128 : (s == 4 ? NL_F2 + MAT128 : NL_Q + MAT128 * (s - 5)))));
   };
-  auto issue = [&](int s) { dma_blocks<WAVES>(wring + (s % NU_SLOTS) * NU_STAGE * BLK, W + stage_blk(s) * BLK, NU_STAGE); };
+  auto issue = [&](int s) { dma_blocks<NodeRingGeo::NW>(wring + (s % NU_SLOTS) * NU_STAGE * BLK, W + stage_blk(s) * BLK, NU_STAGE); };
   // biases and stage 0, then this node's rows, landed here (the compiler cannot count the DMA
   // loops, so a row used later would make it wait for every stage in flight), then stages 1-2
-  dma_vec<WAVES>(vlds, a.wvec, NVEC / 128);
+  dma_vec<NodeRingGeo::NW>(vlds, a.wvec, NVEC / 128);
   issue(0);
   RawRow<u16> hin;
   hin.load(reinterpret_cast<const u16*>(a.h_in) + (int64_t)v * HID, g);
@@ -1596,16 +1205,26 @@ __global__ __launch_bounds__(THREADS, 1) void k_node_update_ring(NodeArgs a) {
 // consumed after a DMA issue makes the wave wait for the whole in-flight weight stage (vmcnt
 // counts in order, and the compiler cannot count a runtime-length DMA loop), which exposed the
 // DMA latency at every stage.
+// Launch geometry of k_node_layer (di_node_layer, and di_node_update's fp32 path): DI_NODE_NW
+// waves (16 nodes each) per block. Round 2's 2-wave build faulted (code 719) because
+// di_node_update's fp32 launch kept a hard-coded 256-thread block while the kernel had been
+// compiled for 128 (__launch_bounds__(64 * 2)): every launch site now takes its shape from
+// NodeGeo. A C3 micro-batch has 16k nodes: 4-wave blocks give 250 blocks, 2-wave blocks 500
+// (measured beside the pair stream 58 vs 55 us per launch, so 4 is the default; the 2-wave build
+// is a tested variant, tools/build_variants.py "node2").
+#ifndef DI_NODE_NW
+#define DI_NODE_NW 4
+#endif
+using NodeGeo = KernelGeo<DI_NODE_NW>;
 template <class DT, bool FINAL>
-__global__ __launch_bounds__(THREADS, 2) void k_node_layer(NodeArgs a) {
+__global__ __launch_bounds__(NodeGeo::THREADS, 2) void k_node_layer(NodeArgs a) {
   using T = typename DT::T;
-  DI_GEOT_ENTRY();
   constexpr bool FAST = DT::kBF16;
   constexpr bool DB = DT::kBF16;
-  using Pipe = WPipe<T, WAVES, DB, MAT128, 128>;
+  using Pipe = WPipe<T, NodeGeo::NW, DB, MAT128, 128>;
   __shared__ __attribute__((aligned(16))) char lds[(DB ? 2 : 1) * Pipe::SLOT_BYTES];
   const int lane = lane_id(), g = lane >> 4;
-  const int r = row_id<WAVES>();
+  const int r = row_id<NodeGeo::NW>();
   const bool valid = r < a.Nt;
   const int v = valid ? r : a.Nt - 1;
   const T* W = reinterpret_cast<const T*>(a.wmat);
@@ -1726,26 +1345,23 @@ __global__ __launch_bounds__(THREADS, 2) void k_node_layer(NodeArgs a) {
 // ================================================================ C ABI
 using namespace di;
 
-static inline int grid_rows(int n, int rows = ROWS_PER_BLOCK) { return (n + rows - 1) / rows; }
-
-static inline int num_cus() {
-  static const int n = [] {
-    int dev = 0, v = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0)
-      v = 256;
-    return v;
-  }();
-  return n;
-}
+// grid / block of a launch, both from the kernel's geometry struct
+template <class Geom>
+static inline dim3 grid_of(int n) { return dim3((unsigned)((n + Geom::ROWS - 1) / Geom::ROWS)); }
+template <class Geom>
+static inline dim3 block_of() { return dim3(Geom::THREADS); }
 
 static inline int launch_status() {
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? DI_OK : (int)e;
 }
 
+static inline bool dtype_ok(di_dtype dt) { return dt == DI_BF16 || dt == DI_F32; }
+
 extern "C" int di_abi_version(void) { return DI_ABI_VERSION; }
 
 extern "C" int64_t di_blob_bytes(int kind, di_dtype dtype, int vec) {
+  if (!dtype_ok(dtype)) return -1;
   const int64_t esz = dtype == DI_BF16 ? 2 : 4;
   int64_t blk = 0, nvec = 0;
   switch (kind) {
@@ -1763,14 +1379,15 @@ extern "C" int64_t di_blob_bytes(int kind, di_dtype dtype, int vec) {
 
 extern "C" int di_node_embed(const di_graph* g, di_dtype dt, int32_t in_dim, const float* node_f, const void* wmat,
                              const float* wvec, void* h_out, void* qkv_out, void* stream) {
-  if (!g || !node_f || !wmat || !wvec || !h_out || !qkv_out || g->num_nodes <= 0 || in_dim <= 0 || in_dim > HID)
+  if (!g || !node_f || !wmat || !wvec || !h_out || !qkv_out || g->num_nodes <= 0 || in_dim <= 0 || in_dim > HID ||
+      !dtype_ok(dt))
     return DI_EINVAL;
   EmbedArgs a{g->num_nodes, in_dim, node_f, wmat, wvec, h_out, qkv_out};
   hipStream_t s = (hipStream_t)stream;
   if (dt == DI_BF16)
-    hipLaunchKernelGGL(k_node_embed<BF16T>, dim3(grid_rows(a.Nt)), dim3(THREADS), 0, s, a);
+    hipLaunchKernelGGL(k_node_embed<BF16T>, grid_of<EmbedGeo>(a.Nt), block_of<EmbedGeo>(), 0, s, a);
   else
-    hipLaunchKernelGGL(k_node_embed<F32T>, dim3(grid_rows(a.Nt)), dim3(THREADS), 0, s, a);
+    hipLaunchKernelGGL(k_node_embed<F32T>, grid_of<EmbedGeo>(a.Nt), block_of<EmbedGeo>(), 0, s, a);
   return launch_status();
 }
 
@@ -1779,13 +1396,13 @@ extern "C" int di_init_edge(const di_graph* g, di_dtype dt, const float* edge_f,
                             void* f_out, void* fn_out, void* stream) {
   const bool gc = (g ? g->flags : 0) & DI_GRAPH_GEO_REF;
   if (!g || !edge_f || !wmat || !wvec || !pos_src_tab || !pos_dst_tab || !f_out || (!fn_out && !gc) ||
-      g->num_edges <= 0)
+      g->num_edges <= 0 || !dtype_ok(dt))
     return DI_EINVAL;
   InitArgs a{g->num_edges, edge_f, g->src, g->dst, g->node_pos, wmat, wvec, pos_src_tab, pos_dst_tab,
              f_out, fn_out};
   hipStream_t s = (hipStream_t)stream;
-  const dim3 gb(grid_rows(a.Et, InitGeo<BF16T>::ROWS)), bb(InitGeo<BF16T>::THREADS);
-  const dim3 gf(grid_rows(a.Et, InitGeo<F32T>::ROWS)), bf(InitGeo<F32T>::THREADS);
+  const dim3 gb = grid_of<InitGeo<BF16T>>(a.Et), bb = block_of<InitGeo<BF16T>>();
+  const dim3 gf = grid_of<InitGeo<F32T>>(a.Et), bf = block_of<InitGeo<F32T>>();
   if (dt == DI_BF16 && gc) hipLaunchKernelGGL((k_init_edge<BF16T, true>), gb, bb, 0, s, a);
   else if (dt == DI_BF16) hipLaunchKernelGGL((k_init_edge<BF16T, false>), gb, bb, 0, s, a);
   else if (gc) hipLaunchKernelGGL((k_init_edge<F32T, true>), gf, bf, 0, s, a);
@@ -1800,34 +1417,22 @@ extern "C" int di_edge_layer(const di_graph* g, di_dtype dt, int final_layer, co
   // DI_GRAPH_GEO_REF: the neighbour-message branch is skipped (exactly zero), fn_in is not read and
   // fn_out not written (every edge-layer kernel; di_conformation computes the branch)
   const bool gc = g && (g->flags & DI_GRAPH_GEO_REF);
-  if (!g || !edge_f || !f_in || (!fn_in && !gc) || !qkv || !wmat || !wvec || !alpha_out || g->num_edges <= 0)
+  if (!g || !edge_f || !f_in || (!fn_in && !gc) || !qkv || !wmat || !wvec || !alpha_out || g->num_edges <= 0 ||
+      !dtype_ok(dt))
     return DI_EINVAL;
   if (!final_layer && (!f_out || (!fn_out && !gc))) return DI_EINVAL;
   EdgeArgs a{g->num_edges, edge_f, g->src, g->dst, g->nbr, f_in, fn_in, qkv, wmat, wvec, alpha_out,
              f_out, fn_out};
   hipStream_t s = (hipStream_t)stream;
-  if (dt == DI_BF16 && g_edge_kernel == 1) {
-    dim3 grid(grid_rows(a.Et, Lean::ROWS)), block(Lean::THREADS);
+  if (dt == DI_BF16) {
+    // grouped form: 128 edges (two 16-row groups per wave) per 4-wave block
+    const dim3 grid((unsigned)((a.Et + Lean::ROWS_ALL - 1) / Lean::ROWS_ALL)), block = block_of<Lean>();
     if (final_layer && gc) hipLaunchKernelGGL((k_edge_lean<1, true>), grid, block, 0, s, a);
     else if (final_layer) hipLaunchKernelGGL((k_edge_lean<1, false>), grid, block, 0, s, a);
     else if (gc) hipLaunchKernelGGL((k_edge_lean<0, true>), grid, block, 0, s, a);
     else hipLaunchKernelGGL((k_edge_lean<0, false>), grid, block, 0, s, a);
-  } else if (dt == DI_BF16) {
-    // persistent: two resident blocks per CU
-#ifndef DI_EDGE_PERSIST
-#define DI_EDGE_PERSIST 0
-#endif
-    const int tiles = grid_rows(a.Et, EdgeGeo<BF16T>::ROWS);
-    // ring: one 8-wave block per CU, persistent over the tiles; barrier pipe: 2 blocks per CU
-    const int resident = (EdgeGeo<BF16T>::RING ? 1 : 2) * num_cus();
-    const bool persist = EdgeGeo<BF16T>::RING || DI_EDGE_PERSIST;
-    dim3 grid(persist && tiles > resident ? resident : xcd_grid(tiles)), block(EdgeGeo<BF16T>::THREADS);
-    if (final_layer && gc) hipLaunchKernelGGL((k_edge_layer<BF16T, 1, true>), grid, block, 0, s, a);
-    else if (final_layer) hipLaunchKernelGGL((k_edge_layer<BF16T, 1>), grid, block, 0, s, a);
-    else if (gc) hipLaunchKernelGGL((k_edge_layer<BF16T, 0, true>), grid, block, 0, s, a);
-    else hipLaunchKernelGGL((k_edge_layer<BF16T, 0>), grid, block, 0, s, a);
   } else {
-    dim3 grid(xcd_grid(grid_rows(a.Et, EdgeGeo<F32T>::ROWS))), block(EdgeGeo<F32T>::THREADS);
+    const dim3 grid = grid_of<Geo<F32T>>(a.Et), block = block_of<Geo<F32T>>();
     if (final_layer && gc) hipLaunchKernelGGL((k_edge_layer<F32T, 1, true>), grid, block, 0, s, a);
     else if (final_layer) hipLaunchKernelGGL((k_edge_layer<F32T, 1>), grid, block, 0, s, a);
     else if (gc) hipLaunchKernelGGL((k_edge_layer<F32T, 0, true>), grid, block, 0, s, a);
@@ -1836,38 +1441,30 @@ extern "C" int di_edge_layer(const di_graph* g, di_dtype dt, int final_layer, co
   return launch_status();
 }
 
-extern "C" int di_edge_config(int32_t kernel) {
-  if (kernel < -1 || kernel > 1) return DI_EINVAL;
-  const int prev = g_edge_kernel;
-  if (kernel >= 0) g_edge_kernel = kernel;
-  return prev;
-}
-
 extern "C" int di_conformation(const di_graph* g, di_dtype dt, const float* edge_f, const void* f_in,
                                const void* fn_in, const void* wmat, const float* wvec, void* conf_out,
                                void* stream) {
-  if (!g || !edge_f || !f_in || !fn_in || !wmat || !wvec || !conf_out || g->num_edges <= 0) return DI_EINVAL;
+  if (!g || !edge_f || !f_in || !fn_in || !wmat || !wvec || !conf_out || g->num_edges <= 0 || !dtype_ok(dt))
+    return DI_EINVAL;
   EdgeArgs a{g->num_edges, edge_f, g->src, g->dst, g->nbr, f_in, fn_in, nullptr, wmat, wvec, nullptr,
              conf_out, nullptr};
   hipStream_t s = (hipStream_t)stream;
-  if (dt == DI_BF16) {
-    dim3 grid(xcd_grid(grid_rows(a.Et, EdgeGeo<BF16T>::ROWS))), block(EdgeGeo<BF16T>::THREADS);
-    hipLaunchKernelGGL((k_edge_layer<BF16T, 2>), grid, block, 0, s, a);
-  } else {
-    dim3 grid(xcd_grid(grid_rows(a.Et, EdgeGeo<F32T>::ROWS))), block(EdgeGeo<F32T>::THREADS);
-    hipLaunchKernelGGL((k_edge_layer<F32T, 2>), grid, block, 0, s, a);
-  }
+  if (dt == DI_BF16)
+    hipLaunchKernelGGL((k_edge_layer<BF16T, 2>), grid_of<Geo<BF16T>>(a.Et), block_of<Geo<BF16T>>(), 0, s, a);
+  else
+    hipLaunchKernelGGL((k_edge_layer<F32T, 2>), grid_of<Geo<F32T>>(a.Et), block_of<Geo<F32T>>(), 0, s, a);
   return launch_status();
 }
 
 extern "C" int di_node_layer(const di_graph* g, di_dtype dt, int final_layer, const float* alpha,
                              const void* h_in, const void* qkv, const void* wmat, const float* wvec,
                              void* h_out, void* qkv_out, void* hT_out, void* stream) {
-  if (!g || !alpha || !h_in || !qkv || !wmat || !wvec || !h_out || g->num_nodes <= 0) return DI_EINVAL;
+  if (!g || !alpha || !h_in || !qkv || !wmat || !wvec || !h_out || g->num_nodes <= 0 || !dtype_ok(dt))
+    return DI_EINVAL;
   if (!final_layer && !qkv_out) return DI_EINVAL;
   NodeArgs a{g->num_nodes, nullptr, hT_out, g->src, g->in_ptr, alpha, h_in, qkv, wmat, wvec, h_out, qkv_out};
   hipStream_t s = (hipStream_t)stream;
-  dim3 grid(grid_rows(a.Nt)), block(THREADS);
+  const dim3 grid = grid_of<NodeGeo>(a.Nt), block = block_of<NodeGeo>();
   if (dt == DI_BF16) {
     if (final_layer) hipLaunchKernelGGL((k_node_layer<BF16T, true>), grid, block, 0, s, a);
     else hipLaunchKernelGGL((k_node_layer<BF16T, false>), grid, block, 0, s, a);
@@ -1880,7 +1477,8 @@ extern "C" int di_node_layer(const di_graph* g, di_dtype dt, int final_layer, co
 
 extern "C" int di_node_aggregate(const di_graph* g, di_dtype dt, const float* alpha, const void* qkv, float* attn_out,
                                  void* stream) {
-  if (!g || !alpha || !qkv || !attn_out || !g->src || !g->in_ptr || g->num_nodes <= 0) return DI_EINVAL;
+  if (!g || !alpha || !qkv || !attn_out || !g->src || !g->in_ptr || g->num_nodes <= 0 || !dtype_ok(dt))
+    return DI_EINVAL;
   AggrArgs a{g->num_nodes, g->src, g->in_ptr, alpha, qkv, attn_out};
   hipStream_t s = (hipStream_t)stream;
   dim3 grid((a.Nt + 15) / 16), block(256);
@@ -1892,15 +1490,16 @@ extern "C" int di_node_aggregate(const di_graph* g, di_dtype dt, const float* al
 extern "C" int di_node_update(const di_graph* g, di_dtype dt, int final_layer, const float* attn, const void* h_in,
                               const void* wmat, const float* wvec, void* h_out, void* qkv_out, void* hT_out,
                               void* stream) {
-  if (!g || !attn || !h_in || !wmat || !wvec || !h_out || g->num_nodes <= 0) return DI_EINVAL;
+  if (!g || !attn || !h_in || !wmat || !wvec || !h_out || g->num_nodes <= 0 || !dtype_ok(dt)) return DI_EINVAL;
   if (!final_layer && !qkv_out) return DI_EINVAL;
   NodeArgs a{g->num_nodes, attn, hT_out, nullptr, nullptr, nullptr, h_in, nullptr, wmat, wvec, h_out, qkv_out};
   hipStream_t s = (hipStream_t)stream;
-  dim3 grid(grid_rows(a.Nt)), block(THREADS);
   if (dt == DI_BF16) {
+    const dim3 grid = grid_of<NodeRingGeo>(a.Nt), block = block_of<NodeRingGeo>();
     if (final_layer) hipLaunchKernelGGL((k_node_update_ring<true>), grid, block, 0, s, a);
     else hipLaunchKernelGGL((k_node_update_ring<false>), grid, block, 0, s, a);
   } else {
+    const dim3 grid = grid_of<NodeGeo>(a.Nt), block = block_of<NodeGeo>();
     if (final_layer) hipLaunchKernelGGL((k_node_layer<F32T, true>), grid, block, 0, s, a);
     else hipLaunchKernelGGL((k_node_layer<F32T, false>), grid, block, 0, s, a);
   }

@@ -493,7 +493,7 @@ __global__ __launch_bounds__(64) void k_nbr_ids_torch(const int* __restrict__ no
   const int g = blockIdx.x, lane = threadIdx.x;
   const int n0 = node_off[g], n = node_off[g + 1] - n0;
   const int E = n * k, e0 = n0 * k, km1 = k - 1;
-  const int total = 2 * E * km1;  // draws of the 2E randperm(k) calls (host checks the int32 range)
+  const int total = 2 * E * km1;  // draws of the 2E randperm(k) calls (int32: di_build_nbr_ids_torch checks)
   if (lane == 0) {                // init_with_uint32(seed)
     uint32_t s = (uint32_t)(seeds[g] & 0xffffffffull);
     st[0] = s;
@@ -642,10 +642,12 @@ extern "C" int di_knn_graph(int32_t num_graphs, const int32_t* node_off, int32_t
 extern "C" int di_build_nbr_ids_torch(int32_t num_graphs, const int32_t* node_off, int32_t k, const uint64_t* seeds,
                                       int32_t num_nodes, const int32_t* src, const int32_t* dst, int32_t* nbr_out,
                                       void* stream) {
-  // chains of <= 4096 nodes (the builder's node-count limit) keep the draw count 2*n*k*(k-1) in int32
+  // k_nbr_ids_torch counts a chain's mt19937 draws, 2 n k (k-1), in int32: bounded through the
+  // batch total (every chain's n <= num_nodes), checked here on the host
   if (num_graphs <= 0 || num_graphs > 65535 || !node_off || k < 3 || k > 256 || !seeds || num_nodes <= 0 ||
-      (int64_t)num_nodes * k > INT32_MAX || !src || !dst || !nbr_out)
+      !src || !dst || !nbr_out)
     return DI_EINVAL;
+  if (2LL * num_nodes * k * (k - 1) > INT32_MAX) return DI_ERANGE;
   const int num_edges = num_nodes * k;
   hipLaunchKernelGGL(k_nbr_ids_torch, dim3(num_graphs), dim3(64), 0, (hipStream_t)stream, node_off, k, seeds,
                      nbr_out);

@@ -25,21 +25,16 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
-#include <stdlib.h>
 #include "common.h"
 #include "../../include/deepinteract_amd.h"
 
 namespace di {
 
 constexpr int PRO_THREADS = 256;
-#ifndef DI_PRO_TABLE_THREADS
-#define DI_PRO_TABLE_THREADS 512
-#endif
-constexpr int PRO_TTHREADS = DI_PRO_TABLE_THREADS;  // threads per table block (rows in flight)
-#ifndef DI_PRO_CG
-#define DI_PRO_CG 4
-#endif
-constexpr int PRO_CG = DI_PRO_CG;  // channels per table block (<= 4: one floatx4 of weights per k)
+// table-kernel launch shape, measured (profiles/r1_v8_prologue_tables_variants.json): 512 threads x
+// 4 channels 47.7 us vs 256x4 57.6, 1024x4 48.4, 512x2 62.8 (bf16, 8 complexes)
+constexpr int PRO_TTHREADS = 512;  // threads per table block (rows in flight)
+constexpr int PRO_CG = 4;          // channels per table block (<= 4: one floatx4 of weights per k)
 static_assert(PRO_CG >= 1 && PRO_CG <= 4, "PRO_CG");
 constexpr int PRO_SEG = 128;       // 16-B chunks per row segment of the store stream (2 per lane)
 constexpr float PRO_EXP_SAFE = 60.f;
@@ -371,13 +366,9 @@ __global__ __launch_bounds__(PRO_THREADS) void k_prologue_flat(const di_pair_des
 
 using namespace di;
 
-static int pro_env_int(const char* name, int dflt) {
-  const char* e = getenv(name);
-  const int v = e ? atoi(e) : 0;
-  return v > 0 ? v : dflt;
-}
-static const int g_pro_blocks = pro_env_int("DI_PRO_BLOCKS", 512);
-static const int g_pro_waves = pro_env_int("DI_PRO_WAVES", 4);
+// launch shape of the row-streaming store kernel: 512 resident 4-wave blocks
+constexpr int PRO_ROW_BLOCKS = 512;
+constexpr int PRO_ROW_WAVES = 4;
 
 extern "C" int64_t di_head_prologue_work_bytes(int32_t num_complexes, int32_t max_l1, int32_t max_l2,
                                                int32_t channels) {
@@ -395,7 +386,7 @@ extern "C" int di_head_prologue(di_dtype dt, const di_pair_desc* descs, int32_t 
       !(eps >= 0.f) || (dt != DI_BF16 && dt != DI_F32))
     return DI_EINVAL;
   if (((uintptr_t)h & 15) != 0) return DI_EINVAL;  // 16-B row loads in the table kernel
-  if ((int64_t)max_l1 * max_l2 * (dt == DI_BF16 ? 2 : 4) >= (1LL << 31)) return DI_ERANGE;  // 32-bit row offsets
+  if ((int64_t)max_l1 * max_l2 >= (1LL << 31) / (dt == DI_BF16 ? 2 : 4)) return DI_ERANGE;  // 32-bit row offsets
   hipStream_t s = (hipStream_t)stream;
   const int groups = (channels + PRO_CG - 1) / PRO_CG;
   const unsigned tgrid = (unsigned)num_complexes * (unsigned)groups;
@@ -406,12 +397,12 @@ extern "C" int di_head_prologue(di_dtype dt, const di_pair_desc* descs, int32_t 
     hipLaunchKernelGGL(k_prologue_tables<float>, dim3(tgrid), dim3(PRO_TTHREADS), 0, s, descs, hidden, channels,
                        max_l1, max_l2, eps, (const float*)h, conv_w, conv_b, in_gamma, in_beta, work);
   if (aligned16) {
-    const int rows = 64 * g_pro_waves;
+    const int rows = 64 * PRO_ROW_WAVES;
     const int rblocks = (max_l1 + rows - 1) / rows;
     const int64_t items64 = (int64_t)num_complexes * channels * rblocks;
     if (items64 > INT32_MAX) return DI_ERANGE;
     const int items = (int)items64;
-    const unsigned grid = (unsigned)(items < g_pro_blocks ? items : g_pro_blocks);
+    const unsigned grid = (unsigned)(items < PRO_ROW_BLOCKS ? items : PRO_ROW_BLOCKS);
     if (dt == DI_BF16)
       hipLaunchKernelGGL(k_prologue_rows<u16>, dim3(grid), dim3(rows), 0, s, descs, channels, max_l1, max_l2, rblocks,
                          items, (const float*)work, (u16*)out);

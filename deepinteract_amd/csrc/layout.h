@@ -37,17 +37,13 @@ constexpr int EL_RC = 468;
 constexpr int EL_F = 500;     // final_linear [8x4]
 constexpr int EL_FG = 532;    // final gate (sum of the 4 final_* geometric linears) [8x1]
 constexpr int EL_P = 540;     // edge_feats_projection . BN1e
-constexpr int EL_NBLK_FINAL = 572 + 12 * 32;
+constexpr int EL_NBLK_FINAL = 572;
 constexpr int EL_NBLK_CONF = 540;  // kind 6: conformation module alone (stages S0 .. final_linear)
 constexpr int EL_OE = 572;
 constexpr int EL_F1 = 604;    // 2 x [8x4] (hidden halves)
 constexpr int EL_F2 = 668;    // 2 x [8x4] (input halves)
 constexpr int EL_NN = 732;    // next layer's nbr_linear
-// f16 copies of the 12 ResBlock matrices (same scaling, same fragment order), read only by the
-// grouped bf16 kernel built with DI_LEAN_F16RES (SiLU in packed f16 inside the ResBlocks);
-// intermediate layer at EL_R16_INT, final layer at EL_R16_FIN
-constexpr int EL_R16_INT = 764, EL_R16_FIN = 572;
-constexpr int EL_NBLK = 764 + 12 * 32;
+constexpr int EL_NBLK = 764;
 constexpr int ELV_OM = 0, ELV_RES = 128, ELV_RC = 1664, ELV_F = 1792, ELV_P = 1920;
 constexpr int ELV_N_FINAL = 2048;
 constexpr int ELV_N_CONF = 1920;

@@ -173,7 +173,8 @@ extern "C" int di_gemm_bias_act(di_dtype dt, int32_t rows, int32_t in_dim, int32
                                 int32_t x_ld, const void* w_packed, const float* bias, int32_t act,
                                 const void* res, int32_t res_ld, void* y, int32_t y_ld, void* stream) {
   if (!x || !w_packed || !y || rows <= 0 || in_dim <= 0 || out_dim <= 0 || out_dim % 16 || x_ld < in_dim ||
-      y_ld < out_dim || y_ld % 4 || (res && (res_ld < out_dim || res_ld % 4)) || act < 0 || act > 1)
+      y_ld < out_dim || y_ld % 4 || (res && (res_ld < out_dim || res_ld % 4)) || act < 0 || act > 1 ||
+      (dt != DI_F32 && dt != DI_BF16))
     return DI_EINVAL;
   GemmArgs a{rows, in_dim, out_dim, x_ld, y_ld, res_ld, act, x, w_packed, bias, res, y};
   dim3 grid((rows + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK, (out_dim / 16 + 7) / 8), block(THREADS);
@@ -184,7 +185,9 @@ extern "C" int di_gemm_bias_act(di_dtype dt, int32_t rows, int32_t in_dim, int32
 
 extern "C" int di_geo_attention(const di_graph* g, di_dtype dt, const void* qkv, const void* proj_e, void* e_out,
                                 float* alpha_out, void* h_out, void* stream) {
-  if (!g || !qkv || !proj_e || !alpha_out || !h_out || g->num_edges <= 0 || g->num_nodes <= 0) return DI_EINVAL;
+  if (!g || !qkv || !proj_e || !alpha_out || !h_out || g->num_edges <= 0 || g->num_nodes <= 0 ||
+      (dt != DI_F32 && dt != DI_BF16))
+    return DI_EINVAL;
   hipStream_t s = (hipStream_t)stream;
   const unsigned ge = (unsigned)(((int64_t)g->num_edges * 4 + 255) / 256);
   const unsigned gn = (unsigned)(((int64_t)g->num_nodes * 32 + 255) / 256);

@@ -4,39 +4,42 @@
 //     T[c, i, j] = h2[j, c - H]      for c >= H          (NCHW, [2H, L1, L2] per complex)
 // The reference materialises it with two repeat_interleave tensors plus a cat (3x the output
 // bytes); here every output byte is written exactly once: a pure HBM store stream (512 MB per
-// 2x1000-residue complex in bf16), with non-temporal 16-B stores (write-once data, kept out of
-// the caches the concurrently running GeoT kernels use).
+// 2x1000-residue complex in bf16).
 //
-// Persistent grid: a few blocks per CU walk work items (complex, channel, 64K-element chunk);
-// no LDS, so the kernel co-resides with the GeoT kernels on the other stream (which hold the
-// LDS) instead of starving them of CU slots. Chain-2 planes read the transposed features hT
-// [H, Nt] (written by the final node layer), so each 16-B store is fed by one 16-B load.
+// Kernels (di_pair_launch.kernel; all persistent, no LDS, so they co-reside with the GeoT kernels
+// of the other stream, which hold the LDS):
+//  * k_pair_lines (DI_PAIR_LINES, the default for 128-B-aligned planes): every store instruction
+//    writes whole 128-B lines. A channel plane repeats with a period of p = 128 / gcd(row bytes,
+//    128) rows (p <= 8; 2000-B rows: p = 8 rows = 125 lines), so line r + P t of the plane holds the
+//    same bytes for every t (chain 2) or the same bytes of rows p t .. p t + p - 1 (chain 1). A wave
+//    owns 8 line residues (8 lanes x 16 B each) and streams t = 0, 1, ...: per-lane constant data
+//    and address, the period offset in an SGPR. Row-by-row streaming (k_pair_rows) splits the
+//    128-B line at every row boundary between two partial writes (+2.9 % write traffic measured
+//    at 2000-B rows).
+//  * k_pair_rows (DI_PAIR_ROWS): a wave owns 64 whole rows; the row vector (chain 2) / row value
+//    (chain 1) is loaded once per 128-chunk segment, then only stores (16-B aligned planes).
+//  * k_pair_vec (DI_PAIR_VECTOR): one 16-B load per 16-B store over flat plane positions.
+//  * k_pair_flat: any shape / alignment, one element per thread and step.
+// beside != 0 (the schedule beside GeoT): after every row / period the wave waits until at most
+// PAIR_INFLIGHT of its stores are outstanding, and stores are non-temporal. The per-CU
+// vector-memory queue is in order, so a store-only wave that runs 60 stores ahead parks every
+// load of the co-resident GeoT waves (weight-stage DMA, gathers) behind ~1k cycles of store drain.
+// Measured beside GeoT (C3, round 2): in-flight bound n = 1/2/3/4/6 -> 5.14/5.53/5.50/5.37-5.61/
+// 5.23 k complexes/s (unbounded 5.01 k); nt stores 7472 vs plain 7002 complexes/s (sc0 7018,
+// sc1 3818). Alone the plain policy is faster (row kernel 681 vs 875 us per 4.1 GB).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
-#include <stdlib.h>
 #include "common.h"
 #include "../../include/deepinteract_amd.h"
 
 namespace di {
 
-constexpr int PAIR_THREADS = 256;
-constexpr int PAIR_CHUNK = 65536;  // elements per work item
-constexpr int PAIR_MAX_BLOCKS = 256;  // one 4-wave block per CU: leaves the GeoT kernels their issue slots
+constexpr int PAIR_THREADS = 256;   // k_pair_vec / k_pair_flat
+constexpr int PAIR_CHUNK = 65536;   // elements per k_pair_vec / k_pair_flat work item
 constexpr int PAIR_UNROLL = 4;
-// Store cache policy of the row kernel's 16-B stores (gfx950 CPol bits: 2 = nt, 16 = sc1).
-// Measured on the C3 pair tensor (4.1 GB per launch, alone): plain 681 us (6.0 TB/s), nt 875 us;
-// sc1 / sc1+nt slowed the per-vector kernel by 15 % without speeding up the concurrent GeoT.
-// The per-vector (legacy aligned) kernel keeps non-temporal stores.
-#ifndef DI_PAIR_STORE
-#define DI_PAIR_STORE 0
-#endif
-// ... and of the bounded row kernel that runs beside GeoT (kernel 3): non-temporal, so the store
-// stream does not evict GeoT's L2-resident weight stages and rows. Measured beside GeoT (C3, 512
-// complexes): nt 7472 vs plain 7002 complexes/s (GeoT edge layer 429 vs 471 us, pair 1045 vs
-// 1082 us); sc0 7018, sc1 3818.
-#ifndef DI_PAIR_STORE_BESIDE
-#define DI_PAIR_STORE_BESIDE 2
-#endif
+constexpr int PAIR_INFLIGHT = 3;    // stores in flight per wave when beside GeoT
+constexpr int PAIR_SEG = 128;       // 16-B chunks per row segment of k_pair_rows (2 per lane)
+constexpr int PAIR_MAX_PLANE_ROWS = 1 << 20;  // k_pair_vec / k_pair_flat row index from an fp32 quotient
 
 template <typename T>
 struct Vec16;
@@ -52,30 +55,37 @@ struct Vec16<u16> {
   static constexpr int N = 8;
 };
 
-// Row index of flat plane position q (q < 2^24, exact in fp32): the fp32 quotient is off by at
-// most one and is corrected with two selects, instead of a 64-bit integer division per store.
+// store-queue bound of the beside-GeoT schedule (an immediate)
+template <bool BESIDE>
+__device__ __forceinline__ void pair_bound() {
+  if constexpr (BESIDE) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PAIR_INFLIGHT) : "memory");
+}
+// CPol bits of the 16-B buffer stores: non-temporal beside GeoT, plain alone
+template <bool BESIDE>
+constexpr int pair_cpol() { return BESIDE ? 2 : 0; }
+
+// (row, column) of flat plane position q: the fp32 quotient is within one of q / l2 for
+// q / l2 < 2^20 (PAIR_MAX_PLANE_ROWS) and corrected with two selects; the remainder is exact
+// in 64-bit arithmetic.
 __device__ __forceinline__ void plane_rc(uint32_t q, uint32_t l2, float inv_l2, uint32_t& i, uint32_t& j) {
-  int32_t ii = (int32_t)((float)q * inv_l2);
-  int32_t jj = (int32_t)q - ii * (int32_t)l2;
-  if (jj < 0) { --ii; jj += (int32_t)l2; }
-  if (jj >= (int32_t)l2) { ++ii; jj -= (int32_t)l2; }
+  int64_t ii = (int64_t)((float)q * inv_l2);
+  int64_t jj = (int64_t)q - ii * (int64_t)l2;
+  if (jj < 0) { --ii; jj += l2; }
+  if (jj >= (int64_t)l2) { ++ii; jj -= l2; }
   i = (uint32_t)ii;
   j = (uint32_t)jj;
 }
 
-template <typename T, bool ALIGNED>
-__global__ __launch_bounds__(PAIR_THREADS) void k_pair_tensor(const di_pair_desc* __restrict__ descs, int hidden,
-                                                            const T* __restrict__ h, const T* __restrict__ hT,
-                                                            int nrows, int chunks, int items,
-                                                            T* __restrict__ out, int pace) {
-  using V = typename Vec16<T>::V;
-  constexpr int VEC = Vec16<T>::N;
+// ---- generic: any shape and alignment -------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(PAIR_THREADS) void k_pair_flat(const di_pair_desc* __restrict__ descs, int hidden,
+                                                          const T* __restrict__ h, const T* __restrict__ hT,
+                                                          int nrows, int chunks, int items, T* __restrict__ out) {
   for (int item = blockIdx.x; item < items; item += gridDim.x) {
     const int chunk = item % chunks;
     const int rest = item / chunks;
     const int c = rest % (2 * hidden);
-    const int cpx = rest / (2 * hidden);
-    const di_pair_desc d = descs[cpx];
+    const di_pair_desc d = descs[rest / (2 * hidden)];
     const uint32_t l2 = (uint32_t)d.l2;
     const uint32_t plane = (uint32_t)d.l1 * l2;
     const uint32_t q_begin = (uint32_t)chunk * PAIR_CHUNK;
@@ -84,99 +94,104 @@ __global__ __launch_bounds__(PAIR_THREADS) void k_pair_tensor(const di_pair_desc
     const float inv_l2 = 1.0f / (float)l2;
     T* o = out + d.out_off + (int64_t)c * plane;
     const bool second = c >= hidden;
-    const T* h1c = h + d.h1_row * hidden + c;                                      // column c of chain 1
-    const T* h2t = hT ? hT + (int64_t)(c - hidden) * nrows + d.h2_row : nullptr;  // row c-H of hT
-    const T* h2c = h + d.h2_row * hidden + (c - hidden);                           // strided fallback
-    if (ALIGNED) {
-#if !(DI_PAIR_STORE == 0 || DI_PAIR_STORE == 2)
-      const __amdgpu_buffer_rsrc_t orsrc = buf_rsrc(o);  // plane base: q * sizeof(T) < 2^31
-#endif
-      // PAIR_UNROLL independent 16-B vectors per thread per trip: the hT loads (L2 hits) of a
-      // trip are all in flight before its stores
-      constexpr uint32_t STEP = PAIR_THREADS * VEC;
-      for (uint32_t q0 = q_begin + threadIdx.x * VEC; q0 < q_end; q0 += PAIR_UNROLL * STEP) {
-        V vals[PAIR_UNROLL];
+    const T* h1c = h + d.h1_row * hidden + c;
+    const T* h2t = hT ? hT + (int64_t)(c - hidden) * nrows + d.h2_row : nullptr;
+    const T* h2c = h + d.h2_row * hidden + (c - hidden);
+    for (uint32_t q = q_begin + threadIdx.x; q < q_end; q += PAIR_THREADS) {
+      uint32_t i, j;
+      plane_rc(q, l2, inv_l2, i, j);
+      o[q] = second ? (h2t ? h2t[j] : h2c[(int64_t)j * hidden]) : h1c[(int64_t)i * hidden];
+    }
+  }
+}
+
+// ---- 16-B aligned planes: one load per non-temporal 16-B store --------------------------------
+template <typename T>
+__global__ __launch_bounds__(PAIR_THREADS) void k_pair_vec(const di_pair_desc* __restrict__ descs, int hidden,
+                                                         const T* __restrict__ h, const T* __restrict__ hT, int nrows,
+                                                         int chunks, int items, T* __restrict__ out) {
+  using V = typename Vec16<T>::V;
+  constexpr int VEC = Vec16<T>::N;
+  constexpr uint32_t STEP = PAIR_THREADS * VEC;
+  for (int item = blockIdx.x; item < items; item += gridDim.x) {
+    const int chunk = item % chunks;
+    const int rest = item / chunks;
+    const int c = rest % (2 * hidden);
+    const di_pair_desc d = descs[rest / (2 * hidden)];
+    const uint32_t l2 = (uint32_t)d.l2;
+    const uint32_t plane = (uint32_t)d.l1 * l2;
+    const uint32_t q_begin = (uint32_t)chunk * PAIR_CHUNK;
+    if (q_begin >= plane) continue;
+    const uint32_t q_end = q_begin + PAIR_CHUNK < plane ? q_begin + PAIR_CHUNK : plane;
+    const float inv_l2 = 1.0f / (float)l2;
+    T* o = out + d.out_off + (int64_t)c * plane;
+    const bool second = c >= hidden;
+    const T* h1c = h + d.h1_row * hidden + c;
+    const T* h2t = hT + (int64_t)(c - hidden) * nrows + d.h2_row;
+    // PAIR_UNROLL independent vectors per thread per trip: the trip's loads (L2 hits) are all in
+    // flight before its stores
+    for (uint32_t q0 = q_begin + threadIdx.x * VEC; q0 < q_end; q0 += PAIR_UNROLL * STEP) {
+      V vals[PAIR_UNROLL];
 #pragma unroll
-        for (int u = 0; u < PAIR_UNROLL; ++u) {
-          const uint32_t q = q0 + u * STEP;
-          if (q < q_end) {
-            uint32_t i, j;
-            plane_rc(q, l2, inv_l2, i, j);
-            if (second) {
-              vals[u] = *reinterpret_cast<const V*>(h2t + j);  // j % VEC == 0, L2 % VEC == 0: no row wrap
-            } else {
-              const T v0 = h1c[i * hidden];
-              T tmp[VEC];
+      for (int u = 0; u < PAIR_UNROLL; ++u) {
+        const uint32_t q = q0 + u * STEP;
+        if (q < q_end) {
+          uint32_t i, j;
+          plane_rc(q, l2, inv_l2, i, j);
+          if (second) {
+            vals[u] = *reinterpret_cast<const V*>(h2t + j);  // j % VEC == 0, L2 % VEC == 0: no row wrap
+          } else {
+            const T v0 = h1c[(int64_t)i * hidden];
+            T tmp[VEC];
 #pragma unroll
-              for (int t = 0; t < VEC; ++t) tmp[t] = v0;
-              vals[u] = *reinterpret_cast<const V*>(tmp);
-            }
+            for (int t = 0; t < VEC; ++t) tmp[t] = v0;
+            vals[u] = *reinterpret_cast<const V*>(tmp);
           }
         }
-#pragma unroll
-        for (int u = 0; u < PAIR_UNROLL; ++u) {
-          const uint32_t q = q0 + u * STEP;
-          if (q < q_end) {
-#if DI_PAIR_STORE == 0 || DI_PAIR_STORE == 2
-            __builtin_nontemporal_store(vals[u], reinterpret_cast<V*>(o + q));
-#else
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uintx4, vals[u]), orsrc, (int)(q * sizeof(T)), 0,
-                                                   DI_PAIR_STORE);
-#endif
-          }
-        }
-        for (int t = 0; t < pace; ++t) __builtin_amdgcn_s_sleep(1);  // store-rate pacing (di_pair_pace)
       }
-    } else {
-      for (uint32_t q = q_begin + threadIdx.x; q < q_end; q += PAIR_THREADS) {
-        uint32_t i, j;
-        plane_rc(q, l2, inv_l2, i, j);
-        o[q] = second ? (h2t ? h2t[j] : h2c[j * hidden]) : h1c[i * hidden];
+#pragma unroll
+      for (int u = 0; u < PAIR_UNROLL; ++u) {
+        const uint32_t q = q0 + u * STEP;
+        if (q < q_end) __builtin_nontemporal_store(vals[u], reinterpret_cast<V*>(o + q));
       }
     }
   }
 }
 
-// Row-streaming form of the aligned path (every plane offset, L2 and chain-2 row 16-B aligned).
-// A channel plane is L1 identical-shape rows of L2 elements: chain-2 rows are all the same vector
-// hT[c - H, 0:L2], chain-1 row i is the constant h1[i, c]. A work item is (complex, channel,
-// PAIR_ROWS rows); a wave owns a contiguous run of 64 of them (a cache line split between rows
-// i and i+1 is completed by the same wave back to back). Per 128-chunk segment of the row it loads
-// what its rows need ONCE (two 16-B row-vector pieces per lane, or one chain-1 value per row, one
-// per lane, broadcast with readlane), then issues only stores: buffer_store_dwordx4 with a
-// per-lane constant voffset and the row offset in an SGPR, so a 2-KB row costs two store
-// instructions plus scalar address arithmetic, and no load sits between stores.
+// broadcast a chain-1 value to a 16-B vector (bf16: two copies per dword)
+template <typename T>
+__device__ __forceinline__ uint32_t pair_bcast_bits(const T* p);
+template <>
+__device__ __forceinline__ uint32_t pair_bcast_bits<u16>(const u16* p) {
+  const uint32_t v = *p;
+  return v | (v << 16);
+}
+template <>
+__device__ __forceinline__ uint32_t pair_bcast_bits<float>(const float* p) {
+  return __builtin_bit_cast(uint32_t, *p);
+}
+
+// ---- 16-B aligned planes: row streaming ------------------------------------------------------
+// A work item is (complex, channel, 64 x waves rows); a wave owns a contiguous run of 64 rows. Per
+// 128-chunk segment of the row it loads what its rows need ONCE (two 16-B row-vector pieces per
+// lane, or one chain-1 value per row, one per lane, broadcast with readlane), then issues only
+// stores: buffer_store_dwordx4 with a per-lane constant voffset and the row offset in an SGPR.
 // <= 32 VGPRs: one wave per SIMD co-resides with the edge kernels (2 x 240 VGPRs).
-// Block size is a launch parameter (di_pair_config): 4 waves x one block per CU when the kernel
-// shares every CU with GeoT, 8 waves on a few dedicated CUs (CU-masked stream): 64 CUs alone
-// store 5.6 TB/s, 32 CUs 3.4 TB/s (C3 micro-batch of 8 complexes).
-// INFLIGHT = n > 0 (the "rows_bounded" kernel, di_pair_config kernel 3, the default beside GeoT):
-// after every row the wave waits until at most n of its stores are outstanding. The per-CU
-// vector-memory queue is in order, so a store-only wave that runs 60 stores ahead parks every
-// load of the co-resident GeoT waves (weight-stage DMA, gathers) behind ~1k cycles of store drain;
-// a bounded queue keeps GeoT's loads near the front. Measured beside GeoT (C3, 256 complexes,
-// one 2-wave block per CU): n = 1/2/3/4/6 -> 5.14/5.53/5.50/5.37-5.61/5.23 k complexes/s, the
-// unbounded rows kernel 5.01 k, the per-vector kernel 5.27-5.33 k; 4-wave blocks starve InitEdge.
-#ifndef DI_PAIR_INFLIGHT
-#define DI_PAIR_INFLIGHT 3
-#endif
-constexpr int PAIR_SEG = 128;  // 16-B chunks per row segment (2 per lane)
-template <typename T, int INFLIGHT, int CPOL>
+template <typename T, bool BESIDE>
 __global__ __launch_bounds__(1024) __attribute__((amdgpu_num_vgpr(32)))
 void k_pair_rows(const di_pair_desc* __restrict__ descs, int hidden, const T* __restrict__ h,
-                 const T* __restrict__ hT, int nrows, int rblocks, int items, T* __restrict__ out, int pace) {
+                 const T* __restrict__ hT, int nrows, int rblocks, int items, T* __restrict__ out) {
   using V = typename Vec16<T>::V;
   constexpr int VEC = Vec16<T>::N;
-  const int PAIR_ROWS = (int)blockDim.x;  // rows per work item: 64 per wave
+  const int rows_per_item = (int)blockDim.x;  // 64 per wave
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   for (int item = blockIdx.x; item < items; item += gridDim.x) {
     const int rb = item % rblocks;
     const int rest = item / rblocks;
     const int c = rest % (2 * hidden);
-    const int cpx = rest / (2 * hidden);
-    const di_pair_desc d = descs[cpx];
-    const int r0 = rb * PAIR_ROWS + 64 * wave;  // this wave's rows [r0, r1)
+    const di_pair_desc d = descs[rest / (2 * hidden)];
+    const int r0 = rb * rows_per_item + 64 * wave;  // this wave's rows [r0, r1)
     const int r1 = r0 + 64 < d.l1 ? r0 + 64 : d.l1;
     if (r0 >= r1) continue;  // uniform per wave
     const int nch = d.l2 / VEC;  // 16-B chunks per row
@@ -185,14 +200,7 @@ void k_pair_rows(const di_pair_desc* __restrict__ descs, int hidden, const T* __
     const __amdgpu_buffer_rsrc_t r = buf_rsrc(o);
     const bool second = c >= hidden;
     uint32_t hv = 0;  // chain 1: lane l holds the value of row r0 + l
-    if (!second && r0 + lane < r1) {
-      if constexpr (sizeof(T) == 2) {
-        hv = h[(d.h1_row + r0 + lane) * hidden + c];
-        hv |= hv << 16;
-      } else {
-        hv = __builtin_bit_cast(uint32_t, h[(d.h1_row + r0 + lane) * hidden + c]);
-      }
-    }
+    if (!second && r0 + lane < r1) hv = pair_bcast_bits<T>(h + (d.h1_row + r0 + lane) * hidden + c);
     const T* src = hT + (int64_t)(c - hidden) * nrows + d.h2_row;
     for (int seg = 0; seg < nch; seg += PAIR_SEG) {
       const int k0 = seg + lane, k1 = seg + 64 + lane;  // this lane's chunks of the segment
@@ -210,12 +218,82 @@ void k_pair_rows(const di_pair_desc* __restrict__ descs, int hidden, const T* __
           v1 = v0;
         }
         if (k0 < nch)
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uintx4, v0), r, k0 * 16, soff, CPOL);
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uintx4, v0), r, k0 * 16, soff, pair_cpol<BESIDE>());
         if (two && k1 < nch)
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uintx4, v1), r, k1 * 16, soff, CPOL);
-        if constexpr (INFLIGHT > 0)  // bound this wave's queued stores (see DI_PAIR_INFLIGHT)
-          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(INFLIGHT) : "memory");
-        for (int t = 0; t < pace; ++t) __builtin_amdgcn_s_sleep(1);  // store-rate pacing (di_pair_pace)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uintx4, v1), r, k1 * 16, soff, pair_cpol<BESIDE>());
+        pair_bound<BESIDE>();
+      }
+    }
+  }
+}
+
+// ---- 128-B aligned planes: whole-line streaming -------------------------------------------------
+// Plane geometry (row bytes R, a multiple of 16): the plane repeats every p = 128 / gcd(R, 128) rows
+// = P = p R / 128 lines (period bytes p R, a multiple of 128). Line residue r (0 <= r < P) holds
+// chunks C = 8 r + s (s = 0..7, 16 B each) of the period: row dr = C / (R/16) of the period,
+// chunk k = C % (R/16) of that row. The plane is q = L1 / p whole periods plus a tail of
+// (L1 % p) R / 128 lines (the plane end is line aligned, so the tail is whole lines too).
+// A work item is (complex, channel, group of 8 x waves residues); lane (wave w, l) stores residue
+// r = group * 8 * waves + 8 w + l / 8, chunk s = l % 8, at voffset 128 r + 16 s and soffset t x
+// period for t = 0 .. q (t = q: tail residues only):
+//   chain 2: the value hT[c - H, 8k .. 8k + 7] is the same for every t (loaded once);
+//   chain 1: the value h1[p t + dr, c]: rows t0 p .. t0 p + 63 are loaded one per lane for every
+//            64 / p repeats and each lane picks its row by ds_bpermute.
+template <typename T, bool BESIDE>
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_num_vgpr(32)))
+void k_pair_lines(const di_pair_desc* __restrict__ descs, int hidden, const T* __restrict__ h,
+                  const T* __restrict__ hT, int nrows, int groups, int items, T* __restrict__ out) {
+  using V = typename Vec16<T>::V;
+  constexpr int VEC = Vec16<T>::N;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int nw = (int)(blockDim.x >> 6);
+  for (int item = blockIdx.x; item < items; item += gridDim.x) {
+    const int grp = item % groups;
+    const int rest = item / groups;
+    const int c = rest % (2 * hidden);
+    const di_pair_desc d = descs[rest / (2 * hidden)];
+    const uint32_t R = (uint32_t)d.l2 * sizeof(T);
+    const uint32_t low = R & (0u - R);                    // largest power of two dividing R (>= 16)
+    const int p = 128 / (int)(low < 128u ? low : 128u);   // rows per period
+    const uint32_t period = (uint32_t)p * R;              // bytes
+    const int P = (int)(period >> 7);                     // lines per period
+    const int rw = grp * 8 * nw + 8 * wave;               // this wave's first residue
+    if (rw >= P) continue;  // uniform per wave
+    const int r = rw + (lane >> 3), s = lane & 7;
+    const int nq = d.l1 / p;                              // whole periods
+    const int tail = (int)((uint32_t)(d.l1 - nq * p) * R >> 7);  // lines of the partial period
+    const int nt = nq + (rw < tail ? 1 : 0);             // repeats this wave issues (uniform)
+    const bool on = r < P;                               // lane's residue exists
+    const int nch = (int)(R >> 4);
+    const int C = 8 * r + s;
+    const int dr = C / nch, k = C - dr * nch;
+    T* o = out + d.out_off + (int64_t)c * ((int64_t)d.l1 * d.l2);
+    const __amdgpu_buffer_rsrc_t rs = buf_rsrc(o);
+    const int voff = 128 * r + 16 * s;
+    if (c >= hidden) {
+      V v = {};
+      if (on) v = *reinterpret_cast<const V*>(hT + (int64_t)(c - hidden) * nrows + d.h2_row + (int64_t)k * VEC);
+      for (int t = 0; t < nt; ++t) {
+        if (on && (t < nq || r < tail))
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uintx4, v), rs, voff, (int)(t * period),
+                                                 pair_cpol<BESIDE>());
+        pair_bound<BESIDE>();
+      }
+    } else {
+      const T* h1c = h + d.h1_row * hidden + c;
+      const int G = 64 / p;  // repeats per 64 loaded rows
+      for (int t0 = 0; t0 < nt; t0 += G) {
+        const int row = t0 * p + lane;
+        const uint32_t hv = row < d.l1 ? pair_bcast_bits<T>(h1c + (int64_t)row * hidden) : 0u;
+        const int t1 = t0 + G < nt ? t0 + G : nt;
+        for (int t = t0; t < t1; ++t) {
+          const uint32_t b = (uint32_t)__builtin_amdgcn_ds_bpermute(4 * ((t - t0) * p + dr), (int)hv);
+          if (on && (t < nq || r < tail))
+            __builtin_amdgcn_raw_buffer_store_b128((uintx4){b, b, b, b}, rs, voff, (int)(t * period),
+                                                   pair_cpol<BESIDE>());
+          pair_bound<BESIDE>();
+        }
       }
     }
   }
@@ -225,92 +303,99 @@ void k_pair_rows(const di_pair_desc* __restrict__ descs, int hidden, const T* __
 
 using namespace di;
 
-// resident grid of the persistent pair kernels and waves per row-kernel block (di_pair_config)
-static int env_int(const char* name, int dflt) {
-  const char* e = getenv(name);
-  const int v = e ? atoi(e) : 0;
-  return v > 0 ? v : dflt;
-}
-static int g_pair_blocks = env_int("DI_PAIR_BLOCKS", PAIR_MAX_BLOCKS);
-static int g_pair_waves = env_int("DI_PAIR_WAVES", 4);
-static int g_pair_kernel = env_int("DI_PAIR_KERNEL", 1);  // 1 row-streaming, 2 per-vector, 3 row-streaming
-                                                          // with bounded in-flight stores (aligned path)
-static int g_pair_pace = env_int("DI_PAIR_PACE", 0);      // s_sleep(1) (~64 clk) per row / per trip of stores
-
-// Store-rate pacing of the aligned pair kernels when they share the GPU with GeoT: each wave
-// sleeps `pace` x 64 clocks after every row (row kernel) or every PAIR_UNROLL-vector trip
-// (vector kernel), so the store stream leaves the memory pipeline headroom for GeoT's loads.
-extern "C" int di_pair_pace(int32_t pace) {
-  if (pace < 0 || pace > 1000) return DI_EINVAL;
-  g_pair_pace = pace;
-  return DI_OK;
+static int pair_num_cus() {
+  static const int n = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0)
+      v = 256;
+    return v;
+  }();
+  return n;
 }
 
-extern "C" int di_pair_config(int32_t blocks, int32_t waves_per_block, int32_t kernel) {
-  if (blocks < 0 || waves_per_block < 0 || waves_per_block > 16 || kernel < 0 || kernel > 3) return DI_EINVAL;
-  if (blocks > 0) g_pair_blocks = blocks;
-  if (waves_per_block > 0) g_pair_waves = waves_per_block;
-  if (kernel > 0) g_pair_kernel = kernel;
+// a * b <= limit for non-negative a, b, without forming the (possibly overflowing) product
+static inline bool mul_le(int64_t a, int64_t b, int64_t limit) { return a == 0 || b <= limit / a; }
+
+extern "C" int di_pair_tensor_check(int32_t num_complexes, int32_t max_l1, int32_t max_l2, int32_t hidden,
+                                    int32_t elem_bytes, const di_pair_launch* launch) {
+  if (num_complexes <= 0 || max_l1 <= 0 || max_l2 <= 0 || hidden <= 0 || (elem_bytes != 2 && elem_bytes != 4))
+    return DI_EINVAL;
+  if (launch) {
+    if (launch->kernel < DI_PAIR_AUTO || launch->kernel > DI_PAIR_LINES || launch->blocks < 0 ||
+        launch->waves_per_block < 0 || launch->waves_per_block > 16 || (launch->beside != 0 && launch->beside != 1))
+      return DI_EINVAL;
+  }
+  // 32-bit byte offsets inside a channel plane (buffer stores: soffset / voffset < 2^31) and the
+  // fp32-quotient row index of the flat kernels
+  if (max_l1 > PAIR_MAX_PLANE_ROWS) return DI_ERANGE;
+  const int64_t plane = (int64_t)max_l1 * max_l2;  // < 2^51
+  if (plane * elem_bytes >= (1LL << 31)) return DI_ERANGE;
+  // work items of any kernel: planes x (row blocks <= L1, residue groups <= L2, flat chunks)
+  const int64_t chunks = (plane + PAIR_CHUNK - 1) / PAIR_CHUNK;
+  int64_t per_plane = max_l1 > max_l2 ? max_l1 : max_l2;
+  if (chunks > per_plane) per_plane = chunks;
+  const int64_t planes = (int64_t)num_complexes * 2 * hidden;  // < 2^63
+  if (!mul_le(planes, per_plane, INT32_MAX)) return DI_ERANGE;
   return DI_OK;
 }
 
 extern "C" int di_pair_tensor(di_dtype dt, const di_pair_desc* descs, int32_t num_complexes, int32_t max_l1,
-                              int32_t max_l2, int32_t hidden, int32_t aligned16, const void* h, const void* hT,
-                              int32_t num_rows, void* out, void* stream) {
-  if (!descs || !h || !out || num_complexes <= 0 || max_l1 <= 0 || max_l2 <= 0 || hidden <= 0) return DI_EINVAL;
-  if (aligned16 && !hT) return DI_EINVAL;
-  const int64_t plane = (int64_t)max_l1 * max_l2;
-  const int chunks = (int)((plane + PAIR_CHUNK - 1) / PAIR_CHUNK);
-  if (plane >= (1 << 24)) return DI_ERANGE;  // flat plane offsets are exact in fp32 / uint32
-  const int64_t items64 = (int64_t)num_complexes * 2 * hidden * chunks;
-  if (items64 > INT32_MAX) return DI_ERANGE;
-  const int items = (int)items64;
-  const int max_blocks = g_pair_blocks;
-  const unsigned grid = (unsigned)(items < max_blocks ? items : max_blocks);
+                              int32_t max_l2, int32_t hidden, int32_t aligned, const void* h, const void* hT,
+                              int32_t num_rows, const di_pair_launch* launch, void* out, void* stream) {
+  if (!descs || !h || !out || aligned < 0 || aligned > 2 || (dt != DI_BF16 && dt != DI_F32)) return DI_EINVAL;
+  if (aligned && !hT) return DI_EINVAL;
+  const int esz = dt == DI_BF16 ? 2 : 4;
+  const int rc = di_pair_tensor_check(num_complexes, max_l1, max_l2, hidden, esz, launch);
+  if (rc != DI_OK) return rc;
+  const di_pair_launch dflt = {DI_PAIR_AUTO, 0, 0, 0};
+  const di_pair_launch& L = launch ? *launch : dflt;
+  int kernel = L.kernel;
+  if (kernel == DI_PAIR_AUTO) kernel = aligned == 2 ? DI_PAIR_LINES : (aligned == 1 ? DI_PAIR_ROWS : 0);
+  if (kernel == DI_PAIR_LINES && aligned < 2) return DI_EINVAL;  // whole-line stores need 128-B planes
+  if ((kernel == DI_PAIR_ROWS || kernel == DI_PAIR_VECTOR) && aligned < 1) return DI_EINVAL;
+  const int max_blocks = L.blocks > 0 ? L.blocks : pair_num_cus();
+  const int waves = L.waves_per_block > 0 ? L.waves_per_block : 4;
+  const bool beside = L.beside != 0;
   hipStream_t s = (hipStream_t)stream;
-  // aligned16: every channel plane (L1*L2), out_off, L2 and h2_row is a multiple of 16 bytes of
-  // elements: 16-B vector loads and non-temporal 16-B stores.
-  const int vec = dt == DI_BF16 ? 8 : 4;
-#ifndef DI_PAIR_LEGACY
-  if (aligned16 && (g_pair_kernel == 1 || g_pair_kernel == 3)) {
-    const int rows = 64 * g_pair_waves;  // rows per work item
+  const int planes = num_complexes * 2 * hidden;
+  auto grid_of = [&](int items) { return dim3((unsigned)(items < max_blocks ? items : max_blocks)); };
+  if (kernel == DI_PAIR_LINES) {
+    // residue groups per plane: the largest period (p = 8 rows) over every complex's plane
+    const int64_t lines = ((int64_t)8 * max_l2 * esz) >> 7;
+    const int groups = (int)((lines + 8 * waves - 1) / (8 * waves));
+    const int items = planes * groups;
+    const dim3 g = grid_of(items), b(64 * waves);
+    if (dt == DI_BF16) {
+      if (beside) hipLaunchKernelGGL((k_pair_lines<u16, true>), g, b, 0, s, descs, hidden, (const u16*)h, (const u16*)hT, num_rows, groups, items, (u16*)out);
+      else hipLaunchKernelGGL((k_pair_lines<u16, false>), g, b, 0, s, descs, hidden, (const u16*)h, (const u16*)hT, num_rows, groups, items, (u16*)out);
+    } else {
+      if (beside) hipLaunchKernelGGL((k_pair_lines<float, true>), g, b, 0, s, descs, hidden, (const float*)h, (const float*)hT, num_rows, groups, items, (float*)out);
+      else hipLaunchKernelGGL((k_pair_lines<float, false>), g, b, 0, s, descs, hidden, (const float*)h, (const float*)hT, num_rows, groups, items, (float*)out);
+    }
+  } else if (kernel == DI_PAIR_ROWS) {
+    const int rows = 64 * waves;  // rows per work item
     const int rblocks = (max_l1 + rows - 1) / rows;
-    const int64_t ritems64 = (int64_t)num_complexes * 2 * hidden * rblocks;
-    if (ritems64 > INT32_MAX) return DI_ERANGE;
-    const int ritems = (int)ritems64;
-    const unsigned rgrid = (unsigned)(ritems < max_blocks ? ritems : max_blocks);
-    const bool bounded = g_pair_kernel == 3;
-    if (dt == DI_BF16 && bounded)
-      hipLaunchKernelGGL((k_pair_rows<u16, DI_PAIR_INFLIGHT, DI_PAIR_STORE_BESIDE>), dim3(rgrid), dim3(rows), 0, s, descs, hidden,
-                         (const u16*)h, (const u16*)hT, num_rows, rblocks, ritems, (u16*)out, g_pair_pace);
-    else if (dt == DI_BF16)
-      hipLaunchKernelGGL((k_pair_rows<u16, 0, DI_PAIR_STORE>), dim3(rgrid), dim3(rows), 0, s, descs, hidden, (const u16*)h,
-                         (const u16*)hT, num_rows, rblocks, ritems, (u16*)out, g_pair_pace);
-    else if (bounded)
-      hipLaunchKernelGGL((k_pair_rows<float, DI_PAIR_INFLIGHT, DI_PAIR_STORE_BESIDE>), dim3(rgrid), dim3(rows), 0, s, descs, hidden,
-                         (const float*)h, (const float*)hT, num_rows, rblocks, ritems, (float*)out, g_pair_pace);
-    else
-      hipLaunchKernelGGL((k_pair_rows<float, 0, DI_PAIR_STORE>), dim3(rgrid), dim3(rows), 0, s, descs, hidden,
-                         (const float*)h, (const float*)hT, num_rows, rblocks, ritems, (float*)out, g_pair_pace);
-    hipError_t e = hipGetLastError();
-    return e == hipSuccess ? DI_OK : (int)e;
-  }
-#endif
-  if (dt == DI_BF16) {
-    if (aligned16)
-      hipLaunchKernelGGL((k_pair_tensor<u16, true>), dim3(grid), dim3(PAIR_THREADS), 0, s, descs, hidden,
-                         (const u16*)h, (const u16*)hT, num_rows, chunks, items, (u16*)out, g_pair_pace);
-    else
-      hipLaunchKernelGGL((k_pair_tensor<u16, false>), dim3(grid), dim3(PAIR_THREADS), 0, s, descs, hidden,
-                         (const u16*)h, (const u16*)hT, num_rows, chunks, items, (u16*)out, g_pair_pace);
+    const int items = planes * rblocks;
+    const dim3 g = grid_of(items), b(rows);
+    if (dt == DI_BF16) {
+      if (beside) hipLaunchKernelGGL((k_pair_rows<u16, true>), g, b, 0, s, descs, hidden, (const u16*)h, (const u16*)hT, num_rows, rblocks, items, (u16*)out);
+      else hipLaunchKernelGGL((k_pair_rows<u16, false>), g, b, 0, s, descs, hidden, (const u16*)h, (const u16*)hT, num_rows, rblocks, items, (u16*)out);
+    } else {
+      if (beside) hipLaunchKernelGGL((k_pair_rows<float, true>), g, b, 0, s, descs, hidden, (const float*)h, (const float*)hT, num_rows, rblocks, items, (float*)out);
+      else hipLaunchKernelGGL((k_pair_rows<float, false>), g, b, 0, s, descs, hidden, (const float*)h, (const float*)hT, num_rows, rblocks, items, (float*)out);
+    }
   } else {
-    if (aligned16)
-      hipLaunchKernelGGL((k_pair_tensor<float, true>), dim3(grid), dim3(PAIR_THREADS), 0, s, descs, hidden,
-                         (const float*)h, (const float*)hT, num_rows, chunks, items, (float*)out, g_pair_pace);
-    else
-      hipLaunchKernelGGL((k_pair_tensor<float, false>), dim3(grid), dim3(PAIR_THREADS), 0, s, descs, hidden,
-                         (const float*)h, (const float*)hT, num_rows, chunks, items, (float*)out, g_pair_pace);
+    const int chunks = (int)(((int64_t)max_l1 * max_l2 + PAIR_CHUNK - 1) / PAIR_CHUNK);
+    const int items = planes * chunks;
+    const dim3 g = grid_of(items), b(PAIR_THREADS);
+    if (kernel == DI_PAIR_VECTOR) {
+      if (dt == DI_BF16) hipLaunchKernelGGL(k_pair_vec<u16>, g, b, 0, s, descs, hidden, (const u16*)h, (const u16*)hT, num_rows, chunks, items, (u16*)out);
+      else hipLaunchKernelGGL(k_pair_vec<float>, g, b, 0, s, descs, hidden, (const float*)h, (const float*)hT, num_rows, chunks, items, (float*)out);
+    } else {
+      if (dt == DI_BF16) hipLaunchKernelGGL(k_pair_flat<u16>, g, b, 0, s, descs, hidden, (const u16*)h, (const u16*)hT, num_rows, chunks, items, (u16*)out);
+      else hipLaunchKernelGGL(k_pair_flat<float>, g, b, 0, s, descs, hidden, (const float*)h, (const float*)hT, num_rows, chunks, items, (float*)out);
+    }
   }
-  hipError_t e = hipGetLastError();
+  const hipError_t e = hipGetLastError();
   return e == hipSuccess ? DI_OK : (int)e;
 }

@@ -223,23 +223,25 @@ class GeoTEngine:
 
 
 class PairTensorOp:
-    """construct_interact_tensor (deepinteract_utils.py:158-172) for a batch of complexes."""
+    """construct_interact_tensor (deepinteract_utils.py:158-172) for a batch of complexes.
 
-    KERNELS = {"rows": 1, "vector": 2, "rows_bounded": 3}
+    The launch (di_pair_launch) belongs to this op: kernel "auto" | "lines" | "rows" | "vector",
+    resident blocks (0: one per CU), waves per row/line block (0: 4) and ``beside`` (the schedule
+    beside a concurrent GeoT stream: a bounded store queue, non-temporal stores). Every choice
+    writes the same bytes."""
 
-    def __init__(self, device="cuda", blocks: int = 0, waves_per_block: int = 0, kernel: str | None = None,
-                 pace: int | None = None):
-        """blocks / waves_per_block / kernel ("rows" | "vector" | "rows_bounded"): launch shape and kernel of the
-        16-B-aligned path (di_pair_config; 0 / None keep the library's current setting); pace:
-        store-rate pacing, s_sleep(1) per row / vector trip (di_pair_pace; None keeps it)."""
+    KERNELS = {"auto": _lib.DI_PAIR_AUTO, "rows": _lib.DI_PAIR_ROWS, "vector": _lib.DI_PAIR_VECTOR,
+               "lines": _lib.DI_PAIR_LINES}
+
+    def __init__(self, device="cuda", kernel: str = "auto", blocks: int = 0, waves_per_block: int = 0,
+                 beside: bool = False):
         self.device = gpu_device(device)
         self.lib = _lib.load()
+        if kernel not in self.KERNELS:
+            raise ValueError(f"pair kernel {kernel!r}: one of {sorted(self.KERNELS)}")
+        self.kernel = kernel
+        self.launch = _lib.DiPairLaunch(self.KERNELS[kernel], int(blocks), int(waves_per_block), int(bool(beside)))
         self._desc_cache = {}
-        k = self.KERNELS[kernel] if kernel else 0
-        if (blocks or waves_per_block or k) and hasattr(self.lib, "di_pair_config"):
-            _lib.check(self.lib.di_pair_config(blocks, waves_per_block, k), "di_pair_config")
-        if pace is not None:
-            _lib.check(self.lib.di_pair_pace(int(pace)), "di_pair_pace")
 
     def descs(self, h1_rows, h2_rows, l1s, l2s, hidden):
         key = (tuple(h1_rows), tuple(h2_rows), tuple(l1s), tuple(l2s), hidden)
@@ -268,17 +270,25 @@ class PairTensorOp:
             out = torch.empty(total, dtype=h.dtype, device=h.device)
         elif out.numel() < total:
             raise ValueError("pair-tensor output buffer too small")
-        vec = 16 // h.element_size()
+        esz = h.element_size()
+        vec = 16 // esz
         if hT is not None and (hT.shape != (hidden, h.shape[0]) or hT.dtype != h.dtype):
             raise ValueError("hT must be h transposed")
-        aligned = hT is not None and h.shape[0] % vec == 0 and out.data_ptr() % 16 == 0 \
-            and all(l2 % vec == 0 for l2 in l2s) and all(o % vec == 0 for o in offs) \
-            and all(r % vec == 0 for r in h2_rows)
+        aligned = int(hT is not None and h.shape[0] % vec == 0 and out.data_ptr() % 16 == 0
+                      and all(l2 % vec == 0 for l2 in l2s) and all(o % vec == 0 for o in offs)
+                      and all(r % vec == 0 for r in h2_rows))
+        if aligned and out.data_ptr() % 128 == 0 and all(o * esz % 128 == 0 for o in offs) \
+                and all(l1 * l2 * esz % 128 == 0 for l1, l2 in zip(l1s, l2s)):
+            aligned = 2  # every channel plane starts on a 128-B line: whole-line stores
+        need = {"lines": 2, "rows": 1, "vector": 1}.get(self.kernel, 0)
+        if aligned < need:
+            raise ValueError(f"pair kernel {self.kernel!r} needs {'128-B' if need == 2 else '16-B'} aligned planes "
+                             f"and hT; this batch allows {['the generic', 'the 16-B', 'the 128-B'][aligned]} path")
         tick = _Ticker(events)
         tick("pair_tensor")
-        _lib.check(self.lib.di_pair_tensor(dt, _ptr(d), len(l1s), max(l1s), max(l2s), hidden, int(aligned),
-                                           _ptr(h.contiguous()), _ptr(hT), h.shape[0], _ptr(out), _stream()),
-                   "di_pair_tensor")
+        _lib.check(self.lib.di_pair_tensor(dt, _ptr(d), len(l1s), max(l1s), max(l2s), hidden, aligned,
+                                           _ptr(h.contiguous()), _ptr(hT), h.shape[0], ctypes.byref(self.launch),
+                                           _ptr(out), _stream()), "di_pair_tensor")
         tick(None)
         views = [out[o:o + 2 * hidden * l1 * l2].view(1, 2 * hidden, l1, l2)
                  for o, l1, l2 in zip(offs, l1s, l2s)]

@@ -136,11 +136,16 @@ class GraphBatch:
     """
 
     def __init__(self, src, dst, nbr, node_f, edge_f, nodes_per_graph, edges_per_graph,
-                 node_count_limit=NODE_COUNT_LIMIT, in_ptr=None, node_pos=None, geo_ref=None):
+                 node_count_limit=NODE_COUNT_LIMIT, in_ptr=None, node_pos=None, geo_ref=None,
+                 _trusted_geo_ref=None):
         """in_ptr / node_pos: precomputed by the device builder (di_knn_graph); when given, the
         destination-major order is guaranteed by construction and not re-checked on the host.
         geo_ref: whether every edge carries the reference featuriser's constant direction /
-        orientation columns (di_graph.flags DI_GRAPH_GEO_REF); None = check edge_f."""
+        orientation columns (di_graph.flags DI_GRAPH_GEO_REF): None = check edge_f; True = claimed by
+        the caller and verified (ValueError if the columns are not the constants: the kernels would
+        skip a branch that is not zero); False = the general path.
+        _trusted_geo_ref: package-internal (device builder, select_graphs, concat_batches), a value
+        known by construction; not checked."""
         self.src, self.dst, self.nbr = src, dst, nbr
         self.node_f, self.edge_f = node_f, edge_f
         self.nodes_per_graph = [int(x) for x in nodes_per_graph]
@@ -172,7 +177,17 @@ class GraphBatch:
         for n, e in zip(self.nodes_per_graph, self.edges_per_graph):
             self.node_off.append(self.node_off[-1] + n)
             self.edge_off.append(self.edge_off[-1] + e)
-        self.geo_ref = edge_feats_geo_ref(edge_f) if geo_ref is None else bool(geo_ref) and self.num_edges > 0
+        if _trusted_geo_ref is not None:
+            self.geo_ref = bool(_trusted_geo_ref) and self.num_edges > 0
+        elif geo_ref is None:
+            self.geo_ref = edge_feats_geo_ref(edge_f)
+        elif geo_ref:
+            if not edge_feats_geo_ref(edge_f):
+                raise ValueError("geo_ref=True but the edge features do not carry the reference featuriser's "
+                                 "constant direction / orientation columns (edge_f[:, 20:27])")
+            self.geo_ref = True
+        else:
+            self.geo_ref = False
         self._c = DiGraph(self.num_nodes, self.num_edges, self.src.data_ptr(), self.dst.data_ptr(),
                           self.nbr.data_ptr(), self.node_pos.data_ptr(), self.in_ptr.data_ptr(),
                           DI_GRAPH_GEO_REF if self.geo_ref else 0)
@@ -259,7 +274,7 @@ def concat_batches(batches: Sequence[GraphBatch]) -> GraphBatch:
                       torch.cat(nfs).contiguous(), torch.cat(efs).contiguous(), nn, ne,
                       node_count_limit=max(b.node_count_limit for b in batches),
                       in_ptr=torch.cat(ptrs).contiguous(), node_pos=torch.cat(poss).contiguous(),
-                      geo_ref=all(b.geo_ref for b in batches))
+                      _trusted_geo_ref=all(b.geo_ref for b in batches))
 
 
 def select_graphs(gb: GraphBatch, indices: Sequence[int]) -> GraphBatch:
@@ -270,5 +285,6 @@ def select_graphs(gb: GraphBatch, indices: Sequence[int]) -> GraphBatch:
         e0, e1 = gb.edge_off[g], gb.edge_off[g + 1]
         parts.append(GraphBatch(gb.src[e0:e1] - n0, gb.dst[e0:e1] - n0, gb.nbr[e0:e1] - e0, gb.node_f[n0:n1],
                                 gb.edge_f[e0:e1], [n1 - n0], [e1 - e0], node_count_limit=gb.node_count_limit,
-                                in_ptr=gb.in_ptr[n0:n1 + 1] - e0, node_pos=gb.node_pos[n0:n1], geo_ref=gb.geo_ref))
+                                in_ptr=gb.in_ptr[n0:n1 + 1] - e0, node_pos=gb.node_pos[n0:n1],
+                                _trusted_geo_ref=gb.geo_ref))
     return concat_batches(parts)

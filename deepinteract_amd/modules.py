@@ -50,8 +50,8 @@ class DGLGeometricTransformer(nn.Module):
                               node_count_limit=node_count_limit, num_node_input_feats=num_hidden_channels)
         if num_hidden_channels != 128 or num_attention_heads != 4:
             raise NotImplementedError("kernels are specialised for 128 hidden channels, 4 heads")
-        if not 0 < node_count_limit <= 4096:
-            raise NotImplementedError("max_num_graph_nodes above 4096 (the on-device kNN's row limit)")
+        if node_count_limit <= 0:
+            raise ValueError("max_num_graph_nodes must be positive")
         self.dtype = dtype
         self.engine = None
 
@@ -88,8 +88,10 @@ class LitGINI(nn.Module):
             # Q/K/V are Linear(H, H) whatever the head count, so a checkpoint trained with another
             # head count would load and silently compute 4-head attention
             raise NotImplementedError("the GeoT kernels are specialised for 128 hidden channels, 4 heads")
-        if not 0 < max_num_graph_nodes <= 4096:
-            raise NotImplementedError("max_num_graph_nodes above 4096 (the on-device kNN's row limit)")
+        if max_num_graph_nodes <= 0:
+            # the GeoT kernels need only node_pos < max_num_graph_nodes (the positional table's rows);
+            # the on-device graph builder's own chain limit (4096) is enforced where it is used
+            raise ValueError("max_num_graph_nodes must be positive")
         self.cfg = GeoTConfig(num_node_input_feats=num_node_input_feats, num_gnn_layers=num_gnn_layers,
                               num_gnn_hidden_channels=num_gnn_hidden_channels,
                               num_gnn_attention_heads=num_gnn_attention_heads, knn=knn,

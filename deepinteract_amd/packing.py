@@ -28,9 +28,8 @@ def _l2e(dtype: str) -> float:
 # ---- csrc/layout.h mirror -------------------------------------------------------------------
 EM_NBLK, EMV_N = 128, 384
 IE_NBLK, IEV_N = 288, 384
-EL_NBLK, ELV_N = 764 + 384, 2560
-EL_NBLK_FINAL, ELV_N_FINAL = 572 + 384, 2048
-EL_R16_INT, EL_R16_FIN = 764, 572
+EL_NBLK, ELV_N = 764, 2560
+EL_NBLK_FINAL, ELV_N_FINAL = 572, 2048
 NL_NBLK, NLV_N = 256, 768
 NL_NBLK_FINAL, NLV_N_FINAL = 160, 384
 EL_NBLK_CONF, ELV_N_CONF = 540, 1920
@@ -137,7 +136,6 @@ class BlobBuilder:
         self.mat = np.zeros(nblk * BLK, dtype=np.float64)
         self.vec = np.zeros(nvec, dtype=np.float64)
         self.used = np.zeros(nblk, dtype=bool)
-        self.f16 = []
 
     def put(self, blk_off: int, w):
         p = pack_matrix(w, self.dtype)
@@ -152,21 +150,11 @@ class BlobBuilder:
         assert off + v.size <= self.nvec
         self.vec[off:off + v.size] = v
 
-    def put_f16(self, blk_off: int, w):
-        """bf16 blobs: a region holding f16 bit patterns (fragment order as put()); fp32 blobs keep
-        the fp32 values (the region is read only by the bf16 grouped kernel's f16 ResBlocks)."""
-        self.put(blk_off, w)
-        self.f16.append((blk_off, pack_matrix(w, self.dtype).size // BLK))
-
     def finish(self):
         assert self.used.all(), np.nonzero(~self.used)[0][:8]
         t = torch.from_numpy(self.mat).to(torch.float32)
         if self.dtype == "bf16":
             t = t.to(torch.bfloat16)
-            bits = t.view(torch.int16)
-            for off, n in self.f16:
-                lo, hi = off * BLK, (off + n) * BLK
-                bits[lo:hi] = torch.from_numpy(self.mat[lo:hi].astype(np.float16).view(np.int16))
         return t, torch.from_numpy(self.vec).to(torch.float32)
 
 
@@ -280,8 +268,6 @@ def edge_blob(sd, li, final, dtype, cfg: GeoTConfig, conf_only=False, c=None):
                 w_in = 1.0 if l == 0 else 1.0 / sc   # input in log2 units after layers 0 and 3
                 w_out = sc                           # every layer feeds silu2 (layer 6: ln2 in the residual fma)
                 bb.put(84 + 32 * i, w * (w_in * w_out))
-                if not conf_only:
-                    bb.put_f16((EL_R16_FIN if final else EL_R16_INT) + 32 * i, w * (w_in * w_out))
                 bb.putv(128 + 128 * i, b * w_out)
                 i += 1
     w, b = lin(sd, f"{c}.res_connect_linear")  # silu2, ln2 folded into the residual fma

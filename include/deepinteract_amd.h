@@ -45,15 +45,19 @@
 extern "C" {
 #endif
 
-#define DI_ABI_VERSION 2
+#define DI_ABI_VERSION 3
 
-/* activation / weight storage type of the GeoT kernels (accumulation is always fp32) */
-typedef enum { DI_F32 = 0, DI_BF16 = 1 } di_dtype;
+/* activation / weight storage type of the GeoT kernels (accumulation is always fp32). A plain
+ * int32 (not a C enum type): a foreign caller may pass any value, and every entry point refuses
+ * values other than DI_F32 / DI_BF16 with DI_EINVAL (a C++ enum holding 5 would be undefined
+ * behaviour before the check could run; found by the host UBSan build). */
+enum { DI_F32 = 0, DI_BF16 = 1 };
+typedef int32_t di_dtype;
 
 enum {
   DI_OK = 0,
   DI_EINVAL = -1,   /* bad shape / null pointer / unsupported config */
-  DI_ERANGE = -2,   /* a chain exceeds NODE_COUNT_LIMIT (reference raises IndexError) */
+  DI_ERANGE = -2,   /* a size beyond the kernels' index range (see each entry point) */
 };
 
 /* A batch of residue graphs (one graph per chain, concatenated). Edges are destination-major:
@@ -114,11 +118,6 @@ int di_edge_layer(const di_graph* g, di_dtype dt, int final_layer, const float* 
                   const void* f_in, const void* fn_in, const void* qkv,
                   const void* wmat, const float* wvec,
                   float* alpha_out /*[Et,4]*/, void* f_out, void* fn_out, void* stream);
-/* Edge-layer kernel of the bf16 path (process-wide scheduling knob, not a reference interface):
- * 0 = two 4-wave blocks per CU, 16 rows per wave; 1 (default) = grouped form, two 4-wave blocks
- * per CU, two 16-row groups per wave sharing every LDS weight fragment. -1 only queries.
- * Returns the previous choice. */
-int di_edge_config(int32_t kernel);
 
 /* hT_out (optional, may be NULL): also write h_out transposed, [128, Nt] (pair-tensor input) */
 int di_node_layer(const di_graph* g, di_dtype dt, int final_layer, const float* alpha,
@@ -136,26 +135,37 @@ int di_node_update(const di_graph* g, di_dtype dt, int final_layer, const float*
                    const void* h_in, const void* wmat, const float* wvec, void* h_out, void* qkv_out,
                    void* hT_out, void* stream);
 
-/* h [Nt, hidden] node features; hT (optional, may be NULL) the same transposed [hidden, Nt]
- * (di_node_layer's hT_out), which turns chain-2 column reads into 16-B vector loads.
- * aligned16 != 0 promises every L1*L2 plane, out_off, L2 and h2_row are multiples of 16 bytes
- * worth of elements (vector loads/stores). Output stores are non-temporal (write-once stream). */
-/* Launch shape of the persistent pair-tensor kernels (process-wide; 0 keeps a value): `blocks`
- * resident blocks, `waves_per_block` (1..16) waves per row-streaming block, `kernel` for the
- * 16-B-aligned case: 1 row-streaming (loads hoisted out of the store stream; fastest alone),
- * 2 per-vector (one load per 16-B store), 3 row-streaming with at most a few stores in flight
- * per wave (the schedule beside GeoT: its loads do not queue behind a long store backlog).
- * Defaults 256 / 4 / 1 (env DI_PAIR_BLOCKS / DI_PAIR_WAVES / DI_PAIR_KERNEL). Not a reference
- * interface: a scheduling knob of this build. */
-int di_pair_config(int32_t blocks, int32_t waves_per_block, int32_t kernel);
-/* Store-rate pacing of the aligned pair kernels (scheduling knob, not a reference interface):
- * every wave sleeps pace x ~64 clocks after each row (row kernel) / vector trip (vector kernel),
- * leaving the memory pipeline headroom for a concurrent GeoT stream. Default 0 (env DI_PAIR_PACE). */
-int di_pair_pace(int32_t pace);
+/* Pair-tensor kernel of a di_pair_tensor call (di_pair_launch.kernel). Scheduling choice of this
+ * build, not a reference interface; every kernel writes the same bytes. */
+enum {
+  DI_PAIR_AUTO = 0,    /* LINES for aligned == 2, ROWS for aligned == 1, the generic kernel otherwise */
+  DI_PAIR_ROWS = 1,    /* a wave streams 64 whole rows (needs aligned >= 1) */
+  DI_PAIR_VECTOR = 2,  /* one 16-B load per 16-B store over flat plane positions (aligned >= 1) */
+  DI_PAIR_LINES = 3,   /* every store writes whole 128-B lines (aligned == 2) */
+};
+/* Launch of one di_pair_tensor call (host struct; NULL = all defaults). */
+typedef struct {
+  int32_t kernel;           /* DI_PAIR_* */
+  int32_t blocks;           /* resident blocks of the persistent grid; 0 = one per CU */
+  int32_t waves_per_block;  /* ROWS / LINES: 1..16 waves per block; 0 = 4 */
+  int32_t beside;           /* 1: the schedule beside a concurrent GeoT stream: at most 3 stores in
+                               flight per wave (its loads do not queue behind a store backlog) and
+                               non-temporal stores; 0: plain stores, unbounded */
+} di_pair_launch;
 
+/* h [Nt, hidden] node features; hT (optional for aligned == 0) the same transposed [hidden, Nt]
+ * (di_node_layer's hT_out), which turns chain-2 column reads into 16-B vector loads.
+ * aligned: 0 none; 1 promises every L2, out_off and h2_row is a multiple of 16 bytes worth of
+ * elements and `out` is 16-B aligned (vector stores); 2 additionally promises every channel plane
+ * starts on a 128-B line (out 128-B aligned, out_off * elem and L1 * L2 * elem multiples of 128).
+ * Limits: L1 * L2 * elem < 2^31 bytes per plane, L1 <= 2^20 (di_pair_tensor_check). */
 int di_pair_tensor(di_dtype dt, const di_pair_desc* descs /*device [B]*/, int32_t num_complexes,
-                   int32_t max_l1, int32_t max_l2, int32_t hidden, int32_t aligned16, const void* h,
-                   const void* hT, int32_t num_rows, void* out, void* stream);
+                   int32_t max_l1, int32_t max_l2, int32_t hidden, int32_t aligned, const void* h,
+                   const void* hT, int32_t num_rows, const di_pair_launch* launch, void* out, void* stream);
+/* The shape / launch validation di_pair_tensor applies before launching (host only): DI_OK,
+ * DI_EINVAL or DI_ERANGE. elem_bytes: 2 (bf16) or 4 (fp32). */
+int di_pair_tensor_check(int32_t num_complexes, int32_t max_l1, int32_t max_l2, int32_t hidden, int32_t elem_bytes,
+                         const di_pair_launch* launch);
 
 /* Fused head prologue: x = ELU(InstanceNorm2d(conv2d_1(T))) of the contact
  * head (ResNet2DInputWithOptAttention.forward, deepinteract_modules.py:1181-1184, 1228-1232) for a
@@ -231,7 +241,8 @@ int di_build_nbr_ids(int32_t num_edges, const int32_t* src, const int32_t* dst, 
  * calls then E dst calls). kNN graphs only (uniform in-degree k, dst-major edges, k >= 3).
  * node_off [G+1], seeds [G] (device); num_nodes = node_off[G]; src/dst [Et = num_nodes*k] global
  * node ids; nbr_out [Et,4] global ids. Two launches: the per-chain mt19937 streams (one wave per
- * chain) write the kept in-edge positions, then every id gets its endpoint's in-edge base. */
+ * chain) write the kept in-edge positions, then every id gets its endpoint's in-edge base.
+ * DI_ERANGE when 2 * num_nodes * k * (k-1) exceeds INT32_MAX (a chain's draw count is int32). */
 int di_build_nbr_ids_torch(int32_t num_graphs, const int32_t* node_off, int32_t k, const uint64_t* seeds,
                            int32_t num_nodes, const int32_t* src, const int32_t* dst, int32_t* nbr_out, void* stream);
 

@@ -25,7 +25,7 @@ def test_library_builds_and_exports_all_declared_symbols():
 
 def test_abi_version_and_blob_sizes():
     lib = _lib.load()
-    assert lib.di_abi_version() == 2
+    assert lib.di_abi_version() == _lib.ABI_VERSION == 3
     for kind, (nblk, nvec) in packing.BLOB_SIZES.items():
         assert lib.di_blob_bytes(kind, _lib.DI_F32, 0) == nblk * 512 * 4
         assert lib.di_blob_bytes(kind, _lib.DI_BF16, 0) == nblk * 512 * 2
@@ -36,13 +36,37 @@ def test_abi_version_and_blob_sizes():
 def test_invalid_arguments_rejected_without_gpu():
     lib = _lib.load()
     assert lib.di_node_embed(None, 0, 113, None, None, None, None, None, None) == -1
-    assert lib.di_pair_tensor(0, None, 0, 0, 0, 128, 1, None, None, 0, None, None) == -1
+    assert lib.di_pair_tensor(0, None, 0, 0, 0, 128, 1, None, None, 0, None, None, None) == -1
     assert lib.di_knn_topk(1, None, None, 20, 10, None, None, None) == -1
-    assert lib.di_pair_config(-1, 4, 0) == -1 and lib.di_pair_config(0, 17, 0) == -1
-    assert lib.di_pair_config(0, 0, 4) == -1
-    assert lib.di_pair_config(0, 0, 0) == 0  # keeps the current launch shape
     assert lib.di_head_prologue(0, None, 1, 8, 8, 128, 128, 1, None, None, None, None, None, 1e-6,
                                 None, None, None) == -1
+
+
+def test_pair_tensor_check_shapes_and_launch():
+    """di_pair_tensor's host-side validation (di_pair_tensor_check), without a GPU: the model limit
+    4096 x 4096 (plane = 2^24 elements, refused with DI_ERANGE in round 2) passes in both dtypes;
+    planes of 2^31 bytes and more, and more than 2^20 rows, are DI_ERANGE; bad launches DI_EINVAL."""
+    import ctypes
+    lib = _lib.load()
+    L = _lib.DiPairLaunch
+    assert lib.di_pair_tensor_check(1, 4096, 4096, 128, 2, None) == 0
+    assert lib.di_pair_tensor_check(8, 4096, 4096, 128, 4, None) == 0
+    assert lib.di_pair_tensor_check(64, 1000, 1000, 128, 2, None) == 0
+    assert lib.di_pair_tensor_check(1, 32768, 32768, 128, 2, None) == -2   # 2 GiB plane
+    assert lib.di_pair_tensor_check(1, 1 << 21, 8, 128, 2, None) == -2     # row index range
+    assert lib.di_pair_tensor_check(0, 10, 10, 128, 2, None) == -1
+    assert lib.di_pair_tensor_check(1, 10, 10, 128, 3, None) == -1
+    for launch, rc in ((L(_lib.DI_PAIR_LINES, 0, 2, 1), 0), (L(4, 0, 0, 0), -1), (L(-1, 0, 0, 0), -1),
+                       (L(0, -1, 0, 0), -1), (L(0, 0, 17, 0), -1), (L(0, 0, 0, 2), -1)):
+        assert lib.di_pair_tensor_check(1, 64, 64, 128, 2, ctypes.byref(launch)) == rc, (launch.kernel, rc)
+    # the lines kernel needs 128-B aligned planes (aligned == 2), rows / vector 16-B ones: refused
+    # before any launch (dummy non-NULL pointers are never dereferenced on these paths)
+    p = ctypes.c_void_p(16)
+    for kernel, aligned in ((_lib.DI_PAIR_LINES, 1), (_lib.DI_PAIR_ROWS, 0), (_lib.DI_PAIR_VECTOR, 0)):
+        launch = L(kernel, 0, 0, 0)
+        assert lib.di_pair_tensor(1, p, 1, 64, 64, 128, aligned, p, p, 128, ctypes.byref(launch), p, None) == -1
+    assert lib.di_pair_tensor(1, p, 1, 64, 64, 128, 3, p, p, 128, None, p, None) == -1
+    assert lib.di_pair_tensor(1, p, 1, 64, 64, 128, 1, p, None, 128, None, p, None) == -1  # aligned needs hT
 
 
 def test_geo_ref_fn_contract_without_gpu():

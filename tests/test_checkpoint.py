@@ -84,6 +84,23 @@ def test_litgini_passes_max_num_graph_nodes_to_config():
     from deepinteract_amd.modules import LitGINI
     assert LitGINI(max_num_graph_nodes=4096).cfg.node_count_limit == 4096
     assert LitGINI().cfg.node_count_limit == 2304
+    # a checkpoint with a larger positional table loads: the GeoT kernels only need
+    # node_pos < max_num_graph_nodes; the on-device builder's 4096-residue chain limit is its own
+    assert LitGINI(max_num_graph_nodes=8192).cfg.node_count_limit == 8192
+    with pytest.raises(ValueError):
+        LitGINI(max_num_graph_nodes=0)
+
+
+def test_builder_refuses_chains_beyond_the_knn_limit():
+    """build_graph_batch raises before touching the device for a chain beyond the kNN's 4096 rows
+    (even when the model's positional table is larger)."""
+    import numpy as np
+    from deepinteract_amd.builder import build_graph_batch
+    n = 4097
+    ch = {"backbone": np.zeros((n, 4, 3), np.float32), "amide_norm": np.zeros((n, 3), np.float32),
+          "dips": np.zeros((n, 106), np.float32)}
+    with pytest.raises(NotImplementedError):
+        build_graph_batch([ch], node_count_limit=8192, device="cuda")
 
 
 def test_load_on_cpu_does_not_touch_the_gpu_and_refuses_cpu_compute(tmp_path):

@@ -46,6 +46,27 @@ def test_geo_ref_detection_and_propagation():
     assert not edge_feats_geo_ref(torch.zeros(4, 28)) and not edge_feats_geo_ref(None)
 
 
+def test_geo_ref_claim_is_verified():
+    """A caller's geo_ref=True is checked against the columns: wrong edge features raise instead of
+    letting the kernels skip a branch that is not zero; the package-internal trusted
+    path (device builder, select_graphs, concat_batches) carries the flag without a check."""
+    from deepinteract_amd.graph import concat_batches, select_graphs
+    z = load_case("tiny")
+    items = [chain_item(z, "g1"), chain_item(z, "g2")]
+    ok = GraphBatch.from_arrays(items, "cpu")
+    args = (ok.src, ok.dst, ok.nbr, ok.node_f, ok.edge_f, ok.nodes_per_graph, ok.edges_per_graph)
+    assert GraphBatch(*args, geo_ref=True).geo_ref
+    assert not GraphBatch(*args, geo_ref=False).geo_ref
+    ef = ok.edge_f.clone()
+    ef[7, 21] = 0.5  # a non-zero direction column
+    bad = (ok.src, ok.dst, ok.nbr, ok.node_f, ef, ok.nodes_per_graph, ok.edges_per_graph)
+    with pytest.raises(ValueError):
+        GraphBatch(*bad, geo_ref=True)
+    assert not GraphBatch(*bad).geo_ref
+    assert select_graphs(ok, [1, 0]).geo_ref and concat_batches([ok, ok]).geo_ref
+    assert not select_graphs(ok.with_geo_ref(False), [0]).geo_ref
+
+
 @pytest.mark.parametrize("case", ["tiny", "c1"])
 def test_conformation_neighbour_messages_vanish(case):
     """The message branch of ConformationModule (oracle restatement of :384-418) is exactly zero

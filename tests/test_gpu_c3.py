@@ -1,8 +1,9 @@
 """C3 parity on the benchmark's own path (BASELINE configs[2]; bench.py step()): synthetic 2x1000
 heterodimers built on the device (kNN, features, torch-seeded neighbour ids), micro-batches of 8
 complexes concatenated as the bench does, bf16 GeoT in two workspace slots on stream A, the
-'vector' pair-tensor kernel reading hT on stream B, cross-stream events between them, three
-micro-batches so slot 0 is reused after its pair tensor has drained.
+pair-tensor kernel reading hT on stream B (the bench's whole-line kernel with its bounded store
+queue, and the per-vector kernel), cross-stream events between them, three micro-batches so slot 0
+is reused after its pair tensor has drained.
 
 Checked against the oracle (fp32 CPU restatement of the reference, pinned to the reference's own
 modules by test_oracle_golden.py) on the same device-built graphs:
@@ -34,11 +35,11 @@ def _oracle_graph(gb, g):
             "edge_f": gb.edge_f[e0:e1].cpu()}
 
 
-@pytest.mark.parametrize("edge_kernel,pair_kernel,side", [(1, "rows_bounded", True), (0, "vector", False)])
-def test_c3_bench_path_bf16_two_slots_two_streams(edge_kernel, pair_kernel, side):
+@pytest.mark.parametrize("pair_kernel,side", [("lines", True), ("vector", False)])
+def test_c3_bench_path_bf16_two_slots_two_streams(pair_kernel, side):
     """side: bench.py's overlapped defaults — node embedding on a side stream beside InitEdge and the
     fused node layer."""
-    from deepinteract_amd import _lib, synth
+    from deepinteract_amd import synth
     from deepinteract_amd.builder import build_graph_batch
     from deepinteract_amd.engine import GeoTEngine, PairTensorOp
     from deepinteract_amd.graph import select_graphs
@@ -58,34 +59,30 @@ def test_c3_bench_path_bf16_two_slots_two_streams(edge_kernel, pair_kernel, side
     h1r = [gb0.node_off[2 * j] for j in range(M)]
     h2r = [gb0.node_off[2 * j + 1] for j in range(M)]
     l1 = l2 = [N_RES] * M
-    # bench.py's schedule beside GeoT: the bounded row-streaming kernel in one 2-wave block per CU
-    pair = PairTensorOp(kernel=pair_kernel, waves_per_block=2 if pair_kernel == "rows_bounded" else 0)
-    prev = _lib.load().di_edge_config(edge_kernel)
-    try:
-        s_geot = torch.cuda.current_stream()
-        s_pair = torch.cuda.Stream()
-        done, keep = [None, None], []
-        for m, gb in enumerate(mbs):
-            slot = m & 1
-            with torch.cuda.stream(s_geot):
-                if done[slot] is not None:
-                    s_geot.wait_event(done[slot])
-                h, e = eng.forward(gb, clone=False, slot=slot)
-                hT = eng.last_hT
-                ready = torch.cuda.Event()
-                ready.record(s_geot)
-            with torch.cuda.stream(s_pair):
-                s_pair.wait_event(ready)
-                out, views = pair(h, h1r, h2r, l1, l2, hT=hT)
-                hc, ec = h.clone(), e.clone()   # snapshot of this slot before it is reused
-                ev = torch.cuda.Event()
-                ev.record(s_pair)
-                done[slot] = ev
-            keep.append((hc, ec, views))
-        torch.cuda.synchronize()
-    finally:
-        PairTensorOp(kernel="rows", waves_per_block=4)  # process-wide launch knobs back to their defaults
-        _lib.load().di_edge_config(prev)
+    # bench.py's schedule beside GeoT: whole-line pair stores with a bounded store queue, one 2-wave
+    # block per CU
+    pair = PairTensorOp(kernel=pair_kernel, waves_per_block=2 if side else 0, beside=side)
+    s_geot = torch.cuda.current_stream()
+    s_pair = torch.cuda.Stream()
+    done, keep = [None, None], []
+    for m, gb in enumerate(mbs):
+        slot = m & 1
+        with torch.cuda.stream(s_geot):
+            if done[slot] is not None:
+                s_geot.wait_event(done[slot])
+            h, e = eng.forward(gb, clone=False, slot=slot)
+            hT = eng.last_hT
+            ready = torch.cuda.Event()
+            ready.record(s_geot)
+        with torch.cuda.stream(s_pair):
+            s_pair.wait_event(ready)
+            out, views = pair(h, h1r, h2r, l1, l2, hT=hT)
+            hc, ec = h.clone(), e.clone()   # snapshot of this slot before it is reused
+            ev = torch.cuda.Event()
+            ev.record(s_pair)
+            done[slot] = ev
+        keep.append((hc, ec, views))
+    torch.cuda.synchronize()
 
     errs = {}
     for m, j in ((0, 0), (0, 5), (2, 3)):
@@ -112,7 +109,7 @@ def test_c3_bench_path_bf16_two_slots_two_streams(edge_kernel, pair_kernel, side
         pt = O.pair_tensor(ref[0], ref[1])[0].numpy()
         got = t[0][torch.as_tensor(idx[:, 0]), torch.as_tensor(idx[:, 1]), torch.as_tensor(idx[:, 2])]
         errs[f"mb{m}_c{j}_pair"] = rel_max(got.float().cpu().numpy(), pt[idx[:, 0], idx[:, 1], idx[:, 2]])
-    print(f"C3 bf16 errors, edge kernel {edge_kernel}, pair kernel {pair_kernel} (max-abs / max-abs ref):", {k: f"{v:.3e}" for k, v in errs.items()})
+    print(f"C3 bf16 errors, pair kernel {pair_kernel} (max-abs / max-abs ref):", {k: f"{v:.3e}" for k, v in errs.items()})
     assert max(errs.values()) < BF16_GEOT_TOL, errs
 
 

@@ -104,18 +104,33 @@ def test_pair_tensor_batched_bf16_unaligned():
         assert torch.equal(v, ref)
 
 
-@pytest.mark.parametrize("kernel,waves", [("rows", 4), ("rows_bounded", 2), ("vector", 4), ("rows", 1)])
-@pytest.mark.parametrize("dtype,sizes", [
-    (torch.bfloat16, [(16, 24), (264, 8), (520, 1000), (8, 4104)]),   # 4104: 5 row segments
-    (torch.float32, [(12, 4), (300, 1000), (4, 2052)]),
-])
-def test_pair_tensor_batched_aligned(dtype, sizes, kernel, waves):
-    """Ragged aligned batch through each aligned kernel (row-streaming, row-streaming with bounded
-    in-flight stores, per-vector) and row-block shape: planes spanning several row blocks, rows
-    spanning several 128-chunk segments, varying L1/L2 per complex."""
+def _pair_ref_check(h, sizes, h1r, h2r, views):
+    for (a, b), s1, s2, v in zip(sizes, h1r, h2r, views):
+        ref = torch.cat((h[s1:s1 + a].t().unsqueeze(0).unsqueeze(3).expand(1, 128, a, b),
+                         h[s2:s2 + b].t().unsqueeze(0).unsqueeze(2).expand(1, 128, a, b)), 1)
+        assert torch.equal(v, ref)
+
+
+# every plane of these batches starts on a 128-B line (lines-eligible); row bytes 48 / 16 / 2000 /
+# 8208 (bf16) and 16 / 4000 / 8208 (fp32) give periods of 8 rows = 3 / 1 / 125 / 513 lines
+_LINES_SIZES = {torch.bfloat16: [(16, 24), (264, 8), (520, 1000), (8, 4104)],
+                torch.float32: [(8, 4), (304, 1000), (8, 2052)]}
+# 16-B aligned (row / vector kernels; the fp32 (12, 4) plane is not line aligned)
+_ROW_SIZES = {torch.bfloat16: [(16, 24), (264, 8), (520, 1000), (8, 4104)],   # 4104: 5 row segments
+              torch.float32: [(12, 4), (300, 1000), (4, 2052)]}
+
+
+@pytest.mark.parametrize("kernel,waves,beside", [("lines", 4, False), ("lines", 2, True), ("lines", 1, False),
+                                                 ("rows", 4, False), ("rows", 2, True), ("rows", 1, False),
+                                                 ("vector", 4, False), ("auto", 0, False)])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_pair_tensor_batched_aligned(dtype, kernel, waves, beside):
+    """Ragged aligned batch through each aligned kernel and launch shape (every launch is the op's
+    own: no process-wide state): planes spanning several row blocks / line periods, rows spanning
+    several 128-chunk segments, varying L1/L2 per complex."""
     from deepinteract_amd.engine import PairTensorOp
-    PairTensorOp(kernel=kernel, waves_per_block=waves)
     torch.manual_seed(1)
+    sizes = (_LINES_SIZES if kernel in ("lines", "auto") else _ROW_SIZES)[dtype]
     rows = sum(a + b for a, b in sizes)
     h = torch.randn(rows, 128, device="cuda").to(dtype)
     h1r, h2r, r = [], [], 0
@@ -123,15 +138,43 @@ def test_pair_tensor_batched_aligned(dtype, sizes, kernel, waves):
         h1r.append(r)
         h2r.append(r + a)
         r += a + b
-    try:
-        _, views = PairTensorOp()(h, h1r, h2r, [a for a, _ in sizes], [b for _, b in sizes], hT=h.t().contiguous())
-        torch.cuda.synchronize()
-    finally:
-        PairTensorOp(kernel="rows", waves_per_block=4)  # process-wide knobs back to the defaults
-    for (a, b), s1, s2, v in zip(sizes, h1r, h2r, views):
-        ref = torch.cat((h[s1:s1 + a].t().unsqueeze(0).unsqueeze(3).expand(1, 128, a, b),
-                         h[s2:s2 + b].t().unsqueeze(0).unsqueeze(2).expand(1, 128, a, b)), 1)
-        assert torch.equal(v, ref)
+    op = PairTensorOp(kernel=kernel, waves_per_block=waves, beside=beside)
+    _, views = op(h, h1r, h2r, [a for a, _ in sizes], [b for _, b in sizes], hT=h.t().contiguous())
+    torch.cuda.synchronize()
+    _pair_ref_check(h, sizes, h1r, h2r, views)
+
+
+def test_pair_tensor_lines_refuses_unaligned_planes():
+    """A 16-B-aligned batch whose planes do not start on 128-B lines: the lines kernel is refused
+    (ValueError before any launch), auto takes the row kernel."""
+    from deepinteract_amd.engine import PairTensorOp
+    sizes = [(12, 4), (300, 1000)]
+    h = torch.randn(sum(a + b for a, b in sizes), 128, device="cuda")
+    h1r, h2r = [0, 16], [12, 316]
+    with pytest.raises(ValueError):
+        PairTensorOp(kernel="lines")(h, h1r, h2r, [12, 300], [4, 1000], hT=h.t().contiguous())
+    _, views = PairTensorOp()(h, h1r, h2r, [12, 300], [4, 1000], hT=h.t().contiguous())
+    torch.cuda.synchronize()
+    _pair_ref_check(h, sizes, h1r, h2r, views)
+
+
+@pytest.mark.parametrize("kernel,beside", [("lines", True), ("rows", False), ("vector", False)])
+def test_pair_tensor_4096_square(kernel, beside):
+    """The model limit (max_num_graph_nodes 4096): one 4096 x 4096 complex, bf16, [256, 4096, 4096]
+    = 8.6 GB; plane = 2^24 elements (round 2 refused it with DI_ERANGE). Every channel plane is
+    compared with its inputs, 32 channels at a time."""
+    from deepinteract_amd.engine import PairTensorOp
+    n = 4096
+    torch.manual_seed(2)
+    h = torch.randn(2 * n, 128, device="cuda").to(torch.bfloat16)
+    out, views = PairTensorOp(kernel=kernel, beside=beside)(h, [0], [n], [n], [n], hT=h.t().contiguous())
+    torch.cuda.synchronize()
+    t = views[0][0]
+    for c0 in range(0, 128, 32):
+        assert torch.equal(t[c0:c0 + 32], h[:n, c0:c0 + 32].t().unsqueeze(2).expand(32, n, n))
+        assert torch.equal(t[128 + c0:128 + c0 + 32], h[n:, c0:c0 + 32].t().unsqueeze(1).expand(32, n, n))
+    del out, views, t
+    torch.cuda.empty_cache()
 
 
 @pytest.mark.parametrize("case", ["knn1k", "tiny", "c1", "c2"])

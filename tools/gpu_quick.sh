@@ -5,5 +5,4 @@ tools/gpu_run.sh \
  "t_aggr:300:python -u -m pytest -x -v --timeout 240 --timeout-method thread tests/test_gpu_node_aggr.py tests/test_gpu_edge_lean.py" \
  "b_ser:240:python bench.py --no-cpu --no-prologue --overlap 0 --complexes 256 --steps 2 --warmup 1 > gpurun_out/b_ser.json" \
  "b_ov:240:python bench.py --no-cpu --no-prologue --complexes 256 --steps 4 --warmup 1 > gpurun_out/b_ov.json" || exit $?
-[ -n "$VARIANTS" ] && NO_PMC=1 OVS="0 1" bash tools/lean_sweep.sh
 exit 0

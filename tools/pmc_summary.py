@@ -18,11 +18,12 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 NAMES = {
-    "k_node_embed": "node_embed", "k_init_edge": "init_edge", "k_edge_layer<di::BF16T, 0>": "edge_layer",
-    "k_edge_layer<di::BF16T, 1>": "edge_layer_final", "k_node_layer<di::BF16T, false>": "node_layer",
+    "k_node_embed": "node_embed", "k_init_edge": "init_edge", "k_edge_layer<di::F32T, 0": "edge_layer",
+    "k_edge_layer<di::F32T, 1": "edge_layer_final", "k_node_layer<di::BF16T, false>": "node_layer",
     "k_node_layer<di::BF16T, true>": "node_layer_final",
     "k_edge_lean<0": "edge_layer", "k_edge_lean<1": "edge_layer_final", "k_node_aggr<di::BF16T>": "node_aggr",
-    "k_node_update_ring<false>": "node_layer", "k_node_update_ring<true>": "node_layer_final", "k_pair_tensor": "pair_tensor", "k_pair_rows": "pair_tensor",
+    "k_node_update_ring<false>": "node_layer", "k_node_update_ring<true>": "node_layer_final", "k_pair_lines": "pair_tensor", "k_pair_rows": "pair_tensor", "k_pair_vec": "pair_tensor",
+    "k_pair_flat": "pair_tensor",
     "k_prologue_rows": "head_prologue_rows", "k_prologue_tables": "head_prologue_tables",
     "k_knn": "knn", "k_geo_feats": "geo_feats", "k_geo_stats": "geo_stats", "k_nbr_ids": "nbr_ids",
 }

@@ -5,5 +5,5 @@
 cd "${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 mapfile -t S < "${1:-tools/_specs.txt}"
 tools/gpu_run.sh "${S[@]}" || exit $?
-[ -n "$CNT_LIB" ] && TAG=$CNT_TAG BENCH_EXTRA="--edge-kernel 1" tools/counters.sh "$CNT_LIB"
+[ -n "$CNT_LIB" ] && TAG=$CNT_TAG tools/counters.sh "$CNT_LIB"
 exit 0
