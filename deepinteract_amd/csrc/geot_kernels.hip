@@ -620,6 +620,79 @@ __device__ __forceinline__ void lin_groups(Act<NBO> (&out)[Lean::LG], const Op<B
   }
   mma_ring2<NBO, NS>(out[0], out[1], op[0], op[1], w, lane);
 }
+// Pipelined form of lin_groups + epilogue, used by every stage with a SiLU: the stage's MFMAs run
+// output-block-pair major, and the epilogue of pair p-1 (SiLU, pack or residual: epi(q, p - 1) for
+// both groups) is issued BETWEEN the 16 MFMAs of pair p -- 4 VALU instructions per MFMA,
+// sched_group_barrier-placed -- so a wave's own SiLU work runs while its MFMAs are in the matrix
+// pipe instead of after them; pair 3's epilogue follows the loop. Measured (C3, round 3, same box):
+// edge layer alone 323 vs 331 us, final 258 vs 267 us; beside the pair stream 423-431 vs 429-437 us;
+// 2 / 3 / 5 VALU per MFMA within noise of 4. The gain is small because the edge layers are bound by
+// the SIMD's issue of SiLU VALU work (v_exp / v_rcp at 8 cycles) plus the MFMA's issue hold, not
+// by the two failing to overlap (tools/diag/silu_overlap_bench.hip).
+constexpr int PIPE_NV = 4;
+template <int NS, class Epi>
+__device__ __forceinline__ void lin_groups_pipe(Act<8> (&out)[Lean::LG], const Op<BF16T, NS> (&op)[Lean::LG],
+                                                const u16* w, const float* bias, int lane, int g, Epi&& epi) {
+  constexpr int NBO = 8, G = 2, N = NBO * NS, D = MMA_DEPTH < N ? MMA_DEPTH : N;
+  constexpr int PSTEPS = G * NS;  // fragment steps per output-block pair
+#pragma unroll
+  for (int q = 0; q < Lean::LG; ++q) {
+    if (bias) init_vec_lds(out[q], bias, g);
+    else zero(out[q]);
+  }
+  auto blk = [](int i) { return (i / (G * NS)) * G + (i % G); };
+  auto kst = [](int i) { return (i % (G * NS)) / G; };
+  bf16x8 fr[D];
+#pragma unroll
+  for (int i = 0; i < D; ++i)
+    fr[i] = *reinterpret_cast<const bf16x8*>(w + (blk(i) * NS + kst(i)) * BLK + lane * 8);
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int p = 0; p < NBO / G; ++p) {
+#pragma unroll
+    for (int j = 0; j < PSTEPS; ++j) {
+      const int i = p * PSTEPS + j;
+      const int bo = blk(i), s = kst(i);
+      out[0].v[bo] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[i % D], op[0].f[s], out[0].v[bo], 0, 0, 0);
+      out[1].v[bo] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[i % D], op[1].f[s], out[1].v[bo], 0, 0, 0);
+      if (i + D < N)
+        fr[i % D] = *reinterpret_cast<const bf16x8*>(w + (blk(i + D) * NS + kst(i + D)) * BLK + lane * 8);
+    }
+    if (p > 0) {
+      epi(0, p - 1);
+      epi(1, p - 1);
+    }
+    // per fragment step: its two MFMAs, each followed by up to PIPE_NV VALU, then the step's LDS read
+#pragma unroll
+    for (int j = 0; j < PSTEPS; ++j) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x402, PIPE_NV, 0);  // VALU | TRANS
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x402, PIPE_NV, 0);  // VALU | TRANS
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  epi(0, NBO / G - 1);
+  epi(1, NBO / G - 1);
+}
+
+// epilogue pieces on output-block pair p (blocks 2p, 2p+1) of an activation
+__device__ __forceinline__ void silu2_pair(Act<8>& a, int p) {
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) a.v[2 * p + h][r] = silu2<true>(a.v[2 * p + h][r]);
+}
+__device__ __forceinline__ void pack_pair(Op<BF16T, 4>& o, const Act<8>& a, int p) {
+  uint4 u;
+  u.x = pack_bf16x2(a.v[2 * p][0], a.v[2 * p][1]);
+  u.y = pack_bf16x2(a.v[2 * p][2], a.v[2 * p][3]);
+  u.z = pack_bf16x2(a.v[2 * p + 1][0], a.v[2 * p + 1][1]);
+  u.w = pack_bf16x2(a.v[2 * p + 1][2], a.v[2 * p + 1][3]);
+  o.f[p] = __builtin_bit_cast(bf16x8, u);
+}
+
 using LeanPipe = WPipe<u16, Lean::NW, true, EL_CAP, 128>;
 
 // stage sequencer of one tile: next() publishes stage i and issues the DMA of stage i + 1.
@@ -672,24 +745,33 @@ __device__ __forceinline__ void lean_res_block(Act<8> (&x)[Lean::LG], LeanStages
   Op<BF16T, 4> op[Lean::LG];
 #pragma unroll
   for (int q = 0; q < Lean::LG; ++q) make_op(op[q], x[q]);
+
 #pragma unroll 1
-  for (int l = 0; l < 3; ++l) {
+  for (int l = 0; l < 2; ++l) {
     const u16* w = st.next();
     Act<8> t[Lean::LG];
-    lin_groups<8, 4>(t, op, w, st.v(), lane, g);
+    Op<BF16T, 4> opn[Lean::LG];
+    // layers 0, 1: t = silu2(W op + b) packed as the next layer's operand
+    lin_groups_pipe<4>(t, op, w, st.v(), lane, g, [&](int q, int p) {
+      silu2_pair(t[q], p);
+      pack_pair(opn[q], t[q], p);
+    });
 #pragma unroll
     for (int q = 0; q < Lean::LG; ++q) {
-      lean_fence();
-      silu2_<8, true>(t[q]);  // log2 units: folded into the next linear / the residual fma
-      if (l < 2) {
-        make_op(op[q], t[q]);
-        pin(op[q]);
-      } else {
-        add_scaled_(x[q], t[q], silu2_unit<true>());
-        pin(x[q]);
-      }
+      op[q] = opn[q];
+      pin(op[q]);
     }
   }
+  const u16* w = st.next();
+  Act<8> t[Lean::LG];
+  // layer 2: x += ln2 * silu2(W op + b)
+  lin_groups_pipe<4>(t, op, w, st.v(), lane, g, [&](int q, int p) {
+    silu2_pair(t[q], p);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) x[q].v[2 * p + h] += silu2_unit<true>() * t[q].v[2 * p + h];
+  });
+#pragma unroll
+  for (int q = 0; q < Lean::LG; ++q) pin(x[q]);
 }
 
 // y = silu2(W x + b); x = F + ln2 * y  (res_connect_linear / final_linear residual)
@@ -706,15 +788,20 @@ __device__ __forceinline__ void lean_f_residual(Act<8> (&x)[Lean::LG], const u16
 #pragma unroll
   for (int q = 0; q < Lean::LG; ++q) make_op(op[q], x[q]);
   Act<8> y[Lean::LG];
-  lin_groups<8, 4>(y, op, w, v, lane, g);
+  // x = F + ln2 * silu2(W x + b), pair by pair (F: the edge's own bf16 row, exact in fp32)
+  lin_groups_pipe<4>(y, op, w, v, lane, g, [&](int q, int p) {
+    silu2_pair(y[q], p);
 #pragma unroll
-  for (int q = 0; q < Lean::LG; ++q) {
-    lean_fence();
-    silu2_<8, true>(y[q]);
-    fr[q].to_act(x[q]);
-    add_scaled_(x[q], y[q], silu2_unit<true>());
-    pin(x[q]);
-  }
+    for (int h = 0; h < 2; ++h) {
+      const int b = 2 * p + h;
+      const uint2 u = fr[q].u[b];
+      const floatx4 f = {__builtin_bit_cast(float, u.x << 16), __builtin_bit_cast(float, u.x & 0xffff0000u),
+                         __builtin_bit_cast(float, u.y << 16), __builtin_bit_cast(float, u.y & 0xffff0000u)};
+      x[q].v[b] = f + silu2_unit<true>() * y[q].v[b];
+    }
+  });
+#pragma unroll
+  for (int q = 0; q < Lean::LG; ++q) pin(x[q]);
 }
 
 template <int MODE, bool GC>
@@ -950,14 +1037,12 @@ void k_edge_lean(EdgeArgs a) {
       w = st.next();  // edge_feats_MLP.0 (BN2e folded), hidden half
       Op<BF16T, 4> top[LG];
       Act<8> t[LG];
-      lin_groups<8, 4>(t, eop, w, st.v(), lane, g);
+      lin_groups_pipe<4>(t, eop, w, st.v(), lane, g, [&](int q, int p) {
+        silu2_pair(t[q], p);
+        pack_pair(top[q], t[q], p);
+      });
 #pragma unroll
-      for (int q = 0; q < LG; ++q) {
-        lean_fence();
-        silu2_<8, true>(t[q]);
-        make_op(top[q], t[q]);
-        pin(top[q]);
-      }
+      for (int q = 0; q < LG; ++q) pin(top[q]);
       w = st.next();  // edge_feats_MLP.3, input half: accumulated into the residual
       mma_ring2<8, 4>(e1[0], e1[1], top[0], top[1], w, lane);
 #pragma unroll
@@ -987,17 +1072,17 @@ void k_edge_lean(EdgeArgs a) {
 // (send_and_recv(u_mul_e('V_h','score'), sum) and (copy_e('score'), sum), then wV / (z + 1e-6):
 // deepinteract_modules.py:93-96, 116). Edges are destination-major (CSR in_ptr), so a node's
 // in-edges are one contiguous range.
-// 16 lanes per destination, 8 features (16 B of bf16) per lane: a gathered V row is one coalesced
-// 256-B access. In-edges go in chunks of U: the chunk's source ids arrive with ONE coalesced load
-// (lane j of the node's 16 reads src[e0 + j], broadcast by ds_bpermute) and the next chunk's ids are
-// in flight while this chunk's alphas and V rows land, so a chunk costs one memory latency; U rows
-// per lane in flight and 16 nodes per 256-thread block (grid = Nt / 16, several blocks per CU) hide
-// it. The products are added one edge at a time in edge order with the same fused multiply-adds as
-// the fused node kernel, so h_attn is bit-identical to what k_node_layer computes internally.
-template <class DT>
-struct AggrCfg {
-  static constexpr int U = DT::kBF16 ? 16 : 8;  // in-edges per chunk (V bytes in flight per lane: U x 16/32)
-};
+// One WAVE per destination (16k destinations of a C3 micro-batch = 64 waves per CU, so the gathers
+// of many destinations are in flight at once). The wave's four 16-lane slots take in-edges
+// round-robin (slot s: edges e0 + s, e0 + s + 4, ...); lane j of a slot owns features 8j .. 8j+7
+// (head j / 4), so every wave-instruction gathers FOUR whole V[src] rows (4 x 256 B bf16) with
+// 16-B lane loads, a 16-edge chunk's loads are all in flight before its first product, and each
+// slot accumulates its edges in edge order. The four slot partials are then combined across lanes
+// as (s0 + s2) + (s1 + s3) (v_permlane32_swap, v_permlane16_swap: no LDS) and slot 0 writes the
+// 512-B fp32 row. (A different summation order from k_node_layer's in-edge-order sums: the two
+// agree to fp32 rounding, tests/test_gpu_node_aggr.py.)
+constexpr int AGG_WAVES = 4;  // destinations per 256-thread block
+constexpr int AGG_CHUNK = 16; // in-edges per chunk (4 per slot)
 struct AggrArgs {
   int Nt;
   const int* src;
@@ -1007,69 +1092,97 @@ struct AggrArgs {
   float* attn;
 };
 
+// x + x[lane ^ 32] and x + x[lane ^ 16] on gfx950's lane-swap instructions
+__device__ __forceinline__ float add_xor32(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(int, x), __builtin_bit_cast(int, x), false, false);
+  return __builtin_bit_cast(float, r[0]) + __builtin_bit_cast(float, r[1]);
+}
+__device__ __forceinline__ float add_xor16(float x) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(int, x), __builtin_bit_cast(int, x), false, false);
+  return __builtin_bit_cast(float, r[0]) + __builtin_bit_cast(float, r[1]);
+}
+
 template <class DT>
-__global__ __launch_bounds__(256) void k_node_aggr(AggrArgs a) {
+__global__ __launch_bounds__(64 * AGG_WAVES) void k_node_aggr(AggrArgs a) {
   using T = typename DT::T;
-  constexpr int U = AggrCfg<DT>::U;
   constexpr int FPL = 8;  // features per lane
-  const int j = threadIdx.x & 15;
-  const int v = blockIdx.x * 16 + (threadIdx.x >> 4);
-  if (v >= a.Nt) return;  // whole 16-lane groups exit together (shuffles stay within a group)
-  const int head = (FPL * j) >> 5;
-  const T* vbase = reinterpret_cast<const T*>(a.qkv) + 2 * HID + FPL * j;
-  const int e0 = a.in_ptr[v], e1 = a.in_ptr[v + 1];
+  const int v = __builtin_amdgcn_readfirstlane(blockIdx.x * AGG_WAVES + (threadIdx.x >> 6));
+  if (v >= a.Nt) return;  // whole waves
+  const int lane = threadIdx.x & 63, slot = lane >> 4, j = lane & 15, head = j >> 2;
+  const int e0 = __builtin_amdgcn_readfirstlane(a.in_ptr[v]);
+  const int e1 = __builtin_amdgcn_readfirstlane(a.in_ptr[v + 1]);
+  const T* vcol = reinterpret_cast<const T*>(a.qkv) + 2 * HID + FPL * j;  // this lane's 8 features of V
   float acc[FPL];
 #pragma unroll
   for (int f = 0; f < FPL; ++f) acc[f] = 0.f;
   float z = 0.f;
-  const int lane_base = threadIdx.x & 48;  // first lane of this node's 16 (within the wave)
-  int id_next = e0 + j < e1 ? a.src[e0 + j] : 0;
-#pragma unroll 1
-  for (int c = e0; c < e1; c += U) {
-    const int n = min(U, e1 - c);
-    // this chunk's ids (lanes 0..n-1 of the group hold them) and alphas / V rows in flight
-    const int id_cur = id_next;
-    int ids[U];
+  // in-edge e's 8 V features (source node sid) and alpha for this lane
+  auto load_edge = [&](int e, int sid, float& al, float (&x)[FPL]) {
+    al = a.alpha[(int64_t)e * 4 + head];
+    const T* row = vcol + (int64_t)sid * 3 * HID;
+    if constexpr (DT::kBF16) {
+      const uint4 w = *reinterpret_cast<const uint4*>(row);
+      const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
-    for (int u = 0; u < U; ++u) ids[u] = __shfl(id_cur, lane_base + (u & 15), 64);
-    float al[U];
-    T vv[U][FPL];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if (u < n) {
-        al[u] = a.alpha[(int64_t)(c + u) * 4 + head];
-        const T* row = vbase + (int64_t)ids[u] * 3 * HID;
-        if constexpr (DT::kBF16) {
-          *reinterpret_cast<uint4*>(vv[u]) = *reinterpret_cast<const uint4*>(row);
-        } else {
-          *reinterpret_cast<float4*>(vv[u]) = *reinterpret_cast<const float4*>(row);
-          *reinterpret_cast<float4*>(vv[u] + 4) = *reinterpret_cast<const float4*>(row + 4);
-        }
+      for (int q = 0; q < 4; ++q) {
+        x[2 * q] = __builtin_bit_cast(float, ws[q] << 16);
+        x[2 * q + 1] = __builtin_bit_cast(float, ws[q] & 0xffff0000u);
       }
+    } else {
+      const float4 w0 = *reinterpret_cast<const float4*>(row);
+      const float4 w1 = *reinterpret_cast<const float4*>(row + 4);
+      x[0] = w0.x; x[1] = w0.y; x[2] = w0.z; x[3] = w0.w;
+      x[4] = w1.x; x[5] = w1.y; x[6] = w1.z; x[7] = w1.w;
     }
-    // ids of the next chunk (U <= 16 lanes of the group)
-    if (c + U < e1) id_next = c + U + j < e1 && j < U ? a.src[c + U + j] : 0;
+  };
+  auto accumulate = [&](float al, const float (&x)[FPL]) {
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if (u < n) {
+    for (int f = 0; f < FPL; ++f) acc[f] += al * x[f];
+    z += al;
+  };
+  int c = e0;
+  // whole chunks: 4 edges per slot, all in flight; the next chunk's source ids load under this
+  // chunk's row gathers
+  int sid[4];
+  if (c + AGG_CHUNK <= e1) {
 #pragma unroll
-        for (int f = 0; f < FPL; ++f) {
-          float x;
-          if constexpr (DT::kBF16) x = __builtin_bit_cast(float, (uint32_t)vv[u][f] << 16);
-          else x = vv[u][f];
-          acc[f] += al[u] * x;
-        }
-        z += al[u];
-      }
+    for (int u = 0; u < 4; ++u) sid[u] = a.src[c + 4 * u + slot];
+  }
+#pragma unroll 1
+  for (; c + AGG_CHUNK <= e1; c += AGG_CHUNK) {
+    float al[4], x[4][FPL];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) load_edge(c + 4 * u + slot, sid[u], al[u], x[u]);
+    const int cn = c + AGG_CHUNK;
+    if (cn + AGG_CHUNK <= e1) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) sid[u] = a.src[cn + 4 * u + slot];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) accumulate(al[u], x[u]);
+  }
+#pragma unroll 1
+  for (; c < e1; c += 4) {  // the tail, 4 edges (one per slot) at a time
+    const int e = c + slot;
+    if (e < e1) {
+      float al, x[FPL];
+      load_edge(e, a.src[e], al, x);
+      accumulate(al, x);
     }
   }
-  const float d = z + 1e-6f;
-  float4 o0, o1;
-  o0.x = acc[0] / d; o0.y = acc[1] / d; o0.z = acc[2] / d; o0.w = acc[3] / d;
-  o1.x = acc[4] / d; o1.y = acc[5] / d; o1.z = acc[6] / d; o1.w = acc[7] / d;
-  float* out = a.attn + (int64_t)v * HID + FPL * j;
-  *reinterpret_cast<float4*>(out) = o0;
-  *reinterpret_cast<float4*>(out + 4) = o1;
+  // (s0 + s2) + (s1 + s3) in every slot
+#pragma unroll
+  for (int f = 0; f < FPL; ++f) acc[f] = add_xor16(add_xor32(acc[f]));
+  z = add_xor16(add_xor32(z));
+  if (slot == 0) {
+    const float d = z + 1e-6f;
+    float4 o0, o1;
+    o0.x = acc[0] / d; o0.y = acc[1] / d; o0.z = acc[2] / d; o0.w = acc[3] / d;
+    o1.x = acc[4] / d; o1.y = acc[5] / d; o1.z = acc[6] / d; o1.w = acc[7] / d;
+    float* out = a.attn + (int64_t)v * HID + FPL * j;
+    *reinterpret_cast<float4*>(out) = o0;
+    *reinterpret_cast<float4*>(out + 4) = o1;
+  }
 }
 
 // ================================================================ node update (bf16), 4-slot weight ring
@@ -1481,7 +1594,7 @@ extern "C" int di_node_aggregate(const di_graph* g, di_dtype dt, const float* al
     return DI_EINVAL;
   AggrArgs a{g->num_nodes, g->src, g->in_ptr, alpha, qkv, attn_out};
   hipStream_t s = (hipStream_t)stream;
-  dim3 grid((a.Nt + 15) / 16), block(256);
+  const dim3 grid((unsigned)((a.Nt + AGG_WAVES - 1) / AGG_WAVES)), block(64 * AGG_WAVES);
   if (dt == DI_BF16) hipLaunchKernelGGL(k_node_aggr<BF16T>, grid, block, 0, s, a);
   else hipLaunchKernelGGL(k_node_aggr<F32T>, grid, block, 0, s, a);
   return launch_status();

@@ -8,7 +8,7 @@
 //
 // Kernels (di_pair_launch.kernel; all persistent, no LDS, so they co-reside with the GeoT kernels
 // of the other stream, which hold the LDS):
-//  * k_pair_lines (DI_PAIR_LINES, the default for 128-B-aligned planes): every store instruction
+//  * k_pair_lines (DI_PAIR_LINES, 128-B-aligned planes; measured slower, see di_pair_tensor): every store instruction
 //    writes whole 128-B lines. A channel plane repeats with a period of p = 128 / gcd(row bytes,
 //    128) rows (p <= 8; 2000-B rows: p = 8 rows = 125 lines), so line r + P t of the plane holds the
 //    same bytes for every t (chain 2) or the same bytes of rows p t .. p t + p - 1 (chain 1). A wave
@@ -16,7 +16,7 @@
 //    and address, the period offset in an SGPR. Row-by-row streaming (k_pair_rows) splits the
 //    128-B line at every row boundary between two partial writes (+2.9 % write traffic measured
 //    at 2000-B rows).
-//  * k_pair_rows (DI_PAIR_ROWS): a wave owns 64 whole rows; the row vector (chain 2) / row value
+//  * k_pair_rows (DI_PAIR_ROWS, the default): a wave owns 64 whole rows; the row vector (chain 2) / row value
 //    (chain 1) is loaded once per 128-chunk segment, then only stores (16-B aligned planes).
 //  * k_pair_vec (DI_PAIR_VECTOR): one 16-B load per 16-B store over flat plane positions.
 //  * k_pair_flat: any shape / alignment, one element per thread and step.
@@ -350,7 +350,11 @@ extern "C" int di_pair_tensor(di_dtype dt, const di_pair_desc* descs, int32_t nu
   const di_pair_launch dflt = {DI_PAIR_AUTO, 0, 0, 0};
   const di_pair_launch& L = launch ? *launch : dflt;
   int kernel = L.kernel;
-  if (kernel == DI_PAIR_AUTO) kernel = aligned == 2 ? DI_PAIR_LINES : (aligned == 1 ? DI_PAIR_ROWS : 0);
+  // auto: row streaming for any aligned plane. Whole-line stores measured slower (C3, round 3): alone
+  // 866 vs 751 us per 4.1 GB (4 waves), 774 vs 757 (8 waves); beside GeoT 7111-7257 vs 7425-7615
+  // complexes/s -- each wave's 1-KiB stores stride by the 16-KB row period instead of streaming
+  // contiguous rows, which costs more than the +2.9 % partial-line writes they remove
+  if (kernel == DI_PAIR_AUTO) kernel = aligned >= 1 ? DI_PAIR_ROWS : 0;
   if (kernel == DI_PAIR_LINES && aligned < 2) return DI_EINVAL;  // whole-line stores need 128-B planes
   if ((kernel == DI_PAIR_ROWS || kernel == DI_PAIR_VECTOR) && aligned < 1) return DI_EINVAL;
   const int max_blocks = L.blocks > 0 ? L.blocks : pair_num_cus();

@@ -82,9 +82,9 @@ class GeoTEngine:
         self.packed = PackedGeoT(state_dict, dtype, cfg, self.device)
         self._check_blob_sizes()
         self._ws = {}
-        # node layer as two launches (di_node_aggregate + di_node_update; bit-identical to the
-        # fused di_node_layer): the segment reduction at full occupancy instead of 16 lanes per
-        # node inside the MFMA kernel's one-block-per-CU grid
+        # node layer as two launches (di_node_aggregate + di_node_update; equal to the fused
+        # di_node_layer up to fp32 summation order): the segment reduction one wave per
+        # destination at full occupancy instead of inside the MFMA kernel's one-block-per-CU grid
         self.split_node = True
         # optional side stream for the node embedding (concurrent with InitEdge)
         self.embed_stream = None

@@ -128,7 +128,8 @@ int di_node_layer(const di_graph* g, di_dtype dt, int final_layer, const float* 
  * (copy_e, sum) + wV / (z + 1e-6), deepinteract_modules.py:93-96, 116):
  *   attn_out[v, :] = sum_{e: dst(e) = v} alpha[e, head] * V[src(e), :] / (sum_e alpha[e, head] + 1e-6)
  * (fp32 [Nt, 128]; V = columns 256..383 of qkv), then O_node + residual + FFN (+ next layer's
- * Q/K/V, + optional transposed copy) from those rows. Bit-identical to di_node_layer. */
+ * Q/K/V, + optional transposed copy) from those rows. Equal to di_node_layer up to the fp32
+ * summation order of the in-edges (one wave per destination, four interleaved partial sums). */
 int di_node_aggregate(const di_graph* g, di_dtype dt, const float* alpha /*[Et,4]*/, const void* qkv /*[Nt,384]*/,
                       float* attn_out /*[Nt,128]*/, void* stream);
 int di_node_update(const di_graph* g, di_dtype dt, int final_layer, const float* attn /*[Nt,128]*/,
@@ -138,7 +139,7 @@ int di_node_update(const di_graph* g, di_dtype dt, int final_layer, const float*
 /* Pair-tensor kernel of a di_pair_tensor call (di_pair_launch.kernel). Scheduling choice of this
  * build, not a reference interface; every kernel writes the same bytes. */
 enum {
-  DI_PAIR_AUTO = 0,    /* LINES for aligned == 2, ROWS for aligned == 1, the generic kernel otherwise */
+  DI_PAIR_AUTO = 0,    /* ROWS for aligned >= 1, the generic kernel otherwise */
   DI_PAIR_ROWS = 1,    /* a wave streams 64 whole rows (needs aligned >= 1) */
   DI_PAIR_VECTOR = 2,  /* one 16-B load per 16-B store over flat plane positions (aligned >= 1) */
   DI_PAIR_LINES = 3,   /* every store writes whole 128-B lines (aligned == 2) */

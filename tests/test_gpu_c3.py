@@ -1,7 +1,7 @@
 """C3 parity on the benchmark's own path (BASELINE configs[2]; bench.py step()): synthetic 2x1000
 heterodimers built on the device (kNN, features, torch-seeded neighbour ids), micro-batches of 8
 complexes concatenated as the bench does, bf16 GeoT in two workspace slots on stream A, the
-pair-tensor kernel reading hT on stream B (the bench's whole-line kernel with its bounded store
+pair-tensor kernel reading hT on stream B (the bench's row-streaming kernel with its bounded store
 queue, and the per-vector kernel), cross-stream events between them, three micro-batches so slot 0
 is reused after its pair tensor has drained.
 
@@ -35,7 +35,7 @@ def _oracle_graph(gb, g):
             "edge_f": gb.edge_f[e0:e1].cpu()}
 
 
-@pytest.mark.parametrize("pair_kernel,side", [("lines", True), ("vector", False)])
+@pytest.mark.parametrize("pair_kernel,side", [("auto", True), ("vector", False)])
 def test_c3_bench_path_bf16_two_slots_two_streams(pair_kernel, side):
     """side: bench.py's overlapped defaults — node embedding on a side stream beside InitEdge and the
     fused node layer."""
@@ -59,7 +59,7 @@ def test_c3_bench_path_bf16_two_slots_two_streams(pair_kernel, side):
     h1r = [gb0.node_off[2 * j] for j in range(M)]
     h2r = [gb0.node_off[2 * j + 1] for j in range(M)]
     l1 = l2 = [N_RES] * M
-    # bench.py's schedule beside GeoT: whole-line pair stores with a bounded store queue, one 2-wave
+    # bench.py's schedule beside GeoT: row-streaming pair stores with a bounded store queue, one 2-wave
     # block per CU
     pair = PairTensorOp(kernel=pair_kernel, waves_per_block=2 if side else 0, beside=side)
     s_geot = torch.cuda.current_stream()
