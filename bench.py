@@ -453,7 +453,7 @@ def main():
                          "GeoT on the other CUs (needs --overlap 1)")
     ap.add_argument("--cu-layout", default="stride", choices=["stride", "contig"])
     ap.add_argument("--pair-kernel", default="auto", choices=["auto", "lines", "rows", "vector"],
-                    help="pair-tensor kernel (auto: whole-line stores for 128-B aligned planes)")
+                    help="pair-tensor kernel (auto: row streaming for 16-B aligned planes, per-vector otherwise)")
     ap.add_argument("--pair-blocks", type=int, default=0)
     ap.add_argument("--pair-waves", type=int, default=0, help="waves per pair block (default: 2 beside GeoT, 4 alone)")
     ap.add_argument("--pair-beside", type=int, default=None, choices=[0, 1],

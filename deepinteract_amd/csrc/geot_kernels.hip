@@ -1072,17 +1072,18 @@ void k_edge_lean(EdgeArgs a) {
 // (send_and_recv(u_mul_e('V_h','score'), sum) and (copy_e('score'), sum), then wV / (z + 1e-6):
 // deepinteract_modules.py:93-96, 116). Edges are destination-major (CSR in_ptr), so a node's
 // in-edges are one contiguous range.
-// One WAVE per destination (16k destinations of a C3 micro-batch = 64 waves per CU, so the gathers
-// of many destinations are in flight at once). The wave's four 16-lane slots take in-edges
-// round-robin (slot s: edges e0 + s, e0 + s + 4, ...); lane j of a slot owns features 8j .. 8j+7
-// (head j / 4), so every wave-instruction gathers FOUR whole V[src] rows (4 x 256 B bf16) with
-// 16-B lane loads, a 16-edge chunk's loads are all in flight before its first product, and each
-// slot accumulates its edges in edge order. The four slot partials are then combined across lanes
-// as (s0 + s2) + (s1 + s3) (v_permlane32_swap, v_permlane16_swap: no LDS) and slot 0 writes the
-// 512-B fp32 row. (A different summation order from k_node_layer's in-edge-order sums: the two
-// agree to fp32 rounding, tests/test_gpu_node_aggr.py.)
-constexpr int AGG_WAVES = 4;  // destinations per 256-thread block
-constexpr int AGG_CHUNK = 16; // in-edges per chunk (4 per slot)
+// 16 lanes per destination, 8 features (16 B of bf16) per lane: a gathered V row is one coalesced
+// 256-B access. In-edges go in chunks of U: the chunk's source ids arrive with ONE coalesced load
+// (lane j of the node's 16 reads src[e0 + j], broadcast by ds_bpermute) and the next chunk's ids are
+// in flight while this chunk's alphas and V rows land, so a chunk costs one memory latency; U rows
+// per lane in flight and 16 nodes per 256-thread block (grid = Nt / 16, several blocks per CU) hide
+// it. The products are added one edge at a time in edge order with the same fused multiply-adds as
+// the fused node kernel, so h_attn is bit-identical to what k_node_layer computes internally.
+constexpr int AGG_NODES = 16;  // destinations per block (16 lanes each)
+template <class DT>
+struct AggrCfg {
+  static constexpr int U = DT::kBF16 ? 16 : 8;  // in-edges per chunk (V bytes in flight per lane: U x 16/32)
+};
 struct AggrArgs {
   int Nt;
   const int* src;
@@ -1092,97 +1093,69 @@ struct AggrArgs {
   float* attn;
 };
 
-// x + x[lane ^ 32] and x + x[lane ^ 16] on gfx950's lane-swap instructions
-__device__ __forceinline__ float add_xor32(float x) {
-  const auto r = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(int, x), __builtin_bit_cast(int, x), false, false);
-  return __builtin_bit_cast(float, r[0]) + __builtin_bit_cast(float, r[1]);
-}
-__device__ __forceinline__ float add_xor16(float x) {
-  const auto r = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(int, x), __builtin_bit_cast(int, x), false, false);
-  return __builtin_bit_cast(float, r[0]) + __builtin_bit_cast(float, r[1]);
-}
-
 template <class DT>
-__global__ __launch_bounds__(64 * AGG_WAVES) void k_node_aggr(AggrArgs a) {
+__global__ __launch_bounds__(16 * AGG_NODES) void k_node_aggr(AggrArgs a) {
   using T = typename DT::T;
+  constexpr int U = AggrCfg<DT>::U;
   constexpr int FPL = 8;  // features per lane
-  const int v = __builtin_amdgcn_readfirstlane(blockIdx.x * AGG_WAVES + (threadIdx.x >> 6));
-  if (v >= a.Nt) return;  // whole waves
-  const int lane = threadIdx.x & 63, slot = lane >> 4, j = lane & 15, head = j >> 2;
-  const int e0 = __builtin_amdgcn_readfirstlane(a.in_ptr[v]);
-  const int e1 = __builtin_amdgcn_readfirstlane(a.in_ptr[v + 1]);
-  const T* vcol = reinterpret_cast<const T*>(a.qkv) + 2 * HID + FPL * j;  // this lane's 8 features of V
+  const int j = threadIdx.x & 15;
+  const int v = blockIdx.x * AGG_NODES + (threadIdx.x >> 4);
+  if (v >= a.Nt) return;  // whole 16-lane groups exit together (shuffles stay within a group)
+  const int head = (FPL * j) >> 5;
+  const T* vbase = reinterpret_cast<const T*>(a.qkv) + 2 * HID + FPL * j;
+  const int e0 = a.in_ptr[v], e1 = a.in_ptr[v + 1];
   float acc[FPL];
 #pragma unroll
   for (int f = 0; f < FPL; ++f) acc[f] = 0.f;
   float z = 0.f;
-  // in-edge e's 8 V features (source node sid) and alpha for this lane
-  auto load_edge = [&](int e, int sid, float& al, float (&x)[FPL]) {
-    al = a.alpha[(int64_t)e * 4 + head];
-    const T* row = vcol + (int64_t)sid * 3 * HID;
-    if constexpr (DT::kBF16) {
-      const uint4 w = *reinterpret_cast<const uint4*>(row);
-      const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+  const int lane_base = threadIdx.x & 48;  // first lane of this node's 16 (within the wave)
+  int id_next = e0 + j < e1 ? a.src[e0 + j] : 0;
+#pragma unroll 1
+  for (int c = e0; c < e1; c += U) {
+    const int n = min(U, e1 - c);
+    // this chunk's ids (lanes 0..n-1 of the group hold them) and alphas / V rows in flight
+    const int id_cur = id_next;
+    int ids[U];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        x[2 * q] = __builtin_bit_cast(float, ws[q] << 16);
-        x[2 * q + 1] = __builtin_bit_cast(float, ws[q] & 0xffff0000u);
+    for (int u = 0; u < U; ++u) ids[u] = __shfl(id_cur, lane_base + (u & 15), 64);
+    float al[U];
+    T vv[U][FPL];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (u < n) {
+        al[u] = a.alpha[(int64_t)(c + u) * 4 + head];
+        const T* row = vbase + (int64_t)ids[u] * 3 * HID;
+        if constexpr (DT::kBF16) {
+          *reinterpret_cast<uint4*>(vv[u]) = *reinterpret_cast<const uint4*>(row);
+        } else {
+          *reinterpret_cast<float4*>(vv[u]) = *reinterpret_cast<const float4*>(row);
+          *reinterpret_cast<float4*>(vv[u] + 4) = *reinterpret_cast<const float4*>(row + 4);
+        }
       }
-    } else {
-      const float4 w0 = *reinterpret_cast<const float4*>(row);
-      const float4 w1 = *reinterpret_cast<const float4*>(row + 4);
-      x[0] = w0.x; x[1] = w0.y; x[2] = w0.z; x[3] = w0.w;
-      x[4] = w1.x; x[5] = w1.y; x[6] = w1.z; x[7] = w1.w;
     }
-  };
-  auto accumulate = [&](float al, const float (&x)[FPL]) {
+    // ids of the next chunk (U <= 16 lanes of the group)
+    if (c + U < e1) id_next = c + U + j < e1 && j < U ? a.src[c + U + j] : 0;
 #pragma unroll
-    for (int f = 0; f < FPL; ++f) acc[f] += al * x[f];
-    z += al;
-  };
-  int c = e0;
-  // whole chunks: 4 edges per slot, all in flight; the next chunk's source ids load under this
-  // chunk's row gathers
-  int sid[4];
-  if (c + AGG_CHUNK <= e1) {
+    for (int u = 0; u < U; ++u) {
+      if (u < n) {
 #pragma unroll
-    for (int u = 0; u < 4; ++u) sid[u] = a.src[c + 4 * u + slot];
-  }
-#pragma unroll 1
-  for (; c + AGG_CHUNK <= e1; c += AGG_CHUNK) {
-    float al[4], x[4][FPL];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) load_edge(c + 4 * u + slot, sid[u], al[u], x[u]);
-    const int cn = c + AGG_CHUNK;
-    if (cn + AGG_CHUNK <= e1) {
-#pragma unroll
-      for (int u = 0; u < 4; ++u) sid[u] = a.src[cn + 4 * u + slot];
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) accumulate(al[u], x[u]);
-  }
-#pragma unroll 1
-  for (; c < e1; c += 4) {  // the tail, 4 edges (one per slot) at a time
-    const int e = c + slot;
-    if (e < e1) {
-      float al, x[FPL];
-      load_edge(e, a.src[e], al, x);
-      accumulate(al, x);
+        for (int f = 0; f < FPL; ++f) {
+          float x;
+          if constexpr (DT::kBF16) x = __builtin_bit_cast(float, (uint32_t)vv[u][f] << 16);
+          else x = vv[u][f];
+          acc[f] += al[u] * x;
+        }
+        z += al[u];
+      }
     }
   }
-  // (s0 + s2) + (s1 + s3) in every slot
-#pragma unroll
-  for (int f = 0; f < FPL; ++f) acc[f] = add_xor16(add_xor32(acc[f]));
-  z = add_xor16(add_xor32(z));
-  if (slot == 0) {
-    const float d = z + 1e-6f;
-    float4 o0, o1;
-    o0.x = acc[0] / d; o0.y = acc[1] / d; o0.z = acc[2] / d; o0.w = acc[3] / d;
-    o1.x = acc[4] / d; o1.y = acc[5] / d; o1.z = acc[6] / d; o1.w = acc[7] / d;
-    float* out = a.attn + (int64_t)v * HID + FPL * j;
-    *reinterpret_cast<float4*>(out) = o0;
-    *reinterpret_cast<float4*>(out + 4) = o1;
-  }
+  const float d = z + 1e-6f;
+  float4 o0, o1;
+  o0.x = acc[0] / d; o0.y = acc[1] / d; o0.z = acc[2] / d; o0.w = acc[3] / d;
+  o1.x = acc[4] / d; o1.y = acc[5] / d; o1.z = acc[6] / d; o1.w = acc[7] / d;
+  float* out = a.attn + (int64_t)v * HID + FPL * j;
+  *reinterpret_cast<float4*>(out) = o0;
+  *reinterpret_cast<float4*>(out + 4) = o1;
 }
 
 // ================================================================ node update (bf16), 4-slot weight ring
@@ -1594,7 +1567,7 @@ extern "C" int di_node_aggregate(const di_graph* g, di_dtype dt, const float* al
     return DI_EINVAL;
   AggrArgs a{g->num_nodes, g->src, g->in_ptr, alpha, qkv, attn_out};
   hipStream_t s = (hipStream_t)stream;
-  const dim3 grid((unsigned)((a.Nt + AGG_WAVES - 1) / AGG_WAVES)), block(64 * AGG_WAVES);
+  const dim3 grid((unsigned)((a.Nt + AGG_NODES - 1) / AGG_NODES)), block(16 * AGG_NODES);
   if (dt == DI_BF16) hipLaunchKernelGGL(k_node_aggr<BF16T>, grid, block, 0, s, a);
   else hipLaunchKernelGGL(k_node_aggr<F32T>, grid, block, 0, s, a);
   return launch_status();

@@ -1,11 +1,8 @@
 """Node-layer split (di_node_aggregate + di_node_update) vs the fused di_node_layer, and the CSR
 segment reduction itself vs an fp64 torch reference on ragged in-degrees.
 
-* split vs fused: the two sum a destination's in-edges in different orders (the wave-per-destination
-  reduction in four interleaved slot partials, the fused kernel in edge order), so they agree to
-  fp32 rounding: node outputs <= 1e-5 relative in fp32, <= the stated bf16 bound in bf16 (a last-bit
-  fp32 difference can flip a bf16 rounding downstream); the edge outputs (computed before the first
-  node layer) are bit-identical; on the golden cases and on a full C3 micro-batch;
+* split vs fused: bit-identical (same products, same edge order, same division), fp32 and bf16,
+  on the golden cases and on a full C3 micro-batch (8 x 2x1000 residues, k = 20);
 * di_node_aggregate vs fp64 torch on a ragged CSR (in-degrees 0..40, i.e. empty segments and
   segments spanning several 16-edge chunks): <= 1e-5 relative for fp32 V, and for bf16 V (the
   bf16 values are exact in fp32; only the fp32 accumulation rounds).
@@ -37,35 +34,23 @@ def _both(eng, gb):
     return outs
 
 
-SPLIT_TOL = {"f32": 1e-5, "bf16": 1.5e-2}
-
-
-def _rel(a, b):
-    a, b = a.double(), b.double()
-    return float((a - b).abs().max() / b.abs().max())
-
-
 @pytest.mark.parametrize("dtype", ["f32", "bf16"])
 @pytest.mark.parametrize("case", ["tiny", "c2"])
-def test_split_node_layer_matches_fused(dtype, case):
+def test_split_node_layer_bit_identical(dtype, case):
     from deepinteract_amd.graph import GraphBatch
     z = load_case(case)
     gb = GraphBatch.from_arrays([chain_item(z, "g1"), chain_item(z, "g2")], "cuda")
     (h0, e0), (h1, e1) = _both(_engine(dtype), gb)
-    err = _rel(h1, h0)
-    print(f"{case} {dtype} split vs fused node output: {err:.3e}")
-    assert err < SPLIT_TOL[dtype] and torch.equal(e0, e1)
+    assert torch.equal(h0, h1) and torch.equal(e0, e1)
 
 
-def test_split_node_layer_matches_fused_c3_microbatch():
+def test_split_node_layer_bit_identical_c3_microbatch():
     from deepinteract_amd import synth
     from deepinteract_amd.builder import build_graph_batch
     chains = [c for j in range(8) for c in synth.synthetic_complex(950 + j, 1000, 1000)]
     gb = build_graph_batch(chains, k=20, nbr_seeds=list(range(1, 17)))
     (h0, e0), (h1, e1) = _both(_engine("bf16"), gb)
-    err = _rel(h1, h0)
-    print(f"C3 bf16 split vs fused node output: {err:.3e}")
-    assert torch.isfinite(h1.float()).all() and err < SPLIT_TOL["bf16"] and torch.equal(e0, e1)
+    assert torch.equal(h0, h1) and torch.equal(e0, e1)
 
 
 @pytest.mark.parametrize("dtype", ["f32", "bf16"])

@@ -16,7 +16,7 @@ VARIANTS = {
 }
 # New experiments add their -D knob to csrc (defaulting to the shipped value) and an entry here;
 # round 2's knobs (edge ring / persistent tiles / XCD tile order / DMA pumping / f16 ResBlocks / pair
-# pacing, ...) were measured, recorded in DESIGN.md §8 and removed from the sources.
+# pacing, ...) and round 3's scalar-VALU build were measured, recorded in DESIGN.md §8 and removed from the sources.
 
 if __name__ == "__main__":
     names = sys.argv[1:] or list(VARIANTS)
