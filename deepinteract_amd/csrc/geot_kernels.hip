@@ -694,6 +694,9 @@ __device__ __forceinline__ void pack_pair(Op<BF16T, 4>& o, const Act<8>& a, int 
 }
 
 using LeanPipe = WPipe<u16, Lean::NW, true, EL_CAP, 128>;
+#ifndef DI_LEAN_KEEP_F
+#define DI_LEAN_KEEP_F 0
+#endif
 
 // stage sequencer of one tile: next() publishes stage i and issues the DMA of stage i + 1.
 // GC (DI_GRAPH_GEO_REF batches): the sequence starts at orig_msg_linear (stages 0-1, the neighbour
@@ -950,7 +953,9 @@ void k_edge_lean(EdgeArgs a) {
   }
   lean_res_block(x, st, lane, g);
   lean_res_block(x, st, lane, g);
-  load_f(fr, f_row, g);
+  // DI_LEAN_KEEP_F (experiment): the F rows stay in registers from orig_msg_linear to here instead
+  // of being re-read (240 VGPRs, a 12-B spill in k_edge_lean<0, true>)
+  if constexpr (!DI_LEAN_KEEP_F) load_f(fr, f_row, g);
   w = st.next();  // res_connect_linear: x = F + silu(rc(x))
   lean_f_residual(x, w, st.v(), fr, lane, g);
   lean_res_block(x, st, lane, g);
