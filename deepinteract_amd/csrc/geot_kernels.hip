@@ -278,6 +278,124 @@ void k_init_edge(InitArgs a) {
   }
 }
 
+// ---------------------------------------------------------------- InitEdge with resident weights
+// bf16, DI_GRAPH_GEO_REF batches without layer-0 Fn rows (the benchmark path): the weight blocks
+// this path reads -- the collapsed message map (8), the dist and amide projections + their
+// combined_linear_0 slices (2 x 40), the em / dist / amide gates (3 x 8) and combined_linear_1/2
+// (16) -- are 128 blocks = 128 KiB, so ONE block per CU loads them into LDS once and its waves then
+// stream 16-edge tiles with no weight stages, no stage barriers and no L2 weight traffic (the
+// staged kernel above re-streams 6 stages per 64 edges and meets its block at every stage barrier).
+// Waves are independent after the load: tile t = wave + k * (total waves). The arithmetic is the
+// same as k_init_edge<BF16T, true> (same operands, same order).
+#ifndef DI_INIT_PREFETCH
+#define DI_INIT_PREFETCH 1
+#endif
+#ifndef DI_INIT_RES_NW
+#define DI_INIT_RES_NW 12
+#endif
+constexpr int IR_NW = DI_INIT_RES_NW;  // waves per block (3 per SIMD, one block per CU)
+constexpr int IR_NBLK = 128;  // resident weight blocks
+constexpr int IR_T0 = 0, IR_DIST = 8, IR_AMIDE = 48, IR_GATE = 88, IR_C = 112;
+using InitResGeo = KernelGeo<IR_NW>;
+__global__ __attribute__((amdgpu_flat_work_group_size(1, InitResGeo::THREADS), amdgpu_waves_per_eu(IR_NW / 4, IR_NW / 4)))
+void k_init_edge_res(InitArgs a, int ntiles) {
+  __shared__ __attribute__((aligned(16))) u16 w[IR_NBLK * BLK];
+  const u16* W = reinterpret_cast<const u16*>(a.wmat);
+  dma_blocks<IR_NW>(w + IR_T0 * BLK, W + IE_T0 * BLK, 8);
+  dma_blocks<IR_NW>(w + IR_DIST * BLK, W + (IE_T0 + 40 * 1) * BLK, 40);
+  dma_blocks<IR_NW>(w + IR_AMIDE * BLK, W + (IE_T0 + 40 * 4) * BLK, 40);
+  dma_blocks<IR_NW>(w + IR_GATE * BLK, W + IE_GEO1 * BLK, 16);               // em1, dist1
+  dma_blocks<IR_NW>(w + (IR_GATE + 16) * BLK, W + (IE_GEO1 + 32) * BLK, 8);  // amide1
+  dma_blocks<IR_NW>(w + IR_C * BLK, W + IE_C1 * BLK, 16);                    // combined_linear_1, _2
+  lds_dma_wait();
+  __syncthreads();
+  const int lane = lane_id(), g = lane >> 4;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // positional-row indices one tile ahead: the src/dst -> node_pos chain of tile k+1 is issued during
+  // tile k, so a tile's start waits for one gather latency (its two positional rows), not three
+  const int stride = gridDim.x * IR_NW;
+  auto edge_of = [&](int t) {
+    const int r = t * ROWS_PER_WAVE + (lane & 15);
+    return r < a.Et ? r : a.Et - 1;
+  };
+  int tile = blockIdx.x * IR_NW + wave;
+  int ps = 0, pd = 0;
+  if (tile < ntiles) {
+    const int e = edge_of(tile);
+    ps = a.node_pos[a.src[e]];
+    pd = a.node_pos[a.dst[e]];
+  }
+#pragma unroll 1
+  for (; tile < ntiles; tile += stride) {
+    const int r = tile * ROWS_PER_WAVE + (lane & 15);
+    const bool valid = r < a.Et;
+    const int e = valid ? r : a.Et - 1;
+    Act<2> geo;
+    load_edge_geo(geo, a.edge_f + (int64_t)e * NFEAT_E, g);
+    Op<BF16T, 1> gop;
+    make_op(gop, geo);
+    // combined_linear_0 over [emb[src], emb[dst], em0, silu(d0), 0, orient const, silu(a0)]
+    Act<8> acc;
+    load_row(acc, a.pos_src + (int64_t)ps * HID, g);
+    add_row(acc, a.pos_dst + (int64_t)pd * HID, g);
+    add_vec(acc, a.wvec + IEV_ORC, g);
+    const bool more = DI_INIT_PREFETCH && tile + stride < ntiles;  // uniform
+    int sn = 0, dn = 0;
+    if (more) {
+      const int en = edge_of(tile + stride);
+      sn = a.src[en];
+      dn = a.dst[en];
+    }
+    mma_ring<8, 1>(acc, gop, w + IR_T0 * BLK, lane);
+#pragma unroll 1
+    for (int i = 0; i < 2; ++i) {
+      const u16* wt = w + (i == 0 ? IR_DIST : IR_AMIDE) * BLK;
+      Act<8> y;
+      zero(y);
+      mma_ring<8, 1>(y, gop, wt, lane);
+      silu2_<8, true>(y);
+      Op<BF16T, 4> yop;
+      make_op(yop, y);
+      mma_ring<8, 4>(acc, yop, wt + 8 * BLK, lane);
+    }
+    if (more) {  // the next tile's positional-row indices, from ids loaded a stage ago
+      ps = a.node_pos[sn];
+      pd = a.node_pos[dn];
+    } else if (!DI_INIT_PREFETCH && tile + stride < ntiles) {
+      const int en = edge_of(tile + stride);
+      ps = a.node_pos[a.src[en]];
+      pd = a.node_pos[a.dst[en]];
+    }
+    silu2_<8, true>(acc);
+    // gating: (em1 + silu(d1) + 0 + orient const + silu(a1)) * c
+    {
+      Act<8> gs;
+      init_vec(gs, a.wvec + IEV_OGATE, g);
+#pragma unroll 1
+      for (int t = 0; t < 3; ++t) {
+        Act<8> y;
+        zero(y);
+        mma_ring<8, 1>(y, gop, w + (IR_GATE + 8 * t) * BLK, lane);
+        if (t > 0) silu2_<8, true>(y);
+        add_(gs, y);
+      }
+      mul_(acc, gs);
+    }
+    // combined_linear_2(combined_linear_1(.)) : 128 -> 28 (padded 32) -> 128
+    Act<2> z;
+    zero(z);
+    Op<BF16T, 4> aop;
+    make_op(aop, acc);
+    mma_ring<2, 4>(z, aop, w + IR_C * BLK, lane);
+    Act<8> f;
+    zero(f);
+    Op<BF16T, 1> zop;
+    make_op(zop, z);
+    mma_ring<8, 1>(f, zop, w + (IR_C + 8) * BLK, lane);
+    if (valid) store_edge_row(f, reinterpret_cast<u16*>(a.f_out) + (int64_t)e * HID, g);
+  }
+}
+
 // ================================================================ fused edge layer
 // Weight stage order of the edge layer: block offsets / sizes (csrc/layout.h) and the fp32
 // vector (bias) staged with each layer (-1: none).
@@ -1163,6 +1281,60 @@ __global__ __launch_bounds__(16 * AGG_NODES) void k_node_aggr(AggrArgs a) {
   *reinterpret_cast<float4*>(out + 4) = o1;
 }
 
+// The CSR segment sum of one node held in the MFMA layout (wv[b][q] = feature 16b + 4g + q of node
+// v): wV / (z + 1e-6) with wV = sum alpha * V[src], z = sum alpha over v's in-edges
+// (deepinteract_modules.py:93-96, 116). Shared by the fused node layers (k_node_layer,
+// k_node_update_ring with attn == NULL); k_node_aggr computes the same products in the same order.
+template <class DT>
+__device__ __forceinline__ void node_gather(Act<8>& wv, const NodeArgs& a, int v, int g) {
+  using T = typename DT::T;
+  const T* qkv = reinterpret_cast<const T*>(a.qkv);
+  zero(wv);
+  floatx4 z = {0.f, 0.f, 0.f, 0.f};
+  // In-edges in groups of UNR: the group's source ids, alphas and V[src] rows are all in flight
+  // before the first product (one latency per group instead of two dependent ones per edge); the
+  // products are still added one edge at a time in edge order (the reference's summation order).
+  constexpr int UNR = DT::kBF16 ? 4 : 2;
+  const int e0 = a.in_ptr[v], e1 = a.in_ptr[v + 1];
+  int e = e0;
+#pragma unroll 1
+  for (; e + UNR <= e1; e += UNR) {
+    int sid[UNR];
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) sid[u] = a.src[e + u];
+    floatx4 al[UNR];
+    RawRow<T> vr[UNR];
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      al[u] = ld4(a.alpha + (int64_t)(e + u) * 4);
+      vr[u].load(qkv + (int64_t)sid[u] * 3 * HID + 2 * HID, g);
+    }
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      Act<8> vv;
+      vr[u].to_act(vv);
+#pragma unroll
+      for (int b = 0; b < 8; ++b) wv.v[b] += al[u][b >> 1] * vv.v[b];
+      z += al[u];
+    }
+  }
+#pragma unroll 1
+  for (; e < e1; ++e) {
+    const floatx4 al = ld4(a.alpha + (int64_t)e * 4);
+    Act<8> vv;
+    load_row(vv, qkv + (int64_t)a.src[e] * 3 * HID + 2 * HID, g);
+#pragma unroll
+    for (int b = 0; b < 8; ++b) wv.v[b] += al[b >> 1] * vv.v[b];
+    z += al;
+  }
+#pragma unroll
+  for (int b = 0; b < 8; ++b) {
+    const float d = z[b >> 1] + 1e-6f;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) wv.v[b][q] = wv.v[b][q] / d;
+  }
+}
+
 // ================================================================ node update (bf16), 4-slot weight ring
 // O_node + residual + FFN (+ next layer's Q/K/V, + hT) from the aggregated rows of k_node_aggr.
 // Nt / 64 blocks is one block per CU, so a stage's 32 MFMAs per wave (~0.3 us) are far shorter than
@@ -1328,54 +1500,8 @@ __global__ __launch_bounds__(NodeGeo::THREADS, 2) void k_node_layer(NodeArgs a) 
 
   // send_and_recv(u_mul_e('V_h','score'), sum) and (copy_e('score'), sum); h = wV / (z + 1e-6)
   Act<8> wv;
-  if (a.attn != nullptr) {  // aggregated by k_node_aggr (same products, order and division)
-    load_row(wv, a.attn + (int64_t)v * HID, g);
-  } else {
-  zero(wv);
-  floatx4 z = {0.f, 0.f, 0.f, 0.f};
-  // In-edges in groups of UNR: the group's source ids, alphas and V[src] rows are all in flight
-  // before the first product (one latency per group instead of two dependent ones per edge); the
-  // products are still added one edge at a time in edge order (the reference's summation order).
-  constexpr int UNR = DT::kBF16 ? 4 : 2;
-  const int e0 = a.in_ptr[v], e1 = a.in_ptr[v + 1];
-  int e = e0;
-#pragma unroll 1
-  for (; e + UNR <= e1; e += UNR) {
-    int sid[UNR];
-#pragma unroll
-    for (int u = 0; u < UNR; ++u) sid[u] = a.src[e + u];
-    floatx4 al[UNR];
-    RawRow<T> vr[UNR];
-#pragma unroll
-    for (int u = 0; u < UNR; ++u) {
-      al[u] = ld4(a.alpha + (int64_t)(e + u) * 4);
-      vr[u].load(qkv + (int64_t)sid[u] * 3 * HID + 2 * HID, g);
-    }
-#pragma unroll
-    for (int u = 0; u < UNR; ++u) {
-      Act<8> vv;
-      vr[u].to_act(vv);
-#pragma unroll
-      for (int b = 0; b < 8; ++b) wv.v[b] += al[u][b >> 1] * vv.v[b];
-      z += al[u];
-    }
-  }
-#pragma unroll 1
-  for (; e < e1; ++e) {
-    const floatx4 al = ld4(a.alpha + (int64_t)e * 4);
-    Act<8> vv;
-    load_row(vv, qkv + (int64_t)a.src[e] * 3 * HID + 2 * HID, g);
-#pragma unroll
-    for (int b = 0; b < 8; ++b) wv.v[b] += al[b >> 1] * vv.v[b];
-    z += al;
-  }
-#pragma unroll
-  for (int b = 0; b < 8; ++b) {
-    const float d = z[b >> 1] + 1e-6f;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) wv.v[b][q] = wv.v[b][q] / d;
-  }
-  }
+  if (a.attn != nullptr) load_row(wv, a.attn + (int64_t)v * HID, g);  // k_node_aggr: same products, order, division
+  else node_gather<DT>(wv, a, v, g);
   // n = in1 + O_node(h)
   const T* w = pipe.next();
   settle(hin);  // landed with the O stage (the barrier drained vmcnt); no wait on the F1 DMA later
@@ -1449,6 +1575,14 @@ static inline int launch_status() {
 
 static inline bool dtype_ok(di_dtype dt) { return dt == DI_BF16 || dt == DI_F32; }
 
+// compute units of the current device (persistent grids)
+static int num_cus() {
+  int dev = 0, v = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0)
+    v = 256;
+  return v;
+}
+
 extern "C" int di_abi_version(void) { return DI_ABI_VERSION; }
 
 extern "C" int64_t di_blob_bytes(int kind, di_dtype dtype, int vec) {
@@ -1498,6 +1632,21 @@ extern "C" int di_init_edge(const di_graph* g, di_dtype dt, const float* edge_f,
   else if (dt == DI_BF16) hipLaunchKernelGGL((k_init_edge<BF16T, false>), gb, bb, 0, s, a);
   else if (gc) hipLaunchKernelGGL((k_init_edge<F32T, true>), gf, bf, 0, s, a);
   else hipLaunchKernelGGL((k_init_edge<F32T, false>), gf, bf, 0, s, a);
+  return launch_status();
+}
+
+extern "C" int di_init_edge_resident(const di_graph* g, const float* edge_f, const void* wmat, const float* wvec,
+                                     const float* pos_src_tab, const float* pos_dst_tab, void* f_out, void* stream) {
+  if (!g || !(g->flags & DI_GRAPH_GEO_REF) || !g->src || !g->dst || !g->node_pos || !edge_f || !wmat || !wvec ||
+      !pos_src_tab || !pos_dst_tab || !f_out || g->num_edges <= 0)
+    return DI_EINVAL;
+  InitArgs a{g->num_edges, edge_f, g->src, g->dst, g->node_pos, wmat, wvec, pos_src_tab, pos_dst_tab, f_out, nullptr};
+  // one block per CU holding the path's weights; never more blocks than the tiles need
+  const int ntiles = (a.Et + ROWS_PER_WAVE - 1) / ROWS_PER_WAVE;
+  const int need = (ntiles + IR_NW - 1) / IR_NW;
+  const int cus = num_cus();
+  hipLaunchKernelGGL(k_init_edge_res, dim3((unsigned)(need < cus ? need : cus)), block_of<InitResGeo>(), 0,
+                     (hipStream_t)stream, a, ntiles);
   return launch_status();
 }
 

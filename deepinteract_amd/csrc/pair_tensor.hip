@@ -353,7 +353,11 @@ extern "C" int di_pair_tensor(di_dtype dt, const di_pair_desc* descs, int32_t nu
   // auto: row streaming for any aligned plane. Whole-line stores measured slower (C3, round 3): alone
   // 866 vs 751 us per 4.1 GB (4 waves), 774 vs 757 (8 waves); beside GeoT 7111-7257 vs 7425-7615
   // complexes/s -- each wave's 1-KiB stores stride by the 16-KB row period instead of streaming
-  // contiguous rows, which costs more than the +2.9 % partial-line writes they remove
+  // contiguous rows, which costs more than the +2.9 % partial-line writes they remove. A third form
+  // (round 3: row streaming's 64-row runs written as consecutive whole-line 1-KiB stores, chain-2
+  // chunks from an LDS copy of the hT row, chain-1 values by ds_bpermute) was slower too: alone 770
+  // vs 753 us, beside GeoT 5840-5937 vs 7320-7549 complexes/s (its per-store LDS reads queue behind
+  // the edge kernels' fragment reads); removed
   if (kernel == DI_PAIR_AUTO) kernel = aligned >= 1 ? DI_PAIR_ROWS : 0;
   if (kernel == DI_PAIR_LINES && aligned < 2) return DI_EINVAL;  // whole-line stores need 128-B planes
   if ((kernel == DI_PAIR_ROWS || kernel == DI_PAIR_VECTOR) && aligned < 1) return DI_EINVAL;

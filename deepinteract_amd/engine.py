@@ -177,9 +177,17 @@ class GeoTEngine:
                                          _ptr(p.embed[1]), _ptr(h[0]), _ptr(qkv[0]), st), "di_node_embed")
             ev1 = None
         tick("init_edge")
-        _lib.check(lib.di_init_edge(g, dt, _ptr(gb.edge_f), _ptr(p.init[0]), _ptr(p.init[1]),
-                                    _ptr(p.pos_src), _ptr(p.pos_dst), _ptr(f[0]), _ptr(fn[0]), st),
-                   "di_init_edge")
+        if self.dtype == "bf16" and gb.geo_ref and self.embed_stream is None:
+            # the path's InitEdge weights resident in LDS (one block per CU): faster alone; beside the
+            # side-stream node embedding (an LDS-staged kernel that cannot share its CU) the staged
+            # kernel is used instead
+            _lib.check(lib.di_init_edge_resident(g, _ptr(gb.edge_f), _ptr(p.init[0]), _ptr(p.init[1]),
+                                                 _ptr(p.pos_src), _ptr(p.pos_dst), _ptr(f[0]), st),
+                       "di_init_edge_resident")
+        else:
+            _lib.check(lib.di_init_edge(g, dt, _ptr(gb.edge_f), _ptr(p.init[0]), _ptr(p.init[1]),
+                                        _ptr(p.pos_src), _ptr(p.pos_dst), _ptr(f[0]), _ptr(fn[0]), st),
+                       "di_init_edge")
         if after_init is not None:
             after_init.record(torch.cuda.current_stream())
         if ev1 is not None:

@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define DI_ABI_VERSION 3
+#define DI_ABI_VERSION 4
 
 /* activation / weight storage type of the GeoT kernels (accumulation is always fp32). A plain
  * int32 (not a C enum type): a foreign caller may pass any value, and every entry point refuses
@@ -113,6 +113,14 @@ int di_init_edge(const di_graph* g, di_dtype dt, const float* edge_f /*[Et,28]*/
                  const void* wmat, const float* wvec,
                  const float* pos_src_tab /*[2304,128]*/, const float* pos_dst_tab /*[2304,128]*/,
                  void* f_out /*[Et,128]*/, void* fn_out /*[Et,128]*/, void* stream);
+/* The same InitEdge for bf16 DI_GRAPH_GEO_REF batches without layer-0 Fn rows, with the 128 KiB of
+ * weight blocks that path reads resident in LDS (one block per CU; waves stride over 16-edge tiles):
+ * F bit-identical to di_init_edge. A scheduling choice of this build: faster alone, but its block
+ * holds 128 KiB of a CU's 160 KiB LDS, so LDS-staged kernels of other streams (the node embedding)
+ * cannot run beside it. DI_EINVAL for batches without DI_GRAPH_GEO_REF. */
+int di_init_edge_resident(const di_graph* g, const float* edge_f /*[Et,28]*/, const void* wmat /*bf16 blob*/,
+                          const float* wvec, const float* pos_src_tab, const float* pos_dst_tab,
+                          void* f_out /*[Et,128] bf16*/, void* stream);
 
 int di_edge_layer(const di_graph* g, di_dtype dt, int final_layer, const float* edge_f,
                   const void* f_in, const void* fn_in, const void* qkv,

@@ -25,7 +25,7 @@ def test_library_builds_and_exports_all_declared_symbols():
 
 def test_abi_version_and_blob_sizes():
     lib = _lib.load()
-    assert lib.di_abi_version() == _lib.ABI_VERSION == 3
+    assert lib.di_abi_version() == _lib.ABI_VERSION == 4
     for kind, (nblk, nvec) in packing.BLOB_SIZES.items():
         assert lib.di_blob_bytes(kind, _lib.DI_F32, 0) == nblk * 512 * 4
         assert lib.di_blob_bytes(kind, _lib.DI_BF16, 0) == nblk * 512 * 2
@@ -78,6 +78,8 @@ def test_geo_ref_fn_contract_without_gpu():
     p = ctypes.c_void_p(16)
     g = _lib.DiGraph(8, 16, 16, 16, 16, 16, 16, 0)
     assert lib.di_init_edge(ctypes.byref(g), _lib.DI_BF16, p, p, p, p, p, p, None, None) == -1
+    # the resident InitEdge is the DI_GRAPH_GEO_REF path only
+    assert lib.di_init_edge_resident(ctypes.byref(g), p, p, p, p, p, p, None) == -1
     assert lib.di_edge_layer(ctypes.byref(g), _lib.DI_BF16, 0, p, p, None, p, p, p, p, p, p, None) == -1
     assert lib.di_edge_layer(ctypes.byref(g), _lib.DI_BF16, 0, p, p, p, p, p, p, p, p, None, None) == -1
     assert _lib.DI_GRAPH_GEO_REF == 1

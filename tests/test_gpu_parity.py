@@ -310,3 +310,32 @@ def test_geot_general_path_nonzero_direction_features(engines, sd, dtype):
         errs += [rel_max(h[n0:n1], n_ref.numpy()), rel_max(e[e0:e1], e_ref.numpy())]
     print(f"tiny, random direction/orientation, {dtype}: node/edge errors", ", ".join(f"{x:.3e}" for x in errs))
     assert max(errs) < tol
+
+
+def test_init_edge_resident_matches_staged(engines):
+    """di_init_edge_resident (bf16 DI_GRAPH_GEO_REF batches without layer-0 Fn rows: the path's 128
+    weight blocks resident in LDS, one block per CU, waves striding over 16-edge tiles with the next
+    tile's indices prefetched) vs di_init_edge (staged weights). Same operands in the same order: F
+    bit-identical. The batch (c2 concatenated 8x: 82k edges, 5120 tiles) gives several tiles per
+    wave; a batch without the flag is refused."""
+    import ctypes
+    from deepinteract_amd import _lib
+    from deepinteract_amd.engine import _ptr
+    from deepinteract_amd.graph import concat_batches
+    gb = concat_batches([_batch(load_case("c2"))] * 8)
+    assert gb.geo_ref and gb.num_edges > 256 * 12 * 16
+    eng = engines["bf16"]
+    p, lib = eng.packed, eng.lib
+    f_res = torch.full((gb.num_edges, 128), float("nan"), dtype=torch.bfloat16, device="cuda")
+    f_stg = torch.full_like(f_res, float("nan"))
+    _lib.check(lib.di_init_edge_resident(ctypes.byref(gb.c_graph), _ptr(gb.edge_f), _ptr(p.init[0]), _ptr(p.init[1]),
+                                         _ptr(p.pos_src), _ptr(p.pos_dst), _ptr(f_res), None), "di_init_edge_resident")
+    _lib.check(lib.di_init_edge(ctypes.byref(gb.c_graph), _lib.DI_BF16, _ptr(gb.edge_f), _ptr(p.init[0]),
+                                _ptr(p.init[1]), _ptr(p.pos_src), _ptr(p.pos_dst), _ptr(f_stg), None, None),
+               "di_init_edge")
+    torch.cuda.synchronize()
+    assert not torch.isnan(f_res.float()).any()
+    assert torch.equal(f_res, f_stg)
+    general = gb.with_geo_ref(False)
+    assert lib.di_init_edge_resident(ctypes.byref(general.c_graph), _ptr(gb.edge_f), _ptr(p.init[0]), _ptr(p.init[1]),
+                                     _ptr(p.pos_src), _ptr(p.pos_dst), _ptr(f_res), None) == -1
