@@ -287,13 +287,9 @@ void k_init_edge(InitArgs a) {
 // staged kernel above re-streams 6 stages per 64 edges and meets its block at every stage barrier).
 // Waves are independent after the load: tile t = wave + k * (total waves). The arithmetic is the
 // same as k_init_edge<BF16T, true> (same operands, same order).
-#ifndef DI_INIT_PREFETCH
-#define DI_INIT_PREFETCH 1
-#endif
-#ifndef DI_INIT_RES_NW
-#define DI_INIT_RES_NW 12
-#endif
-constexpr int IR_NW = DI_INIT_RES_NW;  // waves per block (3 per SIMD, one block per CU)
+// 12 waves = 3 per SIMD at 132 VGPRs; 16 waves (<= 128 VGPRs) measured 968 vs 165 us beside the pair
+// stream (the block no longer fits beside the pair kernel's waves)
+constexpr int IR_NW = 12;
 constexpr int IR_NBLK = 128;  // resident weight blocks
 constexpr int IR_T0 = 0, IR_DIST = 8, IR_AMIDE = 48, IR_GATE = 88, IR_C = 112;
 using InitResGeo = KernelGeo<IR_NW>;
@@ -339,7 +335,7 @@ void k_init_edge_res(InitArgs a, int ntiles) {
     load_row(acc, a.pos_src + (int64_t)ps * HID, g);
     add_row(acc, a.pos_dst + (int64_t)pd * HID, g);
     add_vec(acc, a.wvec + IEV_ORC, g);
-    const bool more = DI_INIT_PREFETCH && tile + stride < ntiles;  // uniform
+    const bool more = tile + stride < ntiles;  // uniform
     int sn = 0, dn = 0;
     if (more) {
       const int en = edge_of(tile + stride);
@@ -361,10 +357,6 @@ void k_init_edge_res(InitArgs a, int ntiles) {
     if (more) {  // the next tile's positional-row indices, from ids loaded a stage ago
       ps = a.node_pos[sn];
       pd = a.node_pos[dn];
-    } else if (!DI_INIT_PREFETCH && tile + stride < ntiles) {
-      const int en = edge_of(tile + stride);
-      ps = a.node_pos[a.src[en]];
-      pd = a.node_pos[a.dst[en]];
     }
     silu2_<8, true>(acc);
     // gating: (em1 + silu(d1) + 0 + orient const + silu(a1)) * c
@@ -812,9 +804,6 @@ __device__ __forceinline__ void pack_pair(Op<BF16T, 4>& o, const Act<8>& a, int 
 }
 
 using LeanPipe = WPipe<u16, Lean::NW, true, EL_CAP, 128>;
-#ifndef DI_LEAN_KEEP_F
-#define DI_LEAN_KEEP_F 0
-#endif
 
 // stage sequencer of one tile: next() publishes stage i and issues the DMA of stage i + 1.
 // GC (DI_GRAPH_GEO_REF batches): the sequence starts at orig_msg_linear (stages 0-1, the neighbour
@@ -1071,9 +1060,9 @@ void k_edge_lean(EdgeArgs a) {
   }
   lean_res_block(x, st, lane, g);
   lean_res_block(x, st, lane, g);
-  // DI_LEAN_KEEP_F (experiment): the F rows stay in registers from orig_msg_linear to here instead
-  // of being re-read (240 VGPRs, a 12-B spill in k_edge_lean<0, true>)
-  if constexpr (!DI_LEAN_KEEP_F) load_f(fr, f_row, g);
+  // (round 3: holding the F rows in registers from orig_msg_linear to here instead of re-reading them
+  // -- 240 VGPRs, a 12-B spill -- measured equal: 7448 vs 7320-7456 complexes/s)
+  load_f(fr, f_row, g);
   w = st.next();  // res_connect_linear: x = F + silu(rc(x))
   lean_f_residual(x, w, st.v(), fr, lane, g);
   lean_res_block(x, st, lane, g);

@@ -13,10 +13,6 @@ VARIANTS = {
     # 2-wave blocks; every launch site takes its shape from NodeGeo, and tests/test_gpu_node_aggr.py
     # runs against this build (DI_TEST_VARIANT) to keep the non-default value tested
     "node2": ["DI_NODE_NW=2"],
-    # round 3 experiment: one F re-read per edge fewer in k_edge_lean (rows kept in registers)
-    "keepf": ["DI_LEAN_KEEP_F=1"],
-    # round 3: the resident InitEdge without the one-tile-ahead index prefetch
-    "initnopf": ["DI_INIT_PREFETCH=0"],
 }
 # New experiments add their -D knob to csrc (defaulting to the shipped value) and an entry here;
 # round 2's knobs (edge ring / persistent tiles / XCD tile order / DMA pumping / f16 ResBlocks / pair
