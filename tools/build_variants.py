@@ -13,6 +13,8 @@ VARIANTS = {
     # 2-wave blocks; every launch site takes its shape from NodeGeo, and tests/test_gpu_node_aggr.py
     # runs against this build (DI_TEST_VARIANT) to keep the non-default value tested
     "node2": ["DI_NODE_NW=2"],
+    # round 3: fp32 SiLU as libm expf + IEEE division (the round-2 default)
+    "f32exact": ["DI_F32_FAST_SILU=0"],
 }
 # New experiments add their -D knob to csrc (defaulting to the shipped value) and an entry here;
 # round 2's knobs (edge ring / persistent tiles / XCD tile order / DMA pumping / f16 ResBlocks / pair
