@@ -404,7 +404,6 @@ def sub_record(what, dtype, geo_ref, complexes, pool_gb, P, M, n_res, k, args, d
     eng = GeoTEngine(sd, dtype, cfg, device=dev)
     eng.split_node = args.node_kernel == "split"
     eng.embed_stream = torch.cuda.Stream(dev) if args.embed_stream else None
-    eng.fuse_embed_init = args.init_kernel == "fused"
     mbs = [select_graphs(pool_gb, [2 * ((m * M + j) % P) + s for j in range(M) for s in (0, 1)]).with_geo_ref(geo_ref)
            for m in range(complexes // M)]
     gb0 = mbs[0]
@@ -473,10 +472,6 @@ def main():
                          "Default: fused when overlapped, split otherwise")
     ap.add_argument("--embed-stream", type=int, default=None, choices=[0, 1],
                     help="1: node embedding on a side stream, concurrent with InitEdge (default when overlapped)")
-    ap.add_argument("--init-kernel", default="fused", choices=["fused", "split"],
-                    help="fused: node embedding + InitEdge in one launch, weights resident in LDS (bf16, "
-                         "reference-featurised batches); split: separate launches (the embedding on a side stream "
-                         "when --embed-stream 1)")
     ap.add_argument("--kernel-events", default="all", choices=["all", "dominant"],
                     help="HIP events around every launch in the timed region (all) or only around the "
                          "pair-tensor kernel, the GeoT kernels timed in one untimed step after it")
@@ -534,7 +529,6 @@ def main():
     eng.split_node = args.node_kernel == "split"
     if args.embed_stream:
         eng.embed_stream = torch.cuda.Stream(dev)
-    eng.fuse_embed_init = args.init_kernel == "fused"
     num_cus = torch.cuda.get_device_properties(dev).multi_processor_count
     if args.pair_cus and not args.overlap:
         raise SystemExit("--pair-cus needs --overlap 1 or 2")
@@ -630,9 +624,7 @@ def main():
                    + (f"; DIAGNOSTIC: {args.only} stream only (not the metric)" if args.only else "")
                    + ("" if args.geo_ref else "; DI_GRAPH_GEO_REF cleared (general path)")
                    + f"; node layer {args.node_kernel}"
-                   + ("; node embedding + InitEdge fused (resident weights)" if args.init_kernel == "fused" and
-                      args.dtype == "bf16" and args.geo_ref else
-                      ("; node embedding on a side stream" if args.embed_stream else ""))
+                   + ("; node embedding on a side stream" if args.embed_stream else "")
                    + (f"; {args.slots} workspace slots" if args.overlap else "")
                    + (f"; {args.geot_streams} GeoT streams" if args.geot_streams > 1 else "")
                    + ("" if args.kernel_events == "all" else "; GeoT kernel events from an untimed step")

@@ -293,18 +293,18 @@ constexpr int IR_NW = 12;
 constexpr int IR_NBLK = 128;  // resident weight blocks
 constexpr int IR_T0 = 0, IR_DIST = 8, IR_AMIDE = 48, IR_GATE = 88, IR_C = 112;
 using InitResGeo = KernelGeo<IR_NW>;
-// the path's 128 InitEdge weight blocks -> LDS (issued by every wave; completion awaited by the caller)
-__device__ __forceinline__ void init_res_load(u16* w, const u16* W) {
+__global__ __attribute__((amdgpu_flat_work_group_size(1, InitResGeo::THREADS), amdgpu_waves_per_eu(IR_NW / 4, IR_NW / 4)))
+void k_init_edge_res(InitArgs a, int ntiles) {
+  __shared__ __attribute__((aligned(16))) u16 w[IR_NBLK * BLK];
+  const u16* W = reinterpret_cast<const u16*>(a.wmat);
   dma_blocks<IR_NW>(w + IR_T0 * BLK, W + IE_T0 * BLK, 8);
   dma_blocks<IR_NW>(w + IR_DIST * BLK, W + (IE_T0 + 40 * 1) * BLK, 40);
   dma_blocks<IR_NW>(w + IR_AMIDE * BLK, W + (IE_T0 + 40 * 4) * BLK, 40);
   dma_blocks<IR_NW>(w + IR_GATE * BLK, W + IE_GEO1 * BLK, 16);               // em1, dist1
   dma_blocks<IR_NW>(w + (IR_GATE + 16) * BLK, W + (IE_GEO1 + 32) * BLK, 8);  // amide1
   dma_blocks<IR_NW>(w + IR_C * BLK, W + IE_C1 * BLK, 16);                    // combined_linear_1, _2
-}
-
-// the 16-edge tiles of this wave over the resident weights
-__device__ __forceinline__ void init_res_tiles(const InitArgs& a, const u16* w, int ntiles) {
+  lds_dma_wait();
+  __syncthreads();
   const int lane = lane_id(), g = lane >> 4;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   // positional-row indices one tile ahead: the src/dst -> node_pos chain of tile k+1 is issued during
@@ -386,72 +386,6 @@ __device__ __forceinline__ void init_res_tiles(const InitArgs& a, const u16* w, 
     mma_ring<8, 1>(f, zop, w + (IR_C + 8) * BLK, lane);
     if (valid) store_edge_row(f, reinterpret_cast<u16*>(a.f_out) + (int64_t)e * HID, g);
   }
-}
-
-
-__global__ __attribute__((amdgpu_flat_work_group_size(1, InitResGeo::THREADS), amdgpu_waves_per_eu(IR_NW / 4, IR_NW / 4)))
-void k_init_edge_res(InitArgs a, int ntiles) {
-  __shared__ __attribute__((aligned(16))) u16 w[IR_NBLK * BLK];
-  init_res_load(w, reinterpret_cast<const u16*>(a.wmat));
-  lds_dma_wait();
-  __syncthreads();
-  init_res_tiles(a, w, ntiles);
-}
-
-// Node embedding (+ layer-0 Q/K/V) fused in front of the resident InitEdge: the embedding blob's 128
-// blocks (W_emb, W_q, W_k, W_v) fill the same 128 KiB first, the block's waves embed 16-node tiles
-// (the arithmetic of k_node_embed<BF16T>: same operands, same order), then the InitEdge weights
-// replace them. One kernel instead of the embedding beside InitEdge on a side stream, whose 64-KiB
-// blocks cannot share a CU with the resident InitEdge.
-static_assert(EM_NBLK == IR_NBLK, "the embedding blob fills the resident InitEdge's LDS exactly");
-__global__ __attribute__((amdgpu_flat_work_group_size(1, InitResGeo::THREADS), amdgpu_waves_per_eu(IR_NW / 4, IR_NW / 4)))
-void k_embed_init_res(EmbedArgs ea, InitArgs a, int node_tiles, int ntiles) {
-  __shared__ __attribute__((aligned(16))) u16 w[IR_NBLK * BLK];
-  dma_blocks<IR_NW>(w, reinterpret_cast<const u16*>(ea.wmat), EM_NBLK);
-  lds_dma_wait();
-  __syncthreads();
-  {
-    const int lane = lane_id(), g = lane >> 4;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    u16* qkv = reinterpret_cast<u16*>(ea.qkv_out);
-#pragma unroll 1
-    for (int tile = blockIdx.x * IR_NW + wave; tile < node_tiles; tile += gridDim.x * IR_NW) {
-      const int r = tile * ROWS_PER_WAVE + (lane & 15);
-      const bool valid = r < ea.Nt;
-      const int v = valid ? r : ea.Nt - 1;
-      Act<8> x;  // in_dim input columns, zero padded to 128
-      const float* row = ea.node_f + (int64_t)v * ea.in_dim;
-#pragma unroll
-      for (int b = 0; b < 8; ++b)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int f = 16 * b + 4 * g + q;
-          x.v[b][q] = f < ea.in_dim ? row[f] : 0.f;
-        }
-      Act<8> h;
-      zero(h);
-      {
-        Op<BF16T, 4> xop;
-        make_op(xop, x);
-        mma_ring<8, 4>(h, xop, w + EM_EMB * BLK, lane);
-      }
-      if (valid) store_row(h, reinterpret_cast<u16*>(ea.h_out) + (int64_t)v * HID, g);
-      Op<BF16T, 4> hop;
-      make_op(hop, h);
-#pragma unroll 1
-      for (int q = 0; q < 3; ++q) {
-        Act<8> t;
-        init_vec(t, ea.wvec + EMV_Q + 128 * q, g);
-        mma_ring<8, 4>(t, hop, w + (EM_Q + MAT128 * q) * BLK, lane);
-        if (valid) store_row(t, qkv + (int64_t)v * 3 * HID + q * HID, g);
-      }
-    }
-  }
-  __syncthreads();  // every wave is done with the embedding weights
-  init_res_load(w, reinterpret_cast<const u16*>(a.wmat));
-  lds_dma_wait();
-  __syncthreads();
-  init_res_tiles(a, w, ntiles);
 }
 
 // ================================================================ fused edge layer
@@ -1702,28 +1636,6 @@ extern "C" int di_init_edge_resident(const di_graph* g, const float* edge_f, con
   const int cus = num_cus();
   hipLaunchKernelGGL(k_init_edge_res, dim3((unsigned)(need < cus ? need : cus)), block_of<InitResGeo>(), 0,
                      (hipStream_t)stream, a, ntiles);
-  return launch_status();
-}
-
-extern "C" int di_embed_init_edge_resident(const di_graph* g, int32_t in_dim, const float* node_f,
-                                           const void* embed_wmat, const float* embed_wvec, void* h_out,
-                                           void* qkv_out, const float* edge_f, const void* init_wmat,
-                                           const float* init_wvec, const float* pos_src_tab,
-                                           const float* pos_dst_tab, void* f_out, void* stream) {
-  if (!g || !(g->flags & DI_GRAPH_GEO_REF) || !g->src || !g->dst || !g->node_pos || g->num_nodes <= 0 ||
-      g->num_edges <= 0 || in_dim <= 0 || in_dim > HID || !node_f || !embed_wmat || !embed_wvec || !h_out ||
-      !qkv_out || !edge_f || !init_wmat || !init_wvec || !pos_src_tab || !pos_dst_tab || !f_out)
-    return DI_EINVAL;
-  EmbedArgs ea{g->num_nodes, in_dim, node_f, embed_wmat, embed_wvec, h_out, qkv_out};
-  InitArgs a{g->num_edges, edge_f, g->src, g->dst, g->node_pos, init_wmat, init_wvec, pos_src_tab, pos_dst_tab,
-             f_out, nullptr};
-  const int ntiles = (a.Et + ROWS_PER_WAVE - 1) / ROWS_PER_WAVE;
-  const int node_tiles = (ea.Nt + ROWS_PER_WAVE - 1) / ROWS_PER_WAVE;
-  const int most = ntiles > node_tiles ? ntiles : node_tiles;
-  const int need = (most + IR_NW - 1) / IR_NW;
-  const int cus = num_cus();
-  hipLaunchKernelGGL(k_embed_init_res, dim3((unsigned)(need < cus ? need : cus)), block_of<InitResGeo>(), 0,
-                     (hipStream_t)stream, ea, a, node_tiles, ntiles);
   return launch_status();
 }
 

@@ -88,10 +88,6 @@ class GeoTEngine:
         self.split_node = True
         # optional side stream for the node embedding (concurrent with InitEdge)
         self.embed_stream = None
-        # bf16 reference-featurised batches: node embedding + InitEdge as one launch with their weights
-        # resident in LDS (di_embed_init_edge_resident); False: separate launches (embedding on
-        # embed_stream if set)
-        self.fuse_embed_init = True
 
     def _check_blob_sizes(self):
         p, dt = self.packed, _DI_DT[self.dtype]
@@ -163,16 +159,7 @@ class GeoTEngine:
         if gb.geo_ref:
             fn = [None, None]
         tick = _Ticker(events)
-        fused = self.fuse_embed_init and self.dtype == "bf16" and gb.geo_ref
-        if fused:
-            # node embedding + InitEdge in one launch, each with its weights resident in LDS
-            tick("init_edge")
-            _lib.check(lib.di_embed_init_edge_resident(g, gb.node_f.shape[1], _ptr(gb.node_f), _ptr(p.embed[0]),
-                                                       _ptr(p.embed[1]), _ptr(h[0]), _ptr(qkv[0]), _ptr(gb.edge_f),
-                                                       _ptr(p.init[0]), _ptr(p.init[1]), _ptr(p.pos_src),
-                                                       _ptr(p.pos_dst), _ptr(f[0]), st), "di_embed_init_edge_resident")
-            ev1 = None
-        elif self.embed_stream is not None:
+        if self.embed_stream is not None:
             # node embedding (+ layer-0 Q/K/V) on a side stream, concurrent with InitEdge (which does
             # not read it); the edge layer waits for both
             cur = torch.cuda.current_stream()
@@ -189,10 +176,8 @@ class GeoTEngine:
             _lib.check(lib.di_node_embed(g, dt, gb.node_f.shape[1], _ptr(gb.node_f), _ptr(p.embed[0]),
                                          _ptr(p.embed[1]), _ptr(h[0]), _ptr(qkv[0]), st), "di_node_embed")
             ev1 = None
-        if fused:
-            pass
-        elif self.dtype == "bf16" and gb.geo_ref and self.embed_stream is None:
-            tick("init_edge")
+        tick("init_edge")
+        if self.dtype == "bf16" and gb.geo_ref and self.embed_stream is None:
             # the path's InitEdge weights resident in LDS (one block per CU): faster alone; beside the
             # side-stream node embedding (an LDS-staged kernel that cannot share its CU) the staged
             # kernel is used instead
@@ -200,7 +185,6 @@ class GeoTEngine:
                                                  _ptr(p.pos_src), _ptr(p.pos_dst), _ptr(f[0]), st),
                        "di_init_edge_resident")
         else:
-            tick("init_edge")
             _lib.check(lib.di_init_edge(g, dt, _ptr(gb.edge_f), _ptr(p.init[0]), _ptr(p.init[1]),
                                         _ptr(p.pos_src), _ptr(p.pos_dst), _ptr(f[0]), _ptr(fn[0]), st),
                        "di_init_edge")
