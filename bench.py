@@ -455,7 +455,7 @@ def main():
     ap.add_argument("--pair-kernel", default="auto", choices=["auto", "lines", "rows", "vector"],
                     help="pair-tensor kernel (auto: row streaming for 16-B aligned planes, per-vector otherwise)")
     ap.add_argument("--pair-blocks", type=int, default=0)
-    ap.add_argument("--pair-waves", type=int, default=0, help="waves per pair block (default: 2 beside GeoT, 4 alone)")
+    ap.add_argument("--pair-waves", type=int, default=0, help="waves per pair block (default 4; beside GeoT on CUs/2 blocks)")
     ap.add_argument("--pair-beside", type=int, default=None, choices=[0, 1],
                     help="bounded store queue + non-temporal stores (default: 1 when overlapped)")
     ap.add_argument("--overlap", type=int, default=1, choices=[0, 1, 2],
@@ -507,7 +507,13 @@ def main():
     if args.pair_beside is None:
         args.pair_beside = 1 if args.overlap and not args.pair_cus else 0
     if not args.pair_waves:
-        args.pair_waves = 2 if args.pair_beside else 4  # 4-wave blocks beside GeoT starve InitEdge
+        # beside GeoT: 4-wave blocks on half the CUs (every SIMD of such a CU gets one store wave, the
+        # other CUs none: 7482-7800 vs 7344-7740 complexes/s for 2-wave blocks on every CU, round 3);
+        # 4-wave blocks on every CU starve InitEdge
+        args.pair_waves = 4
+        if args.pair_beside and not args.pair_blocks:
+            args.pair_blocks = max(1, torch.cuda.get_device_properties(0).multi_processor_count // 2) \
+                if torch.cuda.is_available() else 128
     if args.node_kernel is None:
         args.node_kernel = "fused" if args.overlap else "split"
     if args.embed_stream is None:
@@ -620,6 +626,7 @@ def main():
                    + (f"; pair on {args.pair_cus} dedicated CUs ({args.cu_layout}), GeoT on "
                       f"{num_cus - args.pair_cus}" if args.pair_cus else "")
                    + f"; pair kernel {args.pair_kernel} ({args.pair_waves}-wave blocks"
+                   + (f", {args.pair_blocks} resident" if args.pair_blocks else "")
                    + (", bounded store queue, nt stores)" if args.pair_beside else ")")
                    + (f"; DIAGNOSTIC: {args.only} stream only (not the metric)" if args.only else "")
                    + ("" if args.geo_ref else "; DI_GRAPH_GEO_REF cleared (general path)")

@@ -59,9 +59,11 @@ def test_c3_bench_path_bf16_two_slots_two_streams(pair_kernel, side):
     h1r = [gb0.node_off[2 * j] for j in range(M)]
     h2r = [gb0.node_off[2 * j + 1] for j in range(M)]
     l1 = l2 = [N_RES] * M
-    # bench.py's schedule beside GeoT: row-streaming pair stores with a bounded store queue, one 2-wave
-    # block per CU
-    pair = PairTensorOp(kernel=pair_kernel, waves_per_block=2 if side else 0, beside=side)
+    # bench.py's schedule beside GeoT: row-streaming pair stores with a bounded store queue, 4-wave
+    # blocks on half the CUs
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    pair = PairTensorOp(kernel=pair_kernel, blocks=cus // 2 if side else 0, waves_per_block=4 if side else 0,
+                        beside=side)
     s_geot = torch.cuda.current_stream()
     s_pair = torch.cuda.Stream()
     done, keep = [None, None], []
