@@ -335,6 +335,9 @@ class Schedule:
             # kernel_events "dominant": only the pair-tensor kernel is bracketed by HIP events inside
             # the timed region; the GeoT kernels' event pairs are collected in one untimed step after
             self.step(events, events if kernel_events == "all" else None)
+        # host time to issue the timed steps (every launch is asynchronous): close to `elapsed` would
+        # mean the GPU waits for the host
+        self.host_issue_s = time.perf_counter() - t0
         torch.cuda.synchronize()
         barrier(ws)
         elapsed = max_over_ranks(ws, time.perf_counter() - t0)
@@ -636,6 +639,7 @@ def main():
                    + (f"; {args.geot_streams} GeoT streams" if args.geot_streams > 1 else "")
                    + ("" if args.kernel_events == "all" else "; GeoT kernel events from an untimed step")
                    + f"; edge-layer kernel {'k_edge_lean' if args.dtype == 'bf16' else 'k_edge_layer (f32)'}"},
+        "host_issue_ms_per_step": round(sch.host_issue_s / args.steps * 1e3, 3),
         "hbm_frac_of_peak": round(hbm_frac, 4),
         "mfma_frac_of_peak": round(mfma_frac, 4),
         "mfma_frac_of_peak_executed": round(xmfma_frac, 4),
