@@ -407,6 +407,7 @@ def sub_record(what, dtype, geo_ref, complexes, pool_gb, P, M, n_res, k, args, d
     eng = GeoTEngine(sd, dtype, cfg, device=dev)
     eng.split_node = args.node_kernel == "split"
     eng.embed_stream = torch.cuda.Stream(dev) if args.embed_stream else None
+    eng.fuse_embed_init = args.init_kernel == "fused"
     mbs = [select_graphs(pool_gb, [2 * ((m * M + j) % P) + s for j in range(M) for s in (0, 1)]).with_geo_ref(geo_ref)
            for m in range(complexes // M)]
     gb0 = mbs[0]
@@ -475,6 +476,10 @@ def main():
                          "Default: fused when overlapped, split otherwise")
     ap.add_argument("--embed-stream", type=int, default=None, choices=[0, 1],
                     help="1: node embedding on a side stream, concurrent with InitEdge (default when overlapped)")
+    ap.add_argument("--init-kernel", default=None, choices=["fused", "split"],
+                    help="fused: the node embedding as the first blocks of the InitEdge launch (bf16, reference-"
+                         "featurised batches); split: separate launches (the embedding on a side stream when "
+                         "--embed-stream 1). Default: fused when overlapped, split otherwise")
     ap.add_argument("--kernel-events", default="all", choices=["all", "dominant"],
                     help="HIP events around every launch in the timed region (all) or only around the "
                          "pair-tensor kernel, the GeoT kernels timed in one untimed step after it")
@@ -521,6 +526,10 @@ def main():
         args.node_kernel = "fused" if args.overlap else "split"
     if args.embed_stream is None:
         args.embed_stream = 1 if args.overlap else 0
+    if args.init_kernel is None:
+        # overlapped: InitEdge 157-160 vs 171-173 us per micro-batch beside the pair stream, 7516-7621 vs
+        # 7485-7573 complexes/s (round 3); alone the resident InitEdge after the embedding is as fast
+        args.init_kernel = "fused" if args.overlap else "split"
     ws, rank, local = dist_setup()
     dev = torch.device("cuda", local)
     from deepinteract_amd import synth
@@ -538,6 +547,7 @@ def main():
     eng.split_node = args.node_kernel == "split"
     if args.embed_stream:
         eng.embed_stream = torch.cuda.Stream(dev)
+    eng.fuse_embed_init = args.init_kernel == "fused"
     num_cus = torch.cuda.get_device_properties(dev).multi_processor_count
     if args.pair_cus and not args.overlap:
         raise SystemExit("--pair-cus needs --overlap 1 or 2")
@@ -634,7 +644,9 @@ def main():
                    + (f"; DIAGNOSTIC: {args.only} stream only (not the metric)" if args.only else "")
                    + ("" if args.geo_ref else "; DI_GRAPH_GEO_REF cleared (general path)")
                    + f"; node layer {args.node_kernel}"
-                   + ("; node embedding on a side stream" if args.embed_stream else "")
+                   + ("; node embedding as the first blocks of the InitEdge launch"
+                      if args.init_kernel == "fused" and args.dtype == "bf16" and args.geo_ref else
+                      ("; node embedding on a side stream" if args.embed_stream else ""))
                    + (f"; {args.slots} workspace slots" if args.overlap else "")
                    + (f"; {args.geot_streams} GeoT streams" if args.geot_streams > 1 else "")
                    + ("" if args.kernel_events == "all" else "; GeoT kernel events from an untimed step")

@@ -50,6 +50,7 @@ _SIGS = {
     "di_node_embed": ([ctypes.POINTER(DiGraph), _I, _I, _P, _P, _P, _P, _P, _P], ctypes.c_int),
     "di_init_edge": ([ctypes.POINTER(DiGraph), _I, _P, _P, _P, _P, _P, _P, _P, _P], ctypes.c_int),
     "di_init_edge_resident": ([ctypes.POINTER(DiGraph), _P, _P, _P, _P, _P, _P, _P], ctypes.c_int),
+    "di_embed_init_edge": ([ctypes.POINTER(DiGraph), _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P], ctypes.c_int),
     "di_edge_layer": ([ctypes.POINTER(DiGraph), _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
                       ctypes.c_int),
     "di_node_layer": ([ctypes.POINTER(DiGraph), _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P], ctypes.c_int),

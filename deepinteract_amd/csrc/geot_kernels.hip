@@ -185,17 +185,69 @@ struct InitGeo : Geo<DT> {
   static constexpr bool DBUF = false;
   static constexpr int WPE = DT::kBF16 ? 3 : 2;  // blocks (waves per SIMD) per CU
 };
+// The node embedding (+ layer-0 Q/K/V) as the first `embed_blocks` blocks of an InitEdge launch
+// (di_embed_init_edge): same stages and arithmetic as k_node_embed<BF16T> through InitEdge's single
+// 40-block LDS slot, so the two run side by side inside one launch instead of the embedding on a
+// side stream (whose blocks find no LDS beside InitEdge's until its tail).
+template <class DT>
+__device__ __forceinline__ void embed_block(const EmbedArgs& ea, WPipe<typename DT::T, InitGeo<DT>::NW, false, InitGeo<DT>::CAP>& pipe,
+                                            int blk, int lane, int g) {
+  using T = typename DT::T;
+  const int r = blk * InitGeo<DT>::ROWS + (threadIdx.x >> 6) * ROWS_PER_WAVE + (lane & 15);
+  const bool valid = r < ea.Nt;
+  const int v = valid ? r : ea.Nt - 1;
+  const T* W = reinterpret_cast<const T*>(ea.wmat);
+  pipe.issue(W + EM_EMB * BLK, MAT128);
+  Act<8> x;
+  const float* row = ea.node_f + (int64_t)v * ea.in_dim;
+#pragma unroll
+  for (int b = 0; b < 8; ++b)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int f = 16 * b + 4 * g + q;
+      x.v[b][q] = f < ea.in_dim ? row[f] : 0.f;
+    }
+  const T* w = pipe.next();
+  Act<8> h;
+  zero(h);
+  {
+    Op<DT, 4> xop;
+    make_op(xop, x);
+    mma_ring<8, 4>(h, xop, w, lane);
+  }
+  if (valid) store_row(h, reinterpret_cast<T*>(ea.h_out) + (int64_t)v * HID, g);
+  Op<DT, 4> hop;
+  make_op(hop, h);
+  T* qkv = reinterpret_cast<T*>(ea.qkv_out);
+#pragma unroll 1
+  for (int q = 0; q < 3; ++q) {
+    pipe.issue(W + (EM_Q + MAT128 * q) * BLK, MAT128);
+    w = pipe.next();
+    Act<8> t;
+    init_vec(t, ea.wvec + EMV_Q + 128 * q, g);
+    mma_ring<8, 4>(t, hop, w, lane);
+    if (valid) store_row(t, qkv + (int64_t)v * 3 * HID + q * HID, g);
+  }
+}
+
 template <class DT, bool GC>
 __global__ __attribute__((amdgpu_flat_work_group_size(1, InitGeo<DT>::THREADS),
                           amdgpu_waves_per_eu(InitGeo<DT>::WPE, InitGeo<DT>::WPE)))
-void k_init_edge(InitArgs a) {
+void k_init_edge(InitArgs a, EmbedArgs ea, int embed_blocks) {
   using T = typename DT::T;
   using G = InitGeo<DT>;
   constexpr bool FAST = DT::kBF16;
   constexpr int CAP = G::CAP;
   __shared__ __attribute__((aligned(16))) T lds[(G::DBUF ? 2 : 1) * CAP * BLK];
   const int lane = lane_id(), g = lane >> 4;
-  const int r = row_id<G::NW>();
+  if constexpr (DT::kBF16 && GC) {
+    if ((int)blockIdx.x < embed_blocks) {  // uniform per block
+      WPipe<T, G::NW, false, CAP> epipe(lds);
+      embed_block<DT>(ea, epipe, blockIdx.x, lane, g);
+      return;
+    }
+  }
+  const int r = ((int)blockIdx.x - embed_blocks) * G::ROWS + (threadIdx.x >> 6) * ROWS_PER_WAVE + (lane & 15);
   const bool valid = r < a.Et;
   const int e = valid ? r : a.Et - 1;
   const T* W = reinterpret_cast<const T*>(a.wmat);
@@ -1617,10 +1669,30 @@ extern "C" int di_init_edge(const di_graph* g, di_dtype dt, const float* edge_f,
   hipStream_t s = (hipStream_t)stream;
   const dim3 gb = grid_of<InitGeo<BF16T>>(a.Et), bb = block_of<InitGeo<BF16T>>();
   const dim3 gf = grid_of<InitGeo<F32T>>(a.Et), bf = block_of<InitGeo<F32T>>();
-  if (dt == DI_BF16 && gc) hipLaunchKernelGGL((k_init_edge<BF16T, true>), gb, bb, 0, s, a);
-  else if (dt == DI_BF16) hipLaunchKernelGGL((k_init_edge<BF16T, false>), gb, bb, 0, s, a);
-  else if (gc) hipLaunchKernelGGL((k_init_edge<F32T, true>), gf, bf, 0, s, a);
-  else hipLaunchKernelGGL((k_init_edge<F32T, false>), gf, bf, 0, s, a);
+  const EmbedArgs ne{};
+  if (dt == DI_BF16 && gc) hipLaunchKernelGGL((k_init_edge<BF16T, true>), gb, bb, 0, s, a, ne, 0);
+  else if (dt == DI_BF16) hipLaunchKernelGGL((k_init_edge<BF16T, false>), gb, bb, 0, s, a, ne, 0);
+  else if (gc) hipLaunchKernelGGL((k_init_edge<F32T, true>), gf, bf, 0, s, a, ne, 0);
+  else hipLaunchKernelGGL((k_init_edge<F32T, false>), gf, bf, 0, s, a, ne, 0);
+  return launch_status();
+}
+
+extern "C" int di_embed_init_edge(const di_graph* g, int32_t in_dim, const float* node_f, const void* embed_wmat,
+                                  const float* embed_wvec, void* h_out, void* qkv_out, const float* edge_f,
+                                  const void* init_wmat, const float* init_wvec, const float* pos_src_tab,
+                                  const float* pos_dst_tab, void* f_out, void* stream) {
+  if (!g || !(g->flags & DI_GRAPH_GEO_REF) || !g->src || !g->dst || !g->node_pos || g->num_nodes <= 0 ||
+      g->num_edges <= 0 || in_dim <= 0 || in_dim > HID || !node_f || !embed_wmat || !embed_wvec || !h_out ||
+      !qkv_out || !edge_f || !init_wmat || !init_wvec || !pos_src_tab || !pos_dst_tab || !f_out)
+    return DI_EINVAL;
+  EmbedArgs ea{g->num_nodes, in_dim, node_f, embed_wmat, embed_wvec, h_out, qkv_out};
+  InitArgs a{g->num_edges, edge_f, g->src, g->dst, g->node_pos, init_wmat, init_wvec, pos_src_tab, pos_dst_tab,
+             f_out, nullptr};
+  using G = InitGeo<BF16T>;
+  const int eb = (ea.Nt + G::ROWS - 1) / G::ROWS;
+  const int ib = (a.Et + G::ROWS - 1) / G::ROWS;
+  hipLaunchKernelGGL((k_init_edge<BF16T, true>), dim3((unsigned)(eb + ib)), block_of<G>(), 0, (hipStream_t)stream, a,
+                     ea, eb);
   return launch_status();
 }
 

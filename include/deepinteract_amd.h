@@ -121,6 +121,13 @@ int di_init_edge(const di_graph* g, di_dtype dt, const float* edge_f /*[Et,28]*/
 int di_init_edge_resident(const di_graph* g, const float* edge_f /*[Et,28]*/, const void* wmat /*bf16 blob*/,
                           const float* wvec, const float* pos_src_tab, const float* pos_dst_tab,
                           void* f_out /*[Et,128] bf16*/, void* stream);
+/* di_node_embed + di_init_edge (bf16, DI_GRAPH_GEO_REF, no Fn) as ONE launch: the embedding runs as
+ * the launch's first blocks, beside InitEdge's, through the same LDS slot -- instead of on a side
+ * stream. h_out / qkv_out / f_out bit-identical to the two separate calls. 0 < in_dim <= 128. */
+int di_embed_init_edge(const di_graph* g, int32_t in_dim, const float* node_f /*[Nt,in_dim]*/, const void* embed_wmat,
+                       const float* embed_wvec, void* h_out /*[Nt,128]*/, void* qkv_out /*[Nt,384]*/,
+                       const float* edge_f, const void* init_wmat, const float* init_wvec, const float* pos_src_tab,
+                       const float* pos_dst_tab, void* f_out /*[Et,128]*/, void* stream);
 
 int di_edge_layer(const di_graph* g, di_dtype dt, int final_layer, const float* edge_f,
                   const void* f_in, const void* fn_in, const void* qkv,

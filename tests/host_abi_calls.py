@@ -76,6 +76,7 @@ def main(path):
         expect(lib.di_init_edge(gp, 1, p, p, p, p, p, p, None, None), EINVAL, "init Fn")
         expect(lib.di_init_edge(gp, 9, p, p, p, p, p, p, p, None), EINVAL, "init dtype")
         expect(lib.di_init_edge_resident(gp, p, p, p, p, p, None, None), EINVAL, "init resident f_out")
+        expect(lib.di_embed_init_edge(gp, 129, p, p, p, p, p, p, p, p, p, p, p, None), EINVAL, "embed+init in_dim")
         expect(lib.di_edge_layer(gp, 1, 0, p, p, None, p, p, p, p, p, p, None), EINVAL, "edge Fn in")
         expect(lib.di_edge_layer(gp, 1, 0, p, p, p, p, p, p, p, p, None, None), EINVAL, "edge Fn out")
         expect(lib.di_edge_layer(gp, 1, 0, p, p, p, p, p, p, p, None, p, None), EINVAL, "edge f_out")
@@ -87,7 +88,7 @@ def main(path):
         expect(lib.di_conformation(gp, 1, p, p, None, p, p, p, None), EINVAL, "conformation Fn")
         expect(lib.di_geo_attention(gp, 1, None, p, p, p, p, None), EINVAL, "attention NULL")
     # every graph entry point with a NULL graph (remaining arguments plausible)
-    for fn in ("di_node_embed", "di_init_edge", "di_init_edge_resident", "di_edge_layer", "di_node_layer", "di_node_aggregate",
+    for fn in ("di_node_embed", "di_init_edge", "di_init_edge_resident", "di_embed_init_edge", "di_edge_layer", "di_node_layer", "di_node_aggregate",
                "di_node_update", "di_conformation", "di_geo_attention"):
         argtypes = _lib._SIGS[fn][0]
         args = [None] + [1 if t is _lib._I else p for t in argtypes[1:]]

@@ -80,6 +80,7 @@ def test_geo_ref_fn_contract_without_gpu():
     assert lib.di_init_edge(ctypes.byref(g), _lib.DI_BF16, p, p, p, p, p, p, None, None) == -1
     # the resident InitEdge is the DI_GRAPH_GEO_REF path only
     assert lib.di_init_edge_resident(ctypes.byref(g), p, p, p, p, p, p, None) == -1
+    assert lib.di_embed_init_edge(ctypes.byref(g), 113, p, p, p, p, p, p, p, p, p, p, p, None) == -1
     assert lib.di_edge_layer(ctypes.byref(g), _lib.DI_BF16, 0, p, p, None, p, p, p, p, p, p, None) == -1
     assert lib.di_edge_layer(ctypes.byref(g), _lib.DI_BF16, 0, p, p, p, p, p, p, p, p, None, None) == -1
     assert _lib.DI_GRAPH_GEO_REF == 1

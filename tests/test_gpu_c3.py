@@ -37,8 +37,8 @@ def _oracle_graph(gb, g):
 
 @pytest.mark.parametrize("pair_kernel,side", [("auto", True), ("vector", False)])
 def test_c3_bench_path_bf16_two_slots_two_streams(pair_kernel, side):
-    """side: bench.py's overlapped defaults — node embedding on a side stream beside InitEdge and the
-    fused node layer."""
+    """side: bench.py's overlapped defaults — the node embedding as the first blocks of the InitEdge
+    launch (di_embed_init_edge) and the fused node layer."""
     from deepinteract_amd import synth
     from deepinteract_amd.builder import build_graph_batch
     from deepinteract_amd.engine import GeoTEngine, PairTensorOp
@@ -50,6 +50,7 @@ def test_c3_bench_path_bf16_two_slots_two_streams(pair_kernel, side):
     eng = GeoTEngine(sd, "bf16")
     if side:
         eng.embed_stream = torch.cuda.Stream()
+        eng.fuse_embed_init = True  # bench.py's overlapped default: the embedding inside the InitEdge launch
         eng.split_node = False
     n_cx = M * N_MB
     chains = [c for j in range(n_cx) for c in synth.synthetic_complex(700 + j, N_RES, N_RES)]

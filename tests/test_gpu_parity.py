@@ -339,3 +339,36 @@ def test_init_edge_resident_matches_staged(engines):
     general = gb.with_geo_ref(False)
     assert lib.di_init_edge_resident(ctypes.byref(general.c_graph), _ptr(gb.edge_f), _ptr(p.init[0]), _ptr(p.init[1]),
                                      _ptr(p.pos_src), _ptr(p.pos_dst), _ptr(f_res), None) == -1
+
+
+def test_embed_init_edge_one_launch_matches_separate(engines):
+    """di_embed_init_edge (the node embedding as the first blocks of the staged InitEdge launch) vs
+    di_node_embed + di_init_edge: h, qkv and F bit-identical on the 8x-concatenated c2 batch."""
+    import ctypes
+    from deepinteract_amd import _lib
+    from deepinteract_amd.engine import _ptr
+    from deepinteract_amd.graph import concat_batches
+    gb = concat_batches([_batch(load_case("c2"))] * 8)
+    eng = engines["bf16"]
+    p, lib = eng.packed, eng.lib
+    g = ctypes.byref(gb.c_graph)
+    n, e, d = gb.num_nodes, gb.num_edges, gb.node_f.shape[1]
+    outs = []
+    for fused in (True, False):
+        h = torch.full((n, 128), float("nan"), dtype=torch.bfloat16, device="cuda")
+        qkv = torch.full((n, 384), float("nan"), dtype=torch.bfloat16, device="cuda")
+        f = torch.full((e, 128), float("nan"), dtype=torch.bfloat16, device="cuda")
+        if fused:
+            _lib.check(lib.di_embed_init_edge(g, d, _ptr(gb.node_f), _ptr(p.embed[0]), _ptr(p.embed[1]), _ptr(h),
+                                              _ptr(qkv), _ptr(gb.edge_f), _ptr(p.init[0]), _ptr(p.init[1]),
+                                              _ptr(p.pos_src), _ptr(p.pos_dst), _ptr(f), None), "di_embed_init_edge")
+        else:
+            _lib.check(lib.di_node_embed(g, _lib.DI_BF16, d, _ptr(gb.node_f), _ptr(p.embed[0]), _ptr(p.embed[1]),
+                                         _ptr(h), _ptr(qkv), None), "di_node_embed")
+            _lib.check(lib.di_init_edge(g, _lib.DI_BF16, _ptr(gb.edge_f), _ptr(p.init[0]), _ptr(p.init[1]),
+                                        _ptr(p.pos_src), _ptr(p.pos_dst), _ptr(f), None, None), "di_init_edge")
+        outs.append((h, qkv, f))
+    torch.cuda.synchronize()
+    for a, b in zip(*outs):
+        assert not torch.isnan(a.float()).any()
+        assert torch.equal(a, b)
