@@ -49,6 +49,9 @@ EXEC_EDGE_MAC = {True: {"init_edge": 65_536, "edge_layer": 348_160, "edge_layer_
 EXEC_NODE_EMBED_MAC = 128 * 128 + 3 * 128 * 128
 
 
+EDGE_KERNEL = {"bf16": "k_edge_x32 (v_mfma_f32_32x32x16_bf16)", "f32": "k_edge_layer (v_mfma_f32_16x16x4_f32)"}
+
+
 def node_mac(kind):
     q = 3 * H * H
     if kind == "node_embed":
@@ -119,27 +122,34 @@ def kernel_units(kind, nodes, edges, l1l2, esz=2):
     raise KeyError(kind)
 
 
-def dist_setup():
+def dist_setup(force=False):
+    """One process per GPU (torchrun env). The RCCL process group is created for WORLD_SIZE > 1, or
+    at world size 1 with force (--dist: exercises the collective path on one GPU)."""
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if ws > 1:
+    torch.cuda.set_device(local)
+    if ws > 1 or force:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(local)
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29531")
+        dist.init_process_group("nccl", rank=rank, world_size=ws, device_id=torch.device("cuda", local))
     return ws, rank, local
 
 
+def dist_on():
+    import torch.distributed as dist
+    return dist.is_available() and dist.is_initialized()
+
+
 def barrier(ws):
-    if ws > 1:
+    if dist_on():
         import torch.distributed as dist
         dist.barrier()
 
 
 def max_over_ranks(ws, x):
-    if ws == 1:
+    if not dist_on():
         return x
     import torch.distributed as dist
     t = torch.tensor([x], dtype=torch.float64, device="cuda")
@@ -212,35 +222,62 @@ def head_prologue_record(h1r, h2r, l1, l2, gb, eng, dev, tdt, reps=5):
             "bytes_per_launch": byts}
 
 
-def allgather_record(ws, rank, complexes, n_res, k, dev, reps=3):
+def allgather_record(ws, rank, complexes, n_res, k, dev, reps=3, per_rank=4):
     """Supplementary, outside the metric, two parts:
-    1. the C4 driver end to end on REAL maps: distributed.predict_sharded over 2 synthetic
+    1. the C4 driver end to end on REAL maps: distributed.predict_sharded over `per_rank` synthetic
        complexes per rank (device builder -> bf16 GeoT -> pair tensor -> bf16 head -> contact
-       probabilities) and its ONE RCCL all-gather; every rank then checks it holds every map;
-    2. that all-gather at the metric's size (`complexes` fp32 [L1, L2] maps per rank), the send
+       probabilities), micro-batches of one complex, timed three ways: no collective (the compute
+       alone), the maps gathered round by round with asynchronous all-gathers overlapped with the
+       next micro-batch (chunked, the default) and gathered once at the end; the collectives of the
+       chunked plan are then timed alone, giving exposed = t(chunked) - t(compute) and hidden =
+       t(collectives alone) - exposed. Every rank checks it holds every map, chunked == once;
+    2. one all-gather at the metric's size (`complexes` fp32 [L1, L2] maps per rank), the send
        buffer filled with this rank's real maps (tiled), timed over `reps`."""
     import torch.distributed as dist
     from deepinteract_amd import synth
-    from deepinteract_amd.distributed import gpu_forward, predict_sharded
+    from deepinteract_amd.distributed import ChunkedGather, gpu_forward, predict_sharded
     from deepinteract_amd.modules import LitGINI
     from deepinteract_amd.weights import seeded_state_dict
     model = LitGINI(dtype="bf16", head_dtype=torch.bfloat16).to(dev).eval()
     model.load_reference_state_dict(seeded_state_dict(0))
-    cx = [synth.synthetic_complex(50_000 + i, n_res, n_res) for i in range(2 * ws)]
+    cx = [synth.synthetic_complex(50_000 + i, n_res, n_res) for i in range(per_rank * ws)]
+    fwd = gpu_forward(model, k)
+    predict_sharded(cx[:ws], fwd, micro_batch=1, dtype=torch.float32, device=dev, gather="none")  # warm-up
+
+    def run(mode):
+        barrier(ws)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        maps, plan = predict_sharded(cx, fwd, micro_batch=1, dtype=torch.float32, device=dev, gather=mode)
+        torch.cuda.synchronize()
+        return max_over_ranks(ws, time.perf_counter() - t0), maps, plan
+
+    t_none, mine, plan = run("none")
+    t_chunk, maps, _ = run("chunked")
+    t_once, maps_once, _ = run("once")
+    identical = all(torch.equal(a, b) for a, b in zip(maps, maps_once))
+    # the chunked plan's collectives alone, on the maps already computed
+    sizes = [(n_res, n_res)] * len(cx)
+    local = [mine[i] for i in plan[rank]]
+    gathers = ChunkedGather(sizes, plan, 1, torch.float32, dev)
     barrier(ws)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    maps, plan = predict_sharded(cx, gpu_forward(model, k), micro_batch=2, dtype=torch.float32, device=dev)
+    for c in range(len(gathers.rounds)):
+        ids = gathers.rounds[c][0][rank]
+        gathers.put(c, [local[plan[rank].index(i)] for i in ids])
+    gathers.finish()
     torch.cuda.synchronize()
-    t_pred = max_over_ranks(ws, time.perf_counter() - t0)
+    t_coll = max_over_ranks(ws, time.perf_counter() - t0)
     sums = torch.stack([m.double().sum() for m in maps])
     ref = sums.clone()
     dist.broadcast(ref, 0)
     consistent = bool(torch.equal(sums, ref)) and all(0.0 <= float(m.min()) and float(m.max()) <= 1.0 for m in maps)
-    per_rank = complexes * n_res * n_res
-    local = torch.cat([maps[i].reshape(-1) for i in plan[rank]])
-    send = local.repeat((per_rank + local.numel() - 1) // local.numel())[:per_rank].contiguous()
-    recv = torch.empty(per_rank * ws, dtype=torch.float32, device=dev)
+    exposed = max(t_chunk - t_none, 0.0)
+    per_rank_el = complexes * n_res * n_res
+    local_flat = torch.cat([m.reshape(-1) for m in local])
+    send = local_flat.repeat((per_rank_el + local_flat.numel() - 1) // local_flat.numel())[:per_rank_el].contiguous()
+    recv = torch.empty(per_rank_el * ws, dtype=torch.float32, device=dev)
     dist.all_gather_into_tensor(recv, send)
     torch.cuda.synchronize()
     barrier(ws)
@@ -250,10 +287,16 @@ def allgather_record(ws, rank, complexes, n_res, k, dev, reps=3):
     torch.cuda.synchronize()
     dt = max_over_ranks(ws, (time.perf_counter() - t0) / reps)
     del send, recv
-    return {"predict_sharded": {"complexes": len(cx), "s": round(t_pred, 3), "maps_consistent_on_all_ranks": consistent,
-                                "what": "builder + bf16 GeoT + pair tensor + bf16 head + probs, one all-gather"},
-            "bytes_per_rank": per_rank * 4, "ms": round(dt * 1e3, 3),
-            "algbw_GBs": round(per_rank * 4 * (ws - 1) / dt / 1e9, 1),
+    return {"predict_sharded": {"complexes": len(cx), "micro_batch": 1, "rounds": len(gathers.rounds),
+                                "compute_only_s": round(t_none, 4), "chunked_s": round(t_chunk, 4),
+                                "once_s": round(t_once, 4), "collectives_alone_s": round(t_coll, 4),
+                                "exposed_collective_s": round(exposed, 4),
+                                "hidden_collective_s": round(max(t_coll - exposed, 0.0), 4),
+                                "chunked_equals_once": identical, "maps_consistent_on_all_ranks": consistent,
+                                "what": "builder + bf16 GeoT + pair tensor + bf16 head + probs; maps all-gathered "
+                                        "per micro-batch round (async, overlapped) vs once at the end"},
+            "bytes_per_rank": per_rank_el * 4, "ms": round(dt * 1e3, 3),
+            "algbw_GBs": round(per_rank_el * 4 * max(ws - 1, 1) / dt / 1e9, 1),
             "collective": "all_gather_into_tensor (RCCL), real contact maps tiled to the metric's size"}
 
 
@@ -279,6 +322,11 @@ class Schedule:
             raise SystemExit("--geot-streams 2 needs --slots 4 (two GeoT micro-batches + the pair tensor's in flight)")
         self.done = [None] * self.n_slots  # per slot: event after the pair tensor that last read it
         self.pair_only_inputs = {}         # --only pair: each slot's GeoT outputs, computed in the warm-up
+        # the cross-stream events, created once and re-recorded (a wait enqueued before a re-record
+        # waits for the record it saw): no event creation on the issue path
+        self.ev_done = [torch.cuda.Event() for _ in range(self.n_slots)]
+        self.ev_ready = [torch.cuda.Event() for _ in range(self.n_slots)]
+        self.ev_after = [torch.cuda.Event() for _ in range(self.n_slots)]
 
     def _launch_pair(self, h, hT, ready, slot, after=None, events=None):
         with torch.cuda.stream(self.s_pair):
@@ -286,7 +334,7 @@ class Schedule:
             if after is not None:
                 self.s_pair.wait_event(after)
             self.pair(h, self.h1r, self.h2r, self.l1, self.l2, out=self.pair_buf, events=events, hT=hT)
-            ev = torch.cuda.Event()
+            ev = self.ev_done[slot]
             ev.record(self.s_pair)
             self.done[slot] = ev
 
@@ -296,7 +344,7 @@ class Schedule:
         eng, prev = self.eng, None
         for m, gb in enumerate(self.mbs):
             slot = m % self.n_slots
-            after = torch.cuda.Event() if self.overlap == 2 else None
+            after = self.ev_after[slot] if self.overlap == 2 else None
             sg = self.geot_streams[m % len(self.geot_streams)]
             eng.embed_stream = self.embed_streams[m % len(self.geot_streams)]
             with torch.cuda.stream(sg):
@@ -309,7 +357,7 @@ class Schedule:
                     hT = eng.last_hT
                     if self.only == "pair":
                         self.pair_only_inputs[slot] = (h, hT)
-                ready = torch.cuda.Event()
+                ready = self.ev_ready[slot]
                 ready.record(sg)
             if self.only == "geot":
                 continue
@@ -322,9 +370,15 @@ class Schedule:
         if prev is not None:
             self._launch_pair(*prev, events=events)
 
-    def timed(self, steps, warmup, ws=1, kernel_events="all"):
+    def timed(self, steps, warmup, ws=1, kernel_events="dominant"):
         """(elapsed seconds of `steps` steps, bracketed by barrier + synchronize, max over ranks;
-        per-kernel HIP event pairs recorded inside the timed region)."""
+        per-kernel HIP event pairs).
+
+        kernel_events "dominant" (default): inside the timed region only the dominant kernel (the
+        pair tensor, on its own stream) is bracketed by HIP events -- its roofline is measured live;
+        every GeoT kernel's event pairs come from one untimed step of the same schedule after it.
+        "all": every launch in the timed region is bracketed (round 1-3 behaviour: 16 extra event
+        records per micro-batch on the issue path)."""
         for _ in range(warmup):
             self.step()
         events = {}
@@ -332,11 +386,9 @@ class Schedule:
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(steps):
-            # kernel_events "dominant": only the pair-tensor kernel is bracketed by HIP events inside
-            # the timed region; the GeoT kernels' event pairs are collected in one untimed step after
             self.step(events, events if kernel_events == "all" else None)
-        # host time to issue the timed steps (every launch is asynchronous): close to `elapsed` would
-        # mean the GPU waits for the host
+        # host time to issue the timed steps (every launch is asynchronous; includes any wait for
+        # room in the HIP queues, i.e. back-pressure from the GPU)
         self.host_issue_s = time.perf_counter() - t0
         torch.cuda.synchronize()
         barrier(ws)
@@ -344,6 +396,14 @@ class Schedule:
         if kernel_events != "all":
             self.step(None, events)
             torch.cuda.synchronize()
+        # pure host cost of issuing one step, apart from back-pressure: the same step issued onto idle
+        # streams (drained first), timed to the end of its issue; nothing it issues waits for the GPU
+        # unless a queue fills, so with host_issue_idle_s << elapsed / steps the host never delays a launch
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        self.step()
+        self.host_issue_idle_s = time.perf_counter() - t1
+        torch.cuda.synchronize()
         return elapsed, events
 
 
@@ -477,12 +537,13 @@ def main():
     ap.add_argument("--embed-stream", type=int, default=None, choices=[0, 1],
                     help="1: node embedding on a side stream, concurrent with InitEdge (default when overlapped)")
     ap.add_argument("--init-kernel", default=None, choices=["fused", "split"],
-                    help="fused: the node embedding as the first blocks of the InitEdge launch (bf16, reference-"
+                    help="fused: the node embedding as the first blocks of the InitEdge launch (reference-"
                          "featurised batches); split: separate launches (the embedding on a side stream when "
                          "--embed-stream 1). Default: fused when overlapped, split otherwise")
-    ap.add_argument("--kernel-events", default="all", choices=["all", "dominant"],
-                    help="HIP events around every launch in the timed region (all) or only around the "
-                         "pair-tensor kernel, the GeoT kernels timed in one untimed step after it")
+    ap.add_argument("--kernel-events", default="dominant", choices=["all", "dominant"],
+                    help="HIP events only around the dominant (pair-tensor) kernel in the timed region, the "
+                         "GeoT kernels timed in one untimed step after it (dominant, default), or around "
+                         "every launch in the timed region (all)")
     ap.add_argument("--geot-streams", type=int, default=1, choices=[1, 2],
                     help="GeoT streams (2: micro-batches alternate, needs --slots 4)")
     ap.add_argument("--slots", type=int, default=2, choices=[2, 3, 4], help="GeoT workspace slots when overlapped")
@@ -490,6 +551,9 @@ def main():
                     help="diagnostic (not the metric): run only the GeoT stream or only the pair-tensor stream")
     ap.add_argument("--geo-ref", type=int, default=1, choices=[0, 1],
                     help="0: clear DI_GRAPH_GEO_REF on every batch (the general path; diagnostic)")
+    ap.add_argument("--dist", action="store_true",
+                    help="create the RCCL process group even at world size 1 (runs the contact-map "
+                         "all-gather record on one GPU)")
     ap.add_argument("--lib", default=None, help="tuning: a variant build of the HIP library "
                                                  "(deepinteract_amd.build.build_variant)")
     args = ap.parse_args()
@@ -514,14 +578,14 @@ def main():
     args.node_limit = args.node_limit or 2304
     if args.pair_beside is None:
         args.pair_beside = 1 if args.overlap and not args.pair_cus else 0
+    half_cu_pair_grid = False
     if not args.pair_waves:
         # beside GeoT: 4-wave blocks on half the CUs (every SIMD of such a CU gets one store wave, the
         # other CUs none: 7482-7800 vs 7344-7740 complexes/s for 2-wave blocks on every CU, round 3);
         # 4-wave blocks on every CU starve InitEdge
         args.pair_waves = 4
-        if args.pair_beside and not args.pair_blocks:
-            args.pair_blocks = max(1, torch.cuda.get_device_properties(0).multi_processor_count // 2) \
-                if torch.cuda.is_available() else 128
+        # pair_blocks: half this rank's CUs, set after dist_setup from its own device
+        half_cu_pair_grid = True
     if args.node_kernel is None:
         args.node_kernel = "fused" if args.overlap else "split"
     if args.embed_stream is None:
@@ -530,8 +594,11 @@ def main():
         # overlapped: InitEdge 157-160 vs 171-173 us per micro-batch beside the pair stream, 7516-7621 vs
         # 7485-7573 complexes/s (round 3); alone the resident InitEdge after the embedding is as fast
         args.init_kernel = "fused" if args.overlap else "split"
-    ws, rank, local = dist_setup()
+    ws, rank, local = dist_setup(args.dist)
     dev = torch.device("cuda", local)
+    if half_cu_pair_grid and args.pair_beside and not args.pair_blocks:
+        # beside GeoT: 4-wave blocks on half of THIS rank's CUs
+        args.pair_blocks = max(1, torch.cuda.get_device_properties(dev).multi_processor_count // 2)
     from deepinteract_amd import synth
     from deepinteract_amd.builder import build_graph_batch
     from deepinteract_amd.config import GeoTConfig
@@ -606,7 +673,7 @@ def main():
 
     # ---- supplementary (outside the metric) ------------------------------------------------
     prologue = head_prologue_record(h1r, h2r, l1, l2, mbs[-1], eng, dev, tdt) if not args.no_prologue else None
-    gather = allgather_record(ws, rank, args.complexes, n_res, k, dev) if ws > 1 and args.config == "c3" else None
+    gather = allgather_record(ws, rank, args.complexes, n_res, k, dev) if dist_on() and args.config == "c3" else None
     nodes, edges = gb0.num_nodes, gb0.num_edges
     l1l2 = sum(2 * H * a * b * esz for a, b in zip(l1, l2))
     kern = kernel_table(events, nodes, edges, l1l2, esz, args.dtype, gb0.geo_ref)
@@ -645,13 +712,15 @@ def main():
                    + ("" if args.geo_ref else "; DI_GRAPH_GEO_REF cleared (general path)")
                    + f"; node layer {args.node_kernel}"
                    + ("; node embedding as the first blocks of the InitEdge launch"
-                      if args.init_kernel == "fused" and args.dtype == "bf16" and args.geo_ref else
+                      if args.init_kernel == "fused" and args.geo_ref else
                       ("; node embedding on a side stream" if args.embed_stream else ""))
                    + (f"; {args.slots} workspace slots" if args.overlap else "")
                    + (f"; {args.geot_streams} GeoT streams" if args.geot_streams > 1 else "")
-                   + ("" if args.kernel_events == "all" else "; GeoT kernel events from an untimed step")
-                   + f"; edge-layer kernel {'k_edge_lean' if args.dtype == 'bf16' else 'k_edge_layer (f32)'}"},
+                   + ("; HIP events around every launch in the timed region" if args.kernel_events == "all" else
+                      "; HIP events around the pair-tensor launches only (GeoT kernel events from an untimed step)")
+                   + f"; edge-layer kernel {EDGE_KERNEL[args.dtype]}"},
         "host_issue_ms_per_step": round(sch.host_issue_s / args.steps * 1e3, 3),
+        "host_issue_idle_ms_per_step": round(sch.host_issue_idle_s * 1e3, 3),
         "hbm_frac_of_peak": round(hbm_frac, 4),
         "mfma_frac_of_peak": round(mfma_frac, 4),
         "mfma_frac_of_peak_executed": round(xmfma_frac, 4),
@@ -702,7 +771,7 @@ def main():
                                                         "sample": f"5 complexes after 1 warm-up, {dt2:.1f}s"}
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if ws > 1:
+    if dist_on():
         import torch.distributed as dist
         dist.destroy_process_group()
 

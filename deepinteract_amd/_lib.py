@@ -39,7 +39,7 @@ class DiPairLaunch(ctypes.Structure):
 
 
 DI_PAIR_AUTO, DI_PAIR_ROWS, DI_PAIR_VECTOR, DI_PAIR_LINES = 0, 1, 2, 3
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 
 _P = ctypes.c_void_p
@@ -47,10 +47,12 @@ _I = ctypes.c_int32
 _SIGS = {
     "di_abi_version": ([], ctypes.c_int),
     "di_blob_bytes": ([ctypes.c_int, ctypes.c_int, ctypes.c_int], ctypes.c_int64),
+    "di_blob_layout": ([ctypes.c_int, ctypes.c_int], ctypes.c_int),
     "di_node_embed": ([ctypes.POINTER(DiGraph), _I, _I, _P, _P, _P, _P, _P, _P], ctypes.c_int),
     "di_init_edge": ([ctypes.POINTER(DiGraph), _I, _P, _P, _P, _P, _P, _P, _P, _P], ctypes.c_int),
     "di_init_edge_resident": ([ctypes.POINTER(DiGraph), _P, _P, _P, _P, _P, _P, _P], ctypes.c_int),
-    "di_embed_init_edge": ([ctypes.POINTER(DiGraph), _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P], ctypes.c_int),
+    "di_embed_init_edge": ([ctypes.POINTER(DiGraph), _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
+                           ctypes.c_int),
     "di_edge_layer": ([ctypes.POINTER(DiGraph), _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
                       ctypes.c_int),
     "di_node_layer": ([ctypes.POINTER(DiGraph), _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P], ctypes.c_int),

@@ -17,6 +17,7 @@
 #include <type_traits>
 #include "common.h"
 #include "layout.h"
+#include "mfma32.h"
 #include "../../include/deepinteract_amd.h"
 
 namespace di {
@@ -210,10 +211,15 @@ __device__ __forceinline__ void embed_block(const EmbedArgs& ea, WPipe<typename 
   const T* w = pipe.next();
   Act<8> h;
   zero(h);
+  // bf16: the fragment ring; fp32: the 16x16x4 chain of k_node_embed<F32T> (same operands, same order)
+  auto mm = [&](Act<8>& out, const Op<DT, 4>& op, const T* wm) {
+    if constexpr (DT::kBF16) mma_ring<8, 4>(out, op, wm, lane);
+    else mma<8, 4>(out, op, wm, lane);
+  };
   {
     Op<DT, 4> xop;
     make_op(xop, x);
-    mma_ring<8, 4>(h, xop, w, lane);
+    mm(h, xop, w);
   }
   if (valid) store_row(h, reinterpret_cast<T*>(ea.h_out) + (int64_t)v * HID, g);
   Op<DT, 4> hop;
@@ -225,7 +231,7 @@ __device__ __forceinline__ void embed_block(const EmbedArgs& ea, WPipe<typename 
     w = pipe.next();
     Act<8> t;
     init_vec(t, ea.wvec + EMV_Q + 128 * q, g);
-    mma_ring<8, 4>(t, hop, w, lane);
+    mm(t, hop, w);
     if (valid) store_row(t, qkv + (int64_t)v * 3 * HID + q * HID, g);
   }
 }
@@ -240,7 +246,7 @@ void k_init_edge(InitArgs a, EmbedArgs ea, int embed_blocks) {
   constexpr int CAP = G::CAP;
   __shared__ __attribute__((aligned(16))) T lds[(G::DBUF ? 2 : 1) * CAP * BLK];
   const int lane = lane_id(), g = lane >> 4;
-  if constexpr (DT::kBF16 && GC) {
+  if constexpr (GC) {
     if ((int)blockIdx.x < embed_blocks) {  // uniform per block
       WPipe<T, G::NW, false, CAP> epipe(lds);
       embed_block<DT>(ea, epipe, blockIdx.x, lane, g);
@@ -1231,6 +1237,279 @@ void k_edge_lean(EdgeArgs a) {
   }
 }
 
+// ================================================================ fused edge layer on 32x32x16 MFMA (bf16)
+// The stage sequence and arithmetic of k_edge_lean, with each wave's 32 rows as ONE 32x32 tile
+// (csrc/mfma32.h): a 128x128 linear is 32 v_mfma_f32_32x32x16_bf16 per wave instead of 64
+// v_mfma_f32_16x16x32_bf16, which halves the MFMAs' hold on the SIMD's vector issue (8 cycles per
+// instruction either way) -- the issue slots the SiLU epilogues of the edge layers are bound by.
+// Same weight stages (LDS-DMA double-buffered, one 36-block slot per stage), same block geometry
+// (4 waves, 128 edges per block, two blocks per CU at <= 240 VGPRs); the weight blobs are packed in
+// the 32x32 fragment order (packing.pack_matrix32, di_blob_layout() == 32).
+#ifndef DI_EDGE_X32
+#define DI_EDGE_X32 1
+#endif
+struct EdgeX32Geo {
+  static constexpr int NW = 4, THREADS = 64 * NW, ROWS_PER_WAVE = 32, ROWS = ROWS_PER_WAVE * NW;
+};
+
+// x through one ResBlock: two silu2(W . + b) layers packed as the next operand, then x += ln2 * silu2(W . + b)
+template <int NS, bool GC>
+__device__ __forceinline__ void x32_res_block(X32<4>& x, LeanStages<NS, GC>& st, int lane, int h) {
+  P32<8> op;
+  make_op32(op, x);
+#pragma unroll 1
+  for (int l = 0; l < 2; ++l) {
+    const u16* w = st.next();
+    X32<4> t;
+    P32<8> opn;
+    lin32_pipe<8>(t, op, w, st.v(), lane, h, [&](int b) {
+      silu2_blk(t.v[b]);
+      pack_blk(opn.f[2 * b], opn.f[2 * b + 1], t.v[b]);
+    });
+    op = opn;
+    pin(op);
+  }
+  const u16* w = st.next();
+  X32<4> t;
+  lin32_pipe<8>(t, op, w, st.v(), lane, h, [&](int b) {
+    silu2_blk(t.v[b]);
+    x.v[b] += silu2_unit<true>() * t.v[b];
+  });
+  pin(x);
+}
+
+// x = F + ln2 * silu2(W x + b)  (res_connect_linear / final_linear residual; F the edge's bf16 row)
+__device__ __forceinline__ void x32_f_residual(X32<4>& x, const u16* w, const float* v, const R32<4>& fr, int lane,
+                                               int h) {
+  P32<8> op;
+  make_op32(op, x);
+  X32<4> y;
+  lin32_pipe<8>(y, op, w, v, lane, h, [&](int b) {
+    silu2_blk(y.v[b]);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) set_quad(x.v[b], q, unpack4(fr.u[4 * b + q]) + silu2_unit<true>() * quad(y.v[b], q));
+  });
+  pin(x);
+}
+
+template <int MODE, bool GC>
+__global__ __attribute__((amdgpu_flat_work_group_size(1, EdgeX32Geo::THREADS), amdgpu_waves_per_eu(2, 2),
+                          amdgpu_num_vgpr(120)))
+void k_edge_x32(EdgeArgs a) {
+  constexpr bool FINAL = MODE == 1;
+  constexpr int NS = (FINAL ? EL_NSTAGE_FINAL : EL_NSTAGE) - (GC ? (FINAL ? 2 : 3) : 0);
+  __shared__ __attribute__((aligned(16))) char lds[2 * LeanPipe::SLOT_BYTES];
+  const int lane = lane_id(), h = lane >> 5;
+  const int r = blockIdx.x * EdgeX32Geo::ROWS + (threadIdx.x >> 6) * EdgeX32Geo::ROWS_PER_WAVE + (lane & 31);
+  const bool valid = r < a.Et;
+  const int e = valid ? r : a.Et - 1;
+  const u16* f_row = reinterpret_cast<const u16*>(a.f_in) + (int64_t)e * HID;
+  const u16* qkv = reinterpret_cast<const u16*>(a.qkv);
+  LeanPipe pipe(lds);
+  LeanStages<NS, GC> st{pipe, reinterpret_cast<const u16*>(a.wmat), a.wvec, 0};
+  st.issue(0);
+
+  // the edge's geometric features [28] (fp32 row) as a 32-feature operand, features 28..31 = 0
+  P32<2> gop;
+  {
+    const float* grow = a.edge_f + (int64_t)e * NFEAT_E;
+    X32<1> geo;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int f = 8 * q + 4 * h;
+      set_quad(geo.v[0], q, f < NFEAT_E ? ld4(grow + f) : (floatx4){0.f, 0.f, 0.f, 0.f});
+    }
+    make_op32(gop, geo);
+  }
+  X32<4> x;
+  R32<4> fr;
+  const u16* w;
+  if constexpr (GC) {
+    // DI_GRAPH_GEO_REF: the neighbour messages are multiplied by dir_linear_1(dir_linear_0(0)) = 0
+    // (:408), so x = orig_msg_linear(F) + b exactly; no gathered rows, no stages 0-1
+    fr.load(f_row, h);
+    w = st.next();  // orig_msg_linear (+ its bias)
+    init_vec32_lds(x, st.v(), h);
+  } else {
+    // ---- neighbour-edge messages (conformation_module_message_func :384-418)
+    const u16* fn_in = reinterpret_cast<const u16*>(a.fn_in);
+    const int4 nb = *reinterpret_cast<const int4*>(a.nbr + (int64_t)e * 4);
+    R32<4> xn;  // the gathered silu(nbr_linear(F)) row in flight
+    xn.load(fn_in + (int64_t)nb.x * HID, h);
+    w = st.next();  // stage 0: geometric gates (dist [4x2] blocks 0-7, dir / orient / amide [2x2] at 8 / 12 / 16)
+                    // + downward_proj [2x8] at 20
+    X32<2> gate;
+    {
+      X32<2> t1;
+      zero(gate);
+      mma32<2, 2>(gate, gop, w + 8 * BLK, lane);
+      zero(t1);
+      mma32<2, 2>(t1, gop, w + 12 * BLK, lane);
+#pragma unroll
+      for (int b = 0; b < 2; ++b) gate.v[b] *= t1.v[b];
+      zero(t1);
+      mma32<2, 2>(t1, gop, w + 16 * BLK, lane);
+#pragma unroll
+      for (int b = 0; b < 2; ++b) gate.v[b] *= t1.v[b];
+      pin(gate);
+    }
+    X32<2> s;
+    zero(s);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      // x = silu(nbr_linear(F))[nbr_j] * dist gate, packed block by block (the dist gate recomputed
+      // per neighbour: 2 MFMAs per block instead of 64 live registers)
+      P32<8> xop;
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        asm volatile("" ::: "memory");
+        floatx16 dg = {};
+        dg = mfma32(afrag(w, 2 * b, lane), gop.f[0], dg);
+        dg = mfma32(afrag(w, 2 * b + 1, lane), gop.f[1], dg);
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          asm volatile("" : "+v"(xn.u[4 * b + 2 * t]), "+v"(xn.u[4 * b + 2 * t + 1]));
+          const floatx4 lo = unpack4(xn.u[4 * b + 2 * t]) * quad(dg, 2 * t);
+          const floatx4 hi = unpack4(xn.u[4 * b + 2 * t + 1]) * quad(dg, 2 * t + 1);
+          const uint4 u = {pack_bf16x2(lo[0], lo[1]), pack_bf16x2(lo[2], lo[3]), pack_bf16x2(hi[0], hi[1]),
+                           pack_bf16x2(hi[2], hi[3])};
+          xop.f[2 * b + t] = __builtin_bit_cast(bf16x8, u);
+        }
+      }
+      if (j < 3) {  // the next gathered row, in flight under this one's downward_proj
+        const int nx = j == 0 ? nb.y : (j == 1 ? nb.z : nb.w);
+        xn.load(fn_in + (int64_t)nx * HID, h);
+      }
+      X32<2> y;
+      zero(y);
+      mma32<2, 8>(y, xop, w + 20 * BLK, lane);  // downward_proj
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int k = 0; k < 16; ++k) s.v[b][k] += silu2<true>(y.v[b][k]) * gate.v[b][k];
+      pin(s);
+    }
+    w = st.next();  // stage 1: upward_proj [4x4] (+ orig_msg_linear bias)
+    {
+      P32<4> sop;
+      make_op32(sop, s);
+      zero(x);
+      mma32<4, 4>(x, sop, w, lane);
+      X32<4> bo;
+      init_vec32_lds(bo, st.v(), h);
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        silu2_blk(x.v[b]);
+        x.v[b] = silu2_unit<true>() * x.v[b] + bo.v[b];
+      }
+      pin(x);
+    }
+    fr.load(f_row, h);
+    w = st.next();  // stage 2: orig_msg_linear(res) + nbr
+  }
+  {
+    P32<8> fop;
+    raw_op32(fop, fr);
+    mma32<4, 8>(x, fop, w, lane);
+    pin(x);
+  }
+  x32_res_block(x, st, lane, h);
+  x32_res_block(x, st, lane, h);
+  fr.load(f_row, h);
+  w = st.next();  // res_connect_linear: x = F + silu(rc(x))
+  x32_f_residual(x, w, st.v(), fr, lane, h);
+  x32_res_block(x, st, lane, h);
+  x32_res_block(x, st, lane, h);
+  w = st.next();  // final geometric gate [4x2]
+  {
+    X32<4> fg;
+    zero(fg);
+    mma32<4, 2>(fg, gop, w, lane);
+#pragma unroll
+    for (int b = 0; b < 4; ++b) x.v[b] *= fg.v[b];
+    pin(x);
+  }
+  fr.load(f_row, h);
+  w = st.next();  // final_linear: x = F + silu(final(x)) = conformation output
+  x32_f_residual(x, w, st.v(), fr, lane, h);
+
+  // ---- attention scores (propagate_attention :76-91): head hd = features 32 hd .. 32 hd + 31 = block hd
+  R32<4> kr, qr;  // K[src], Q[dst]: issued before the stage barrier
+  kr.load(qkv + (int64_t)a.src[e] * 3 * HID + HID, h);
+  qr.load(qkv + (int64_t)a.dst[e] * 3 * HID, h);
+  w = st.next();  // edge_feats_projection(BN1e(conf))
+  X32<4> p;
+  {
+    P32<8> xop;
+    make_op32(xop, x);
+    init_vec32_lds(p, st.v(), h);
+    mma32<4, 8>(p, xop, w, lane);
+  }
+  floatx4 al;
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    float sum = 0.f;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const floatx4 kq = unpack4(kr.u[4 * b + q]), qd = unpack4(qr.u[4 * b + q]);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float sc = (kq[i] * qd[i]) * (1.0f / 5.656854249492381f);  // / np.sqrt(32)
+        sc = fminf(fmaxf(sc, -5.f), 5.f);
+        const float pv = sc * p.v[b][4 * q + i];  // score = e_out
+        p.v[b][4 * q + i] = pv;
+        sum += pv;
+      }
+    }
+    sum += __shfl_xor(sum, 32);  // the head's other 16 features: the same row in the other lane half
+    al[b] = expf_<true>(fminf(fmaxf(sum, -5.f), 5.f));
+  }
+  if (valid && h == 0) st4(a.alpha_out + (int64_t)e * 4, al);
+  if constexpr (!FINAL) {
+    // ---- edge output: e = in + O_e(e_out); e = e + FFN(BN2e(e)) (:697-724)
+    P32<8> pop;
+    make_op32(pop, p);
+    pin(pop);
+    fr.load(f_row, h);  // O_edge: re-read
+    w = st.next();      // O_edge_feats
+    X32<4> e1;
+    init_vec32_lds(e1, st.v(), h);
+    mma32<4, 8>(e1, pop, w, lane);
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) set_quad(e1.v[b], q, quad(e1.v[b], q) + unpack4(fr.u[4 * b + q]));
+    pin(e1);
+    P32<8> eop;
+    make_op32(eop, e1);
+    pin(eop);
+#pragma unroll 1
+    for (int half = 0; half < 2; ++half) {
+      w = st.next();  // edge_feats_MLP.0 (BN2e folded), hidden half
+      X32<4> t;
+      P32<8> top;
+      lin32_pipe<8>(t, eop, w, st.v(), lane, h, [&](int b) {
+        silu2_blk(t.v[b]);
+        pack_blk(top.f[2 * b], top.f[2 * b + 1], t.v[b]);
+      });
+      pin(top);
+      w = st.next();  // edge_feats_MLP.3, input half: accumulated into the residual
+      mma32<4, 8>(e1, top, w, lane);
+      pin(e1);
+    }
+    if (valid) store_row32(e1, reinterpret_cast<u16*>(a.f_out) + (int64_t)e * HID, h);
+    if constexpr (GC) return;  // the next layer gathers no silu(nbr_linear(F)) rows
+    make_op32(eop, e1);
+    w = st.next();  // next layer's silu(nbr_linear(.))
+    X32<4> fn;
+    init_vec32_lds(fn, st.v(), h);
+    mma32<4, 8>(fn, eop, w, lane);
+#pragma unroll
+    for (int b = 0; b < 4; ++b) silu_blk(fn.v[b]);
+    if (valid) store_row32(fn, reinterpret_cast<u16*>(a.fn_out) + (int64_t)e * HID, h);
+  }
+}
+
 // ================================================================ node aggregation (CSR segment sum)
 // h_attn[v] = sum_{e in in(v)} alpha[e, head] * V[src e]  /  (sum_e alpha[e, head] + 1e-6)
 // (send_and_recv(u_mul_e('V_h','score'), sum) and (copy_e('score'), sum), then wV / (z + 1e-6):
@@ -1643,6 +1922,11 @@ extern "C" int64_t di_blob_bytes(int kind, di_dtype dtype, int vec) {
   return vec ? nvec * 4 : blk * BLK * esz;
 }
 
+extern "C" int di_blob_layout(int kind, di_dtype dtype) {
+  if (!dtype_ok(dtype) || kind < 0 || kind > 6) return -1;
+  return (dtype == DI_BF16 && DI_EDGE_X32 && (kind == 2 || kind == 3)) ? 32 : 16;
+}
+
 extern "C" int di_node_embed(const di_graph* g, di_dtype dt, int32_t in_dim, const float* node_f, const void* wmat,
                              const float* wvec, void* h_out, void* qkv_out, void* stream) {
   if (!g || !node_f || !wmat || !wvec || !h_out || !qkv_out || g->num_nodes <= 0 || in_dim <= 0 || in_dim > HID ||
@@ -1677,22 +1961,27 @@ extern "C" int di_init_edge(const di_graph* g, di_dtype dt, const float* edge_f,
   return launch_status();
 }
 
-extern "C" int di_embed_init_edge(const di_graph* g, int32_t in_dim, const float* node_f, const void* embed_wmat,
-                                  const float* embed_wvec, void* h_out, void* qkv_out, const float* edge_f,
-                                  const void* init_wmat, const float* init_wvec, const float* pos_src_tab,
-                                  const float* pos_dst_tab, void* f_out, void* stream) {
+template <class DT>
+static void launch_embed_init(const InitArgs& a, const EmbedArgs& ea, hipStream_t s) {
+  using G = InitGeo<DT>;
+  const int eb = (ea.Nt + G::ROWS - 1) / G::ROWS;
+  const int ib = (a.Et + G::ROWS - 1) / G::ROWS;
+  hipLaunchKernelGGL((k_init_edge<DT, true>), dim3((unsigned)(eb + ib)), block_of<G>(), 0, s, a, ea, eb);
+}
+
+extern "C" int di_embed_init_edge(const di_graph* g, di_dtype dt, int32_t in_dim, const float* node_f,
+                                  const void* embed_wmat, const float* embed_wvec, void* h_out, void* qkv_out,
+                                  const float* edge_f, const void* init_wmat, const float* init_wvec,
+                                  const float* pos_src_tab, const float* pos_dst_tab, void* f_out, void* stream) {
   if (!g || !(g->flags & DI_GRAPH_GEO_REF) || !g->src || !g->dst || !g->node_pos || g->num_nodes <= 0 ||
       g->num_edges <= 0 || in_dim <= 0 || in_dim > HID || !node_f || !embed_wmat || !embed_wvec || !h_out ||
-      !qkv_out || !edge_f || !init_wmat || !init_wvec || !pos_src_tab || !pos_dst_tab || !f_out)
+      !qkv_out || !edge_f || !init_wmat || !init_wvec || !pos_src_tab || !pos_dst_tab || !f_out || !dtype_ok(dt))
     return DI_EINVAL;
   EmbedArgs ea{g->num_nodes, in_dim, node_f, embed_wmat, embed_wvec, h_out, qkv_out};
   InitArgs a{g->num_edges, edge_f, g->src, g->dst, g->node_pos, init_wmat, init_wvec, pos_src_tab, pos_dst_tab,
              f_out, nullptr};
-  using G = InitGeo<BF16T>;
-  const int eb = (ea.Nt + G::ROWS - 1) / G::ROWS;
-  const int ib = (a.Et + G::ROWS - 1) / G::ROWS;
-  hipLaunchKernelGGL((k_init_edge<BF16T, true>), dim3((unsigned)(eb + ib)), block_of<G>(), 0, (hipStream_t)stream, a,
-                     ea, eb);
+  if (dt == DI_BF16) launch_embed_init<BF16T>(a, ea, (hipStream_t)stream);
+  else launch_embed_init<F32T>(a, ea, (hipStream_t)stream);
   return launch_status();
 }
 
@@ -1725,7 +2014,14 @@ extern "C" int di_edge_layer(const di_graph* g, di_dtype dt, int final_layer, co
   EdgeArgs a{g->num_edges, edge_f, g->src, g->dst, g->nbr, f_in, fn_in, qkv, wmat, wvec, alpha_out,
              f_out, fn_out};
   hipStream_t s = (hipStream_t)stream;
-  if (dt == DI_BF16) {
+  if (dt == DI_BF16 && DI_EDGE_X32) {
+    // 32x32x16 form: 128 edges (one 32-row tile per wave) per 4-wave block; 32x32-packed blob
+    const dim3 grid((unsigned)((a.Et + EdgeX32Geo::ROWS - 1) / EdgeX32Geo::ROWS)), block(EdgeX32Geo::THREADS);
+    if (final_layer && gc) hipLaunchKernelGGL((k_edge_x32<1, true>), grid, block, 0, s, a);
+    else if (final_layer) hipLaunchKernelGGL((k_edge_x32<1, false>), grid, block, 0, s, a);
+    else if (gc) hipLaunchKernelGGL((k_edge_x32<0, true>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((k_edge_x32<0, false>), grid, block, 0, s, a);
+  } else if (dt == DI_BF16) {
     // grouped form: 128 edges (two 16-row groups per wave) per 4-wave block
     const dim3 grid((unsigned)((a.Et + Lean::ROWS_ALL - 1) / Lean::ROWS_ALL)), block = block_of<Lean>();
     if (final_layer && gc) hipLaunchKernelGGL((k_edge_lean<1, true>), grid, block, 0, s, a);

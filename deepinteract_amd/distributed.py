@@ -17,7 +17,11 @@ lit_model_predict.py:236-239 does).
   arguments every rank passes identically, so a rank that owns no complex still sends a
   buffer of the agreed type.
 * ``predict_sharded`` — the C4 driver: shard -> micro-batched forward (graph build, GeoT,
-  pair tensor / head prologue, head, contact probabilities) -> all_gather_maps.
+  pair tensor / head prologue, head, contact probabilities) -> the maps on every rank, gathered
+  either chunked (default, SURVEY.md §8e: round c gathers every rank's c-th micro-batch of maps
+  with an asynchronous ``all_gather_into_tensor`` issued as soon as they exist, so the collective
+  of round c runs on the process group's stream while round c+1 computes) or ONCE after the last
+  micro-batch (``all_gather_maps``). Both return bit-identical maps.
 """
 from __future__ import annotations
 
@@ -106,29 +110,107 @@ def gpu_forward(model, k: int = 20, seed: int = 0):
     return fn
 
 
+def gather_rounds(sizes: Sequence[tuple], plan, micro_batch: int):
+    """The chunked all-gather's schedule, computed by every rank from the sizes alone: round c holds
+    micro-batch c of every rank (its size-sorted local order cut into micro_batch-sized pieces; a
+    rank with fewer micro-batches contributes nothing to the later rounds). Returns per round
+    (per-rank complex lists, the round's per-rank buffer width in elements)."""
+    mbs = []
+    for p in plan:
+        order = local_order(sizes, p)
+        mbs.append([order[s:s + micro_batch] for s in range(0, len(order), micro_batch)])
+    rounds = []
+    for c in range(max((len(m) for m in mbs), default=0)):
+        members = [m[c] if c < len(m) else [] for m in mbs]
+        width = max(max(sum(sizes[i][0] * sizes[i][1] for i in ids) for ids in members), 1)
+        rounds.append((members, width))
+    return rounds
+
+
+class ChunkedGather:
+    """Round-by-round asynchronous all-gather of contact maps (chunked and overlapped
+    with compute). ``put(c, maps)`` packs this rank's maps of round c into the round's send buffer
+    and issues ``all_gather_into_tensor(..., async_op=True)`` -- on RCCL it runs on the process
+    group's own stream after the work already queued on the current stream, so the next
+    micro-batch's kernels, issued right after, overlap it; ``finish()`` waits for every round and
+    returns the maps of all complexes in global order (views of the rounds' receive buffers)."""
+
+    def __init__(self, sizes, plan, micro_batch, dtype, device, group=None):
+        self.sizes, self.dtype, self.device, self.group = sizes, dtype, device, group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.rounds = gather_rounds(sizes, plan, micro_batch)
+        self.pending = []
+
+    def put(self, c, maps):
+        members, width = self.rounds[c]
+        mine = members[self.rank]
+        if len(maps) != len(mine):
+            raise ValueError(f"rank {self.rank}: {len(maps)} maps for round {c}'s {len(mine)} complexes")
+        send = torch.zeros(width, dtype=self.dtype, device=self.device)
+        if maps:
+            flat = torch.cat([m.reshape(-1).to(device=self.device, dtype=self.dtype) for m in maps])
+            send[:flat.numel()] = flat
+        recv = torch.empty(self.world * width, dtype=self.dtype, device=self.device)
+        work = dist.all_gather_into_tensor(recv, send, group=self.group, async_op=True)
+        self.pending.append((c, recv, send, work))
+
+    def finish(self):
+        # rounds in which this rank has no micro-batch still take part (every rank issues every round)
+        done = {c for c, *_ in self.pending}
+        for c in range(len(self.rounds)):
+            if c not in done:
+                self.put(c, [])
+        out = [None] * len(self.sizes)
+        for c, recv, _send, work in sorted(self.pending, key=lambda t: t[0]):
+            work.wait()
+            members, width = self.rounds[c]
+            for r, ids in enumerate(members):
+                off = r * width
+                for i in ids:
+                    l1, l2 = self.sizes[i]
+                    out[i] = recv[off:off + l1 * l2].view(l1, l2)
+                    off += l1 * l2
+        self.pending = []
+        return out
+
+
 def predict_sharded(complexes: Sequence, forward: Callable, micro_batch: int = 8, dtype=torch.float32,
-                    device=None, group=None):
+                    device=None, group=None, gather: str = "chunked"):
     """C4 driver: every rank runs ``forward`` over its contiguous shard of
-    ``complexes`` in size-sorted micro-batches, then ONE all-gather collects every complex's
-    contact map on every rank.
+    ``complexes`` in size-sorted micro-batches; every complex's contact map ends on every rank.
 
     complexes: per complex a (chain1, chain2) pair of builder inputs (dicts with backbone
     [N,4,3], amide_norm [N,3], dips [N,106]); forward(batch, ids) -> list of [L1, L2] maps for
-    the complexes ``batch`` (global indices ``ids``). Returns the maps of all complexes in
-    global order (views of one gathered buffer) and this rank's plan."""
+    the complexes ``batch`` (global indices ``ids``).
+    gather: "chunked" (default) -- one asynchronous all-gather per micro-batch round, overlapped
+    with the next round's compute (ChunkedGather); "once" -- ONE all-gather after the last
+    micro-batch (all_gather_maps); "none" -- no collective, this rank's maps only (timing the
+    compute alone). Returns the maps (global order; None for other ranks' complexes with "none")
+    and the plan."""
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     sizes = [(int(len(c[0]["backbone"])), int(len(c[1]["backbone"]))) for c in complexes]
     plan = shard(sizes, world)
-    mine = local_order(sizes, plan[rank])
-    maps = {}
-    for s in range(0, len(mine), micro_batch):
-        ids = mine[s:s + micro_batch]
-        for i, m in zip(ids, forward([complexes[i] for i in ids], ids)):
-            if tuple(m.shape) != sizes[i]:
-                raise ValueError(f"complex {i}: map {tuple(m.shape)} != {sizes[i]}")
-            maps[i] = m
     if device is None:
         device = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" \
             else torch.device("cpu")
+    if gather not in ("chunked", "once", "none"):
+        raise ValueError(f"gather {gather!r}: one of chunked, once, none")
+    chunks = ChunkedGather(sizes, plan, micro_batch, dtype, device, group) if gather == "chunked" else None
+    mine = local_order(sizes, plan[rank])
+    maps = {}
+    for c, s in enumerate(range(0, len(mine), micro_batch)):
+        ids = mine[s:s + micro_batch]
+        got = list(forward([complexes[i] for i in ids], ids))
+        for i, m in zip(ids, got):
+            if tuple(m.shape) != sizes[i]:
+                raise ValueError(f"complex {i}: map {tuple(m.shape)} != {sizes[i]}")
+            maps[i] = m
+        if chunks is not None:
+            chunks.put(c, got)
+    if gather == "chunked":
+        return chunks.finish(), plan
+    if gather == "none":
+        return [maps.get(i) for i in range(len(sizes))], plan
     return all_gather_maps([maps[i] for i in plan[rank]], plan, sizes, dtype, device, group), plan

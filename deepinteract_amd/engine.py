@@ -79,17 +79,22 @@ class GeoTEngine:
         self.device = gpu_device(device)
         self.lib = _lib.load()
         self.dtype, self.cfg = dtype, cfg
-        self.packed = PackedGeoT(state_dict, dtype, cfg, self.device)
+        # fragment order of the edge-layer blobs this library build reads (ABI 5)
+        layout = self.lib.di_blob_layout(2, _DI_DT[dtype])
+        if layout not in (16, 32) or layout != self.lib.di_blob_layout(3, _DI_DT[dtype]):
+            raise RuntimeError(f"unexpected edge-blob layout {layout}")
+        self.packed = PackedGeoT(state_dict, dtype, cfg, self.device, edge_layout=layout)
         self._check_blob_sizes()
         self._ws = {}
+        self._ws_views = {}
         # node layer as two launches (di_node_aggregate + di_node_update; equal to the fused
         # di_node_layer up to fp32 summation order): the segment reduction one wave per
         # destination at full occupancy instead of inside the MFMA kernel's one-block-per-CU grid
         self.split_node = True
         # optional side stream for the node embedding (concurrent with InitEdge)
         self.embed_stream = None
-        # bf16 reference-featurised batches: node embedding as the first blocks of the InitEdge launch
-        # (di_embed_init_edge) instead of a separate launch
+        # reference-featurised batches: node embedding as the first blocks of the InitEdge launch
+        # (di_embed_init_edge, bf16 or fp32) instead of a separate launch
         self.fuse_embed_init = False
 
     def _check_blob_sizes(self):
@@ -114,8 +119,13 @@ class GeoTEngine:
         memory. Before a slot's buffers are replaced the device is drained, because a consumer
         on another stream may still be reading them and the caching allocator would otherwise
         hand that memory to the next launch."""
+        key = (slot, num_nodes, num_edges)
+        views = self._ws_views.get(key)
+        if views is not None:
+            return views
         cap = self._ws.get(slot)
         if cap is None or cap[0][0] < num_nodes or cap[0][1] < num_edges:
+            self._ws_views = {}
             if cap is not None:
                 torch.cuda.synchronize(self.device)
             cn = max(num_nodes, cap[0][0] if cap else 0)
@@ -131,12 +141,14 @@ class GeoTEngine:
                 "hT": torch.empty(H * cn, dtype=dt, device=dev),
             })
         b, H = cap[1], self.cfg.num_gnn_hidden_channels
-        return {
+        # views of the slot's buffers, cached per batch shape (the issue path builds no tensors)
+        views = self._ws_views[key] = {
             "h": [t[:num_nodes] for t in b["h"]], "qkv": [t[:num_nodes] for t in b["qkv"]],
             "f": [t[:num_edges] for t in b["f"]], "fn": [t[:num_edges] for t in b["fn"]],
             "alpha": b["alpha"][:num_edges], "attn": b["attn"][:num_nodes],
             "hT": b["hT"][:H * num_nodes].view(H, num_nodes),
         }
+        return views
 
     def forward(self, gb: GraphBatch, clone: bool = True, events=None, slot: int = 0, after_init=None):
         """-> (node feats [Nt,128], edge feats [Et,128]) in the engine dtype.
@@ -162,10 +174,10 @@ class GeoTEngine:
         if gb.geo_ref:
             fn = [None, None]
         tick = _Ticker(events)
-        fused = self.fuse_embed_init and self.dtype == "bf16" and gb.geo_ref
+        fused = self.fuse_embed_init and gb.geo_ref
         if fused:
             tick("init_edge")
-            _lib.check(lib.di_embed_init_edge(g, gb.node_f.shape[1], _ptr(gb.node_f), _ptr(p.embed[0]), _ptr(p.embed[1]),
+            _lib.check(lib.di_embed_init_edge(g, dt, gb.node_f.shape[1], _ptr(gb.node_f), _ptr(p.embed[0]), _ptr(p.embed[1]),
                                               _ptr(h[0]), _ptr(qkv[0]), _ptr(gb.edge_f), _ptr(p.init[0]),
                                               _ptr(p.init[1]), _ptr(p.pos_src), _ptr(p.pos_dst), _ptr(f[0]), st),
                        "di_embed_init_edge")

@@ -76,6 +76,33 @@ def pack_matrix(w, dtype: str) -> np.ndarray:
     return blocks.reshape(-1)
 
 
+def _pack_index32():
+    """(row, col) index arrays of one v_mfma_f32_32x32x16_bf16 A-fragment block (32 output rows x
+    16 input features), in storage order: lane l (r = l & 31, h = l >> 5), element j holds
+    W[32 ob + r][16 s + 8 (j >> 2) + 4 h + (j & 3)] -- the k order in which a 32x32 accumulator,
+    converted pairwise to bf16, is the next MFMA's B operand (csrc/mfma32.h)."""
+    lane = np.arange(64)
+    j = np.arange(8)
+    row = np.broadcast_to((lane & 31)[:, None], (64, 8))
+    col = 8 * (j[None, :] >> 2) + 4 * (lane[:, None] >> 5) + (j[None, :] & 3)
+    return row.reshape(-1), col.reshape(-1)
+
+
+def pack_matrix32(w) -> np.ndarray:
+    """W [Nout, Kin] -> (Nout/32)*(Kin/16) blocks of 512 elements, block order (ob, s): the bf16
+    edge-layer blobs (di_blob_layout() == 32). Same block count as pack_matrix."""
+    w = np.asarray(w, dtype=np.float64)
+    nout, kin = w.shape
+    assert nout % 32 == 0 and kin % 16 == 0, (nout, kin)
+    r, c = _pack_index32()
+    nbo, ns = nout // 32, kin // 16
+    blocks = np.empty((nbo, ns, BLK), dtype=np.float64)
+    for bo in range(nbo):
+        for s in range(ns):
+            blocks[bo, s] = w[32 * bo + r, 16 * s + c]
+    return blocks.reshape(-1)
+
+
 def _pack_index_natural(dtype: str):
     """Natural-k fragment order of di_gemm_bias_act (the B operand is read straight from x)."""
     lane = np.arange(64)
@@ -131,14 +158,15 @@ def fold_bn_after(w, b, s, t):
 
 
 class BlobBuilder:
-    def __init__(self, dtype: str, nblk: int, nvec: int):
-        self.dtype, self.nblk, self.nvec = dtype, nblk, nvec
+    def __init__(self, dtype: str, nblk: int, nvec: int, layout: int = 16):
+        assert layout in (16, 32) and (layout == 16 or dtype == "bf16"), (dtype, layout)
+        self.dtype, self.nblk, self.nvec, self.layout = dtype, nblk, nvec, layout
         self.mat = np.zeros(nblk * BLK, dtype=np.float64)
         self.vec = np.zeros(nvec, dtype=np.float64)
         self.used = np.zeros(nblk, dtype=bool)
 
     def put(self, blk_off: int, w):
-        p = pack_matrix(w, self.dtype)
+        p = pack_matrix32(w) if self.layout == 32 else pack_matrix(w, self.dtype)
         n = p.size // BLK
         assert blk_off + n <= self.nblk, (blk_off, n, self.nblk)
         assert not self.used[blk_off:blk_off + n].any(), blk_off
@@ -232,14 +260,15 @@ def init_blob(sd, dtype, p="gnn_module.0.init_edge_module",
     return mat, vec, pos_src, pos_dst
 
 
-def edge_blob(sd, li, final, dtype, cfg: GeoTConfig, conf_only=False, c=None):
-    """final: kind 3, else kind 2; conf_only: kind 6 (ConformationModule alone, key prefix c)."""
+def edge_blob(sd, li, final, dtype, cfg: GeoTConfig, conf_only=False, c=None, layout=16):
+    """final: kind 3, else kind 2; conf_only: kind 6 (ConformationModule alone, key prefix c).
+    layout: the fragment order of the matrices (16, or 32 for the bf16 32x32x16 edge kernel)."""
     p = f"gnn_module.0.gt_block.{li}"
     c = c or f"{p}.conformation_module"
     if conf_only:
-        bb = BlobBuilder(dtype, EL_NBLK_CONF, ELV_N_CONF)
+        bb = BlobBuilder(dtype, EL_NBLK_CONF, ELV_N_CONF, layout)
     else:
-        bb = BlobBuilder(dtype, EL_NBLK_FINAL if final else EL_NBLK, ELV_N_FINAL if final else ELV_N)
+        bb = BlobBuilder(dtype, EL_NBLK_FINAL if final else EL_NBLK, ELV_N_FINAL if final else ELV_N, layout)
     sc = _l2e(dtype)  # log2-unit SiLU: downward_proj, ResBlock layers 0-1, edge FFN (silu2)
     two = lambda a, b: _np(sd[f"{c}.{a}.weight"]) @ _np(sd[f"{c}.{b}.weight"])  # noqa: E731
     mg = np.zeros((320, 32))
@@ -323,12 +352,20 @@ def node_blob(sd, li, final, dtype):
     return bb.finish()
 
 
+# fragment order of the edge-layer blobs the shipped library expects (di_blob_layout(2 / 3, dtype))
+EDGE_LAYOUT_DEFAULT = {"bf16": 32, "f32": 16}
+
+
 class PackedGeoT:
     """All device-ready weight blobs of one DGLGeometricTransformer (+ node_in_embedding)."""
 
-    def __init__(self, sd, dtype: str = "f32", cfg: GeoTConfig = GeoTConfig(), device="cpu"):
+    def __init__(self, sd, dtype: str = "f32", cfg: GeoTConfig = GeoTConfig(), device="cpu", edge_layout=None):
+        """edge_layout: fragment order of the edge-layer blobs (the library's di_blob_layout(2, dt));
+        None: this build's default (32 for bf16, 16 for fp32)."""
         assert dtype in ("f32", "bf16")
-        self.dtype, self.cfg = dtype, cfg
+        if edge_layout is None:
+            edge_layout = EDGE_LAYOUT_DEFAULT[dtype]
+        self.dtype, self.cfg, self.edge_layout = dtype, cfg, edge_layout
         L = cfg.num_gnn_layers
         dev = torch.device(device)
         mv = lambda pair: tuple(x.to(dev).contiguous() for x in pair)  # noqa: E731
@@ -336,7 +373,7 @@ class PackedGeoT:
         im, iv, ps, pd = init_blob(sd, dtype)
         self.init = mv((im, iv))
         self.pos_src, self.pos_dst = ps.to(dev).contiguous(), pd.to(dev).contiguous()
-        self.edge = [mv(edge_blob(sd, li, li == L - 1, dtype, cfg)) for li in range(L)]
+        self.edge = [mv(edge_blob(sd, li, li == L - 1, dtype, cfg, layout=edge_layout)) for li in range(L)]
         self.node = [mv(node_blob(sd, li, li == L - 1, dtype)) for li in range(L)]
 
     @property

@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define DI_ABI_VERSION 4
+#define DI_ABI_VERSION 5
 
 /* activation / weight storage type of the GeoT kernels (accumulation is always fp32). A plain
  * int32 (not a C enum type): a foreign caller may pass any value, and every entry point refuses
@@ -102,6 +102,12 @@ int di_abi_version(void);
  * 2 edge_layer(non-final), 3 edge_layer(final), 4 node_layer(non-final), 5 node_layer(final).
  * `vec` selects the fp32 vector blob (biases) instead of the matrix blob. */
 int64_t di_blob_bytes(int kind, di_dtype dtype, int vec);
+/* MFMA fragment order of a kind's matrix blob in this build (ABI 5): 16 = blocks of 16 output rows
+ * x 32 input features (v_mfma_f32_16x16x32_bf16 / 16x16x4_f32 A fragments), 32 = blocks of 32
+ * output rows x 16 input features (v_mfma_f32_32x32x16_bf16: the bf16 edge-layer blobs, kinds 2
+ * and 3); -1 for an unknown kind or dtype. Both orders hold the same number of 512-element blocks at
+ * the same block offsets (deepinteract_amd/packing.py: pack_matrix / pack_matrix32). */
+int di_blob_layout(int kind, di_dtype dtype);
 
 /* in_dim: width of node_f rows (113 for LitGINI's raw node features; 128 with an identity
  * embedding when DGLGeometricTransformer is used standalone on already-embedded features) */
@@ -121,13 +127,14 @@ int di_init_edge(const di_graph* g, di_dtype dt, const float* edge_f /*[Et,28]*/
 int di_init_edge_resident(const di_graph* g, const float* edge_f /*[Et,28]*/, const void* wmat /*bf16 blob*/,
                           const float* wvec, const float* pos_src_tab, const float* pos_dst_tab,
                           void* f_out /*[Et,128] bf16*/, void* stream);
-/* di_node_embed + di_init_edge (bf16, DI_GRAPH_GEO_REF, no Fn) as ONE launch: the embedding runs as
- * the launch's first blocks, beside InitEdge's, through the same LDS slot -- instead of on a side
- * stream. h_out / qkv_out / f_out bit-identical to the two separate calls. 0 < in_dim <= 128. */
-int di_embed_init_edge(const di_graph* g, int32_t in_dim, const float* node_f /*[Nt,in_dim]*/, const void* embed_wmat,
-                       const float* embed_wvec, void* h_out /*[Nt,128]*/, void* qkv_out /*[Nt,384]*/,
-                       const float* edge_f, const void* init_wmat, const float* init_wvec, const float* pos_src_tab,
-                       const float* pos_dst_tab, void* f_out /*[Et,128]*/, void* stream);
+/* di_node_embed + di_init_edge (DI_GRAPH_GEO_REF, no Fn) as ONE launch: the embedding runs as the
+ * launch's first blocks, beside InitEdge's, through the same LDS slot -- instead of on a side
+ * stream. h_out / qkv_out / f_out bit-identical to the two separate calls. 0 < in_dim <= 128.
+ * ABI 5: any dtype (fp32 added: the embedding of the reference's precision inside the launch). */
+int di_embed_init_edge(const di_graph* g, di_dtype dt, int32_t in_dim, const float* node_f /*[Nt,in_dim]*/,
+                       const void* embed_wmat, const float* embed_wvec, void* h_out /*[Nt,128]*/,
+                       void* qkv_out /*[Nt,384]*/, const float* edge_f, const void* init_wmat, const float* init_wvec,
+                       const float* pos_src_tab, const float* pos_dst_tab, void* f_out /*[Et,128]*/, void* stream);
 
 int di_edge_layer(const di_graph* g, di_dtype dt, int final_layer, const float* edge_f,
                   const void* f_in, const void* fn_in, const void* qkv,

@@ -11,14 +11,21 @@ import torch
 from deepinteract_amd import packing
 
 
-def _unpack(mat, off, nbo, ns, dtype):
-    r, c = packing._pack_index(dtype)
+def _unpack(mat, off, nout, kin, dtype, layout=16):
+    """W [nout, kin] from the packed blocks at block offset `off` (16-row or 32-row fragment order)."""
     flat = mat.to(torch.float64).numpy()
-    W = np.zeros((16 * nbo, 32 * ns))
+    W = np.zeros((nout, kin))
+    if layout == 32:
+        r, c = packing._pack_index32()
+        rows, cols = 32, 16
+    else:
+        r, c = packing._pack_index(dtype)
+        rows, cols = 16, 32
+    nbo, ns = nout // rows, kin // cols
     for bo in range(nbo):
         for s in range(ns):
             k = off + bo * ns + s
-            W[16 * bo + r, 32 * s + c] = flat[k * 512:(k + 1) * 512]
+            W[rows * bo + r, cols * s + c] = flat[k * 512:(k + 1) * 512]
     return W
 
 
@@ -38,7 +45,8 @@ class Emu:
         self.u = np.log(2.0) if packed.dtype == "bf16" else 1.0  # silu = silu2 * u
 
     def M(self, blob, off, nout, kin):
-        return _unpack(blob[0], off, nout // 16, kin // 32, self.dt)
+        layout = self.p.edge_layout if any(blob is e for e in self.p.edge) else 16
+        return _unpack(blob[0], off, nout, kin, self.dt, layout)
 
     def geot(self, g):
         """g: dict with num_nodes, src, dst, node_f, edge_f, src_nbr, dst_nbr (torch)."""

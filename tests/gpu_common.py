@@ -31,3 +31,12 @@ def rel_max(a, b):
     a = np.asarray(a, dtype=np.float64)
     b = np.asarray(b, dtype=np.float64)
     return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-30))
+
+
+def rel_elem(a, b, floor=0.0):
+    """Elementwise relative error max |a - b| / max(|b|, floor) (north_star's "<= 1e-4 relative"
+    read per element; rel_max is the normwise figure). floor > 0 only for signed features whose
+    reference values cross zero; contact probabilities (in (0, 1)) use none."""
+    a = np.asarray(a, dtype=np.float64)
+    b = np.asarray(b, dtype=np.float64)
+    return float((np.abs(a - b) / np.maximum(np.abs(b), floor)).max())

@@ -76,7 +76,8 @@ def main(path):
         expect(lib.di_init_edge(gp, 1, p, p, p, p, p, p, None, None), EINVAL, "init Fn")
         expect(lib.di_init_edge(gp, 9, p, p, p, p, p, p, p, None), EINVAL, "init dtype")
         expect(lib.di_init_edge_resident(gp, p, p, p, p, p, None, None), EINVAL, "init resident f_out")
-        expect(lib.di_embed_init_edge(gp, 129, p, p, p, p, p, p, p, p, p, p, p, None), EINVAL, "embed+init in_dim")
+        expect(lib.di_embed_init_edge(gp, 1, 129, p, p, p, p, p, p, p, p, p, p, p, None), EINVAL, "embed+init in_dim")
+        expect(lib.di_embed_init_edge(gp, 6, 113, p, p, p, p, p, p, p, p, p, p, p, None), EINVAL, "embed+init dtype")
         expect(lib.di_edge_layer(gp, 1, 0, p, p, None, p, p, p, p, p, p, None), EINVAL, "edge Fn in")
         expect(lib.di_edge_layer(gp, 1, 0, p, p, p, p, p, p, p, p, None, None), EINVAL, "edge Fn out")
         expect(lib.di_edge_layer(gp, 1, 0, p, p, p, p, p, p, p, None, p, None), EINVAL, "edge f_out")

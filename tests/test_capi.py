@@ -25,12 +25,17 @@ def test_library_builds_and_exports_all_declared_symbols():
 
 def test_abi_version_and_blob_sizes():
     lib = _lib.load()
-    assert lib.di_abi_version() == _lib.ABI_VERSION == 4
+    assert lib.di_abi_version() == _lib.ABI_VERSION == 5
     for kind, (nblk, nvec) in packing.BLOB_SIZES.items():
         assert lib.di_blob_bytes(kind, _lib.DI_F32, 0) == nblk * 512 * 4
         assert lib.di_blob_bytes(kind, _lib.DI_BF16, 0) == nblk * 512 * 2
         assert lib.di_blob_bytes(kind, _lib.DI_F32, 1) == nvec * 4
     assert lib.di_blob_bytes(9, _lib.DI_F32, 0) == -1
+    # fragment order (ABI 5): the bf16 edge-layer blobs are packed for v_mfma_f32_32x32x16_bf16
+    for kind in range(7):
+        assert lib.di_blob_layout(kind, _lib.DI_F32) == 16
+        assert lib.di_blob_layout(kind, _lib.DI_BF16) == (32 if kind in (2, 3) else 16)
+    assert lib.di_blob_layout(7, _lib.DI_BF16) == -1 and lib.di_blob_layout(2, 5) == -1
 
 
 def test_invalid_arguments_rejected_without_gpu():
@@ -80,7 +85,8 @@ def test_geo_ref_fn_contract_without_gpu():
     assert lib.di_init_edge(ctypes.byref(g), _lib.DI_BF16, p, p, p, p, p, p, None, None) == -1
     # the resident InitEdge is the DI_GRAPH_GEO_REF path only
     assert lib.di_init_edge_resident(ctypes.byref(g), p, p, p, p, p, p, None) == -1
-    assert lib.di_embed_init_edge(ctypes.byref(g), 113, p, p, p, p, p, p, p, p, p, p, p, None) == -1
+    assert lib.di_embed_init_edge(ctypes.byref(g), _lib.DI_BF16, 113, p, p, p, p, p, p, p, p, p, p, p, None) == -1
+    assert lib.di_embed_init_edge(ctypes.byref(g), _lib.DI_F32, 113, p, p, p, p, p, p, p, p, p, p, p, None) == -1
     assert lib.di_edge_layer(ctypes.byref(g), _lib.DI_BF16, 0, p, p, None, p, p, p, p, p, p, None) == -1
     assert lib.di_edge_layer(ctypes.byref(g), _lib.DI_BF16, 0, p, p, p, p, p, p, p, p, None, None) == -1
     assert _lib.DI_GRAPH_GEO_REF == 1

@@ -1,6 +1,7 @@
-"""World-size-2 gloo tests of the complex-sharded path (CPU): the contiguous sharding plan, the
-single all-gather of contact maps (incl. a rank that owns no complex, bf16 maps) and the
-composed C4 driver ``predict_sharded`` with a CPU stand-in for the GPU forward."""
+"""World-size-2/3 gloo tests of the complex-sharded path (CPU): the contiguous sharding plan, the
+single all-gather of contact maps (incl. a rank that owns no complex, bf16 maps), the chunked
+round-by-round asynchronous all-gather, and the composed C4 driver ``predict_sharded`` with a CPU
+stand-in for the GPU forward (both gather modes: bit-identical maps)."""
 import os
 import socket
 
@@ -10,7 +11,8 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from deepinteract_amd.distributed import all_gather_maps, complex_cost, local_order, predict_sharded, shard
+from deepinteract_amd.distributed import (all_gather_maps, complex_cost, gather_rounds, local_order, predict_sharded,
+                                          shard)
 
 
 def test_shard_contiguous_balanced_and_complete():
@@ -37,6 +39,23 @@ def test_shard_contiguous_balanced_and_complete():
 def test_local_order_size_sorted():
     sizes = [(10, 10), (30, 30), (20, 20), (30, 30)]
     assert local_order(sizes, [0, 1, 2, 3]) == [1, 3, 2, 0]
+
+
+def test_gather_rounds_cover_every_complex_once():
+    """Round c holds micro-batch c of every rank; uneven ranks contribute nothing to later rounds;
+    each round's width is its largest rank's element count."""
+    sizes = [(30, 22), (25, 25), (40, 21), (21, 33), (28, 30), (10, 10), (12, 9)]
+    for world in (1, 2, 3, 8):
+        plan = shard(sizes, world)
+        rounds = gather_rounds(sizes, plan, 2)
+        seen = [i for members, _ in rounds for ids in members for i in ids]
+        assert sorted(seen) == list(range(len(sizes)))
+        for members, width in rounds:
+            assert len(members) == world
+            assert width == max(max(sum(sizes[i][0] * sizes[i][1] for i in ids) for ids in members), 1)
+        for r in range(world):
+            mine = [i for members, _ in rounds for i in members[r]]
+            assert mine == local_order(sizes, plan[r])
 
 
 def _free_port():
@@ -111,23 +130,27 @@ def _cpu_forward(batch, ids):
     return out
 
 
-def _worker_predict(rank, world, port, q):
+def _worker_predict(rank, world, port, gather, dtype, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         cx = _complexes()
-        maps, plan = predict_sharded(cx, _cpu_forward, micro_batch=2)
-        ref = _cpu_forward(cx, list(range(len(cx))))
-        ok = len(maps) == len(cx) and all(torch.equal(m, r) for m, r in zip(maps, ref))
+        maps, plan = predict_sharded(cx, _cpu_forward, micro_batch=2, gather=gather, dtype=dtype)
+        ref = [m.to(dtype) for m in _cpu_forward(cx, list(range(len(cx))))]
+        ok = len(maps) == len(cx) and all(m.dtype == dtype and torch.equal(m, r) for m, r in zip(maps, ref))
         q.put((rank, ok, [len(p) for p in plan]))
     finally:
         dist.destroy_process_group()
 
 
-def test_predict_sharded_gloo():
-    """The composed C4 driver: contiguous shard -> size-sorted micro-batches -> forward -> one
-    all-gather; every rank ends with every complex's map, equal to a single-process run."""
-    res = _spawn(_worker_predict, 2)
+@pytest.mark.parametrize("world,gather,dtype", [(2, "once", torch.float32), (2, "chunked", torch.float32),
+                                                (3, "chunked", torch.float32), (2, "chunked", torch.bfloat16)])
+def test_predict_sharded_gloo(world, gather, dtype):
+    """The composed C4 driver: contiguous shard -> size-sorted micro-batches -> forward -> the maps
+    gathered once at the end or round by round with asynchronous all-gathers (world 3: ranks with
+    different micro-batch counts); every rank ends with every complex's map, equal to a
+    single-process run."""
+    res = _spawn(_worker_predict, world, gather, dtype)
     assert all(ok for _, ok, _ in res), res
     assert sum(res[0][2]) == len(_complexes())

@@ -18,7 +18,7 @@ import numpy as np
 import pytest
 import torch
 
-from gpu_common import chain_arrays, chain_item, load_case, rel_max
+from gpu_common import chain_arrays, chain_item, load_case, rel_elem, rel_max
 
 pytestmark = pytest.mark.gpu
 F32_TOL = 1e-4
@@ -101,6 +101,10 @@ def test_shared_step_and_predict_step(model_f32, case):
     assert rel_max(_np(out[0][0]), z["logits"]) < F32_TOL
     from deepinteract_amd.head import contact_probs
     assert rel_max(_np(contact_probs(out[0][0])), z["probs"]) < F32_TOL
+    # elementwise relative error of every contact probability (north_star: <= 1e-4 relative)
+    pe = rel_elem(_np(contact_probs(out[0][0])), z["probs"])
+    print(f"{case} predict_step contact probabilities: elementwise relative {pe:.3e}")
+    assert pe < F32_TOL
 
 
 def test_gnn_forward_batched_graphs(model_f32):

@@ -10,7 +10,7 @@ import numpy as np
 import pytest
 import torch
 
-from gpu_common import chain_arrays, chain_item, load_case, rel_max
+from gpu_common import chain_arrays, chain_item, load_case, rel_elem, rel_max
 
 pytestmark = pytest.mark.gpu
 
@@ -253,6 +253,11 @@ def test_end_to_end_logits_f32(sd, case):
     torch.cuda.synchronize()
     assert rel_max(logits[0].cpu().numpy(), z["logits"]) < F32_TOL
     assert rel_max(probs[0].cpu().numpy(), z["probs"]) < F32_TOL
+    # elementwise relative error of every contact probability (north_star: <= 1e-4 relative)
+    pe = rel_elem(probs[0].cpu().numpy(), z["probs"])
+    print(f"{case} fp32 contact probabilities: normwise {rel_max(probs[0].cpu().numpy(), z['probs']):.3e}, "
+          f"elementwise relative {pe:.3e}")
+    assert pe < F32_TOL
 
 
 def test_geot_reference_init_weights():
@@ -341,31 +346,35 @@ def test_init_edge_resident_matches_staged(engines):
                                      _ptr(p.pos_src), _ptr(p.pos_dst), _ptr(f_res), None) == -1
 
 
-def test_embed_init_edge_one_launch_matches_separate(engines):
+@pytest.mark.parametrize("dtype", ["bf16", "f32"])
+def test_embed_init_edge_one_launch_matches_separate(engines, dtype):
     """di_embed_init_edge (the node embedding as the first blocks of the staged InitEdge launch) vs
-    di_node_embed + di_init_edge: h, qkv and F bit-identical on the 8x-concatenated c2 batch."""
+    di_node_embed + di_init_edge: h, qkv and F bit-identical on the 8x-concatenated c2 batch, in
+    both storage dtypes (fp32: the reference's precision, round 4)."""
     import ctypes
     from deepinteract_amd import _lib
     from deepinteract_amd.engine import _ptr
     from deepinteract_amd.graph import concat_batches
     gb = concat_batches([_batch(load_case("c2"))] * 8)
-    eng = engines["bf16"]
+    eng = engines[dtype]
     p, lib = eng.packed, eng.lib
+    di = _lib.DI_BF16 if dtype == "bf16" else _lib.DI_F32
+    tdt = torch.bfloat16 if dtype == "bf16" else torch.float32
     g = ctypes.byref(gb.c_graph)
     n, e, d = gb.num_nodes, gb.num_edges, gb.node_f.shape[1]
     outs = []
     for fused in (True, False):
-        h = torch.full((n, 128), float("nan"), dtype=torch.bfloat16, device="cuda")
-        qkv = torch.full((n, 384), float("nan"), dtype=torch.bfloat16, device="cuda")
-        f = torch.full((e, 128), float("nan"), dtype=torch.bfloat16, device="cuda")
+        h = torch.full((n, 128), float("nan"), dtype=tdt, device="cuda")
+        qkv = torch.full((n, 384), float("nan"), dtype=tdt, device="cuda")
+        f = torch.full((e, 128), float("nan"), dtype=tdt, device="cuda")
         if fused:
-            _lib.check(lib.di_embed_init_edge(g, d, _ptr(gb.node_f), _ptr(p.embed[0]), _ptr(p.embed[1]), _ptr(h),
+            _lib.check(lib.di_embed_init_edge(g, di, d, _ptr(gb.node_f), _ptr(p.embed[0]), _ptr(p.embed[1]), _ptr(h),
                                               _ptr(qkv), _ptr(gb.edge_f), _ptr(p.init[0]), _ptr(p.init[1]),
                                               _ptr(p.pos_src), _ptr(p.pos_dst), _ptr(f), None), "di_embed_init_edge")
         else:
-            _lib.check(lib.di_node_embed(g, _lib.DI_BF16, d, _ptr(gb.node_f), _ptr(p.embed[0]), _ptr(p.embed[1]),
+            _lib.check(lib.di_node_embed(g, di, d, _ptr(gb.node_f), _ptr(p.embed[0]), _ptr(p.embed[1]),
                                          _ptr(h), _ptr(qkv), None), "di_node_embed")
-            _lib.check(lib.di_init_edge(g, _lib.DI_BF16, _ptr(gb.edge_f), _ptr(p.init[0]), _ptr(p.init[1]),
+            _lib.check(lib.di_init_edge(g, di, _ptr(gb.edge_f), _ptr(p.init[0]), _ptr(p.init[1]),
                                         _ptr(p.pos_src), _ptr(p.pos_dst), _ptr(f), None, None), "di_init_edge")
         outs.append((h, qkv, f))
     torch.cuda.synchronize()

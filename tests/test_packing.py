@@ -83,6 +83,64 @@ def test_packed_linear_matches_dense(dtype, nout, kin):
     np.testing.assert_array_equal(rows_from_act(out), x @ W.T)
 
 
+def test_packed32_linear_matches_dense():
+    """v_mfma_f32_32x32x16_bf16 lane maps (cdna_hip_programming.md §3: A[l&31][8(l>>5)+j],
+    B[8(l>>5)+j][l&31], C/D row (reg&3)+8(reg>>2)+4(l>>5), col l&31): a pack_matrix32 weight times
+    an activation held as 32x32 accumulators (csrc/mfma32.h), the accumulator's registers 8t..8t+7
+    of block b taken as k-step 2b+t, equals W @ x; and the chained product (output accumulator
+    reused as the next B operand) too."""
+    rng = np.random.default_rng(2)
+
+    def acc_from_rows(x):  # x [32 rows, F] -> acc[lane][block][reg]
+        F = x.shape[1]
+        acc = np.zeros((64, F // 32, 16))
+        for lane in range(64):
+            for b in range(F // 32):
+                for k in range(16):
+                    acc[lane, b, k] = x[lane & 31, 32 * b + 8 * (k >> 2) + 4 * (lane >> 5) + (k & 3)]
+        return acc
+
+    def rows_from_acc(acc):
+        x = np.zeros((32, acc.shape[1] * 32))
+        for lane in range(64):
+            for b in range(acc.shape[1]):
+                for k in range(16):
+                    x[lane & 31, 32 * b + 8 * (k >> 2) + 4 * (lane >> 5) + (k & 3)] = acc[lane, b, k]
+        return x
+
+    def emulate(packed, nbo, ns, acc):
+        out = np.zeros((64, nbo, 16))
+        for s in range(ns):
+            bop = acc[:, s // 2, 8 * (s % 2):8 * (s % 2) + 8]  # [64, 8]
+            B = np.zeros((16, 32))
+            for lane in range(64):
+                B[8 * (lane >> 5):8 * (lane >> 5) + 8, lane & 31] = bop[lane]
+            for bo in range(nbo):
+                blk = packed[(bo * ns + s) * 512:(bo * ns + s + 1) * 512].reshape(64, 8)
+                A = np.zeros((32, 16))
+                for lane in range(64):
+                    A[lane & 31, 8 * (lane >> 5):8 * (lane >> 5) + 8] = blk[lane]
+                D = A @ B
+                for lane in range(64):
+                    for k in range(16):
+                        out[lane, bo, k] += D[(k & 3) + 8 * (k >> 2) + 4 * (lane >> 5), lane & 31]
+        return out
+
+    for nout, kin in ((32, 32), (64, 128), (128, 64)):
+        W = rng.integers(-4, 5, size=(nout, kin)).astype(np.float64)
+        x = rng.integers(-4, 5, size=(32, kin)).astype(np.float64)
+        out = emulate(packing.pack_matrix32(W), nout // 32, kin // 16, acc_from_rows(x))
+        np.testing.assert_array_equal(rows_from_acc(out), x @ W.T)
+    W1 = rng.integers(-3, 4, size=(128, 64)).astype(np.float64)
+    W2 = rng.integers(-3, 4, size=(64, 128)).astype(np.float64)
+    x = rng.integers(-3, 4, size=(32, 64)).astype(np.float64)
+    y = emulate(packing.pack_matrix32(W1), 4, 4, acc_from_rows(x))
+    z = emulate(packing.pack_matrix32(W2), 2, 8, y)
+    np.testing.assert_array_equal(rows_from_acc(z), x @ W1.T @ W2.T)
+    # same block count and offsets as the 16-row order
+    assert packing.pack_matrix32(W1).size == packing.pack_matrix(W1, "bf16").size
+
+
 def test_blob_sizes_match_layout():
     from deepinteract_amd.weights import seeded_state_dict
     sd = seeded_state_dict(0, with_head=False)
@@ -95,6 +153,8 @@ def test_blob_sizes_match_layout():
     assert p.pos_src.shape == (2304, 128)
     pb = packing.PackedGeoT(sd, "bf16")
     assert pb.edge[0][0].dtype == torch.bfloat16
+    assert pb.edge_layout == 32 and p.edge_layout == 16
+    assert pb.edge[0][0].numel() == sizes[2][0] * 512 and pb.edge[1][0].numel() == sizes[3][0] * 512
 
 
 @pytest.mark.parametrize("dtype", ["bf16", "f32"])
