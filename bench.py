@@ -516,6 +516,12 @@ def main():
                     help="K > 0: pair tensor on a CU-masked stream of K dedicated CUs (K blocks x 8 waves), "
                          "GeoT on the other CUs (needs --overlap 1)")
     ap.add_argument("--cu-layout", default="stride", choices=["stride", "contig"])
+    ap.add_argument("--pair-mask", type=int, default=0,
+                    help="K > 0: the pair-tensor stream CU-masked to K CUs (its default grid unchanged), GeoT "
+                         "on every CU; with --node-cus the node layers on a stream masked to the other CUs")
+    ap.add_argument("--node-cus", type=int, default=0, choices=[0, 1],
+                    help="1 (needs --pair-mask): node layers on a stream CU-masked to the CUs the pair stream "
+                         "does not use")
     ap.add_argument("--pair-kernel", default="auto", choices=["auto", "lines", "rows", "vector"],
                     help="pair-tensor kernel (auto: row streaming for 16-B aligned planes, per-vector otherwise)")
     ap.add_argument("--pair-blocks", type=int, default=0)
@@ -662,6 +668,13 @@ def main():
         cus_pair, cus_geot = split_cus(num_cus, args.pair_cus, args.cu_layout)
         s_geot = masked_stream(dev, cus_geot, num_cus)
         s_pair = masked_stream(dev, cus_pair, num_cus)
+    elif args.pair_mask:
+        from deepinteract_amd.streams import masked_stream, split_cus
+        cus_pair, cus_rest = split_cus(num_cus, args.pair_mask, args.cu_layout)
+        s_geot = torch.cuda.current_stream(dev)
+        s_pair = masked_stream(dev, cus_pair, num_cus)
+        if args.node_cus:
+            eng.node_stream = masked_stream(dev, cus_rest, num_cus)
     else:
         s_geot = torch.cuda.current_stream(dev)
         s_pair = torch.cuda.Stream(dev) if args.overlap else s_geot
@@ -705,6 +718,8 @@ def main():
                                "GeoT || pair-tensor (2 HIP streams, pair after InitEdge)"][args.overlap]
                    + (f"; pair on {args.pair_cus} dedicated CUs ({args.cu_layout}), GeoT on "
                       f"{num_cus - args.pair_cus}" if args.pair_cus else "")
+                   + (f"; pair stream masked to {args.pair_mask} CUs ({args.cu_layout})"
+                      + ("; node layers masked to the other CUs" if args.node_cus else "") if args.pair_mask else "")
                    + f"; pair kernel {args.pair_kernel} ({args.pair_waves}-wave blocks"
                    + (f", {args.pair_blocks} resident" if args.pair_blocks else "")
                    + (", bounded store queue, nt stores)" if args.pair_beside else ")")

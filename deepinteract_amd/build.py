@@ -69,6 +69,9 @@ def build(force: bool = False, verbose: bool = True, defines=(), out: str | None
     lib_path = out or LIB
     if not force and not defines and out is None and up_to_date():
         return LIB
+    if not force and out is not None and os.path.exists(out) and \
+            all(os.path.getmtime(p) <= os.path.getmtime(out) for p in _deps()):
+        return out  # a variant (fixed defines per output path) newer than every source
     objdir = os.path.join(os.path.dirname(lib_path), "obj")
     os.makedirs(objdir, exist_ok=True)
     objs = []

@@ -27,7 +27,26 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <atomic>
+
 namespace di {
+
+// Compute units of the CURRENT device (persistent grids), cached per device id: one attribute query
+// per device and process, and a process driving several devices sizes each grid from its own device.
+inline int device_cus() {
+  constexpr int MAXDEV = 64;
+  static std::atomic<int> cache[MAXDEV];  // 0: not queried yet
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0) dev = 0;
+  if (dev < MAXDEV) {
+    const int c = cache[dev].load(std::memory_order_relaxed);
+    if (c > 0) return c;
+  }
+  int v = 0;
+  if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
+  if (dev < MAXDEV) cache[dev].store(v, std::memory_order_relaxed);
+  return v;
+}
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 typedef float floatx2 __attribute__((ext_vector_type(2)));
@@ -270,6 +289,15 @@ template <int NB>
 __device__ __forceinline__ void mul_(Act<NB>& a, const Act<NB>& b_) {
 #pragma unroll
   for (int b = 0; b < NB; ++b) a.v[b] *= b_.v[b];
+}
+
+// scheduling fence between row groups / phases (keeps the compiler from interleaving, and so
+// doubling the live state of, independent groups). The memory clobber also keeps the groups'
+// reads of the same LDS slot (A fragments, biases) from being merged into one live copy shared by
+// both groups.
+__device__ __forceinline__ void lean_fence() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
 }
 
 // ------------------------------------------------------------------ MFMA operands

@@ -446,6 +446,232 @@ void k_init_edge_res(InitArgs a, int ntiles) {
   }
 }
 
+// ================================================================ InitEdgeModule on 32x32x16 MFMA (bf16)
+// The arithmetic of k_init_edge<BF16T, GC> on 32-row tiles (csrc/mfma32.h): every 128-wide stage is
+// half the MFMAs of the 16x16 form, so half the MFMA hold on the SIMD's vector issue the SiLU-heavy
+// InitEdge is bound by (640 SiLU values per edge against 65,536 MAC). The bf16 init blob (kind 1) is
+// packed in the 32x32 fragment order (di_blob_layout(1, bf16) == 32). Geometric terms and gates are
+// produced one 32-feature block at a time (16 registers) and packed / multiplied straight away, so
+// a 32-row tile fits three waves per SIMD (<= 168 VGPRs).
+// Weight phases of one tile (GC: DI_GRAPH_GEO_REF batches):
+//   T0 (collapsed edge-message map, [128x32] 8 blk) -> geometric terms (dist, [dir, orient,] amide:
+//   [128x32] W_t0 + [128x128] combined_linear_0 slice, 40 blk each) -> gates (em1, dist1, [dir1,
+//   orient1,] amide1: [128x32] each) -> combined_linear_1/2 (8 + 8 blk) -> [layer-0 nbr_linear, 32 blk]
+#ifndef DI_INIT_X32
+#define DI_INIT_X32 1
+#endif
+struct InitX32Geo {
+  static constexpr int NW = 4, THREADS = 64 * NW, ROWS_PER_WAVE = 32, ROWS = ROWS_PER_WAVE * NW;
+};
+
+// one 32-row tile of InitEdge; wt(phase) returns the phase's weight blocks (LDS) and gate_off(t) the
+// block offset of gate t (0 em, 1 dist, 2 dir, 3 orient, 4 amide) inside the gates phase.
+// acc enters holding emb[src] + emb[dst] slots (+ the orientation constant for GC).
+template <bool GC, class WT, class GO>
+__device__ __forceinline__ void init_tile_x32(X32<4>& acc, const P32<2>& gop, const float* wvec, int lane, int h,
+                                              WT&& wt, GO&& gate_off, X32<4>& f) {
+  mma32<4, 2>(acc, gop, wt(0), lane);  // t = 0: the collapsed [128, 2] edge-message map
+  constexpr int NT = GC ? 2 : 4;
+#pragma unroll 1
+  for (int i = 0; i < NT; ++i) {
+    const u16* w = wt(1 + i);
+    // y = silu2(W_t0 . g), one 32-feature block at a time, packed as combined_linear_0's operand
+    P32<8> yop;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      lean_fence();  // block by block: one block's fragments and values live at a time
+      floatx16 y = {};
+      y = mfma32(afrag(w, 2 * b, lane), gop.f[0], y);
+      y = mfma32(afrag(w, 2 * b + 1, lane), gop.f[1], y);
+      silu2_blk(y);
+      pack_blk(yop.f[2 * b], yop.f[2 * b + 1], y);
+      asm volatile("" : "+v"(yop.f[2 * b]), "+v"(yop.f[2 * b + 1]));
+    }
+    mma32<4, 8>(acc, yop, w + 8 * BLK, lane);
+    pin(acc);
+  }
+#pragma unroll
+  for (int b = 0; b < 4; ++b) silu2_blk(acc.v[b]);  // combined_edge_logits (log2 units)
+  pin(acc);  // computed here: sunk to their uses, x and rcp(1 + 2^-x) would both stay live
+  // gating: (em1 + silu(d1) + silu(r1) + silu(o1) + silu(a1)) * c, block by block
+  {
+    const u16* w = wt(1 + NT);
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      lean_fence();
+      floatx16 gs = {};
+      if constexpr (GC) {  // silu(o1): the packed constant IEV_OGATE (silu(r1) = 0)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) set_quad(gs, q, ld4(wvec + IEV_OGATE + 32 * b + 8 * q + 4 * h));
+      }
+#pragma unroll
+      for (int t = 0; t < 5; ++t) {
+        if (GC && (t == 2 || t == 3)) continue;
+        __builtin_amdgcn_sched_barrier(0);
+        floatx16 y = {};
+        const u16* wg = w + gate_off(t) * BLK;
+        y = mfma32(afrag(wg, 2 * b, lane), gop.f[0], y);
+        y = mfma32(afrag(wg, 2 * b + 1, lane), gop.f[1], y);
+        if (t > 0) silu2_blk(y);
+        gs += y;
+      }
+      acc.v[b] *= gs;
+      asm volatile("" : "+v"(acc.v[b]));  // computed here (not sunk past the next stage barrier)
+    }
+  }
+  // combined_linear_2(combined_linear_1(.)) : 128 -> 28 (padded 32) -> 128
+  {
+    const u16* w = wt(2 + NT);
+    P32<8> aop;
+    make_op32(aop, acc);
+    X32<1> z;
+    zero(z);
+    mma32<1, 8>(z, aop, w, lane);
+    P32<2> zop;
+    make_op32(zop, z);
+    zero(f);
+    mma32<4, 2>(f, zop, w + 8 * BLK, lane);
+  }
+}
+
+// acc = pos_src[node_pos[src]] + pos_dst[node_pos[dst]] (the orientation constant of GEO_REF batches
+// arrives through the collapsed message map: geo_op32<true>)
+__device__ __forceinline__ void init_acc_x32(X32<4>& acc, const InitArgs& a, int ps, int pd, int h) {
+  const float* rs = a.pos_src + (int64_t)ps * HID;
+  const float* rd = a.pos_dst + (int64_t)pd * HID;
+#pragma unroll
+  for (int b = 0; b < 4; ++b)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int f = 32 * b + 8 * q + 4 * h;
+      set_quad(acc.v[b], q, ld4(rs + f) + ld4(rd + f));
+    }
+}
+
+// the edge's geometric features [28] as a 32-feature operand; ONE: features 28 and 29 = 1 (the
+// bf16 hi / lo columns of the orientation constant in the 32x32 init blob's message map), else 0
+template <bool ONE = false>
+__device__ __forceinline__ void geo_op32(P32<2>& gop, const float* edge_f, int e, int h) {
+  const float* grow = edge_f + (int64_t)e * NFEAT_E;
+  X32<1> geo;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int f = 8 * q + 4 * h;
+    set_quad(geo.v[0], q, f < NFEAT_E ? ld4(grow + f) : (ONE ? (floatx4){1.f, 1.f, 0.f, 0.f} : (floatx4){0.f, 0.f, 0.f, 0.f}));
+  }
+  make_op32(gop, geo);
+}
+
+// staged weights (one 40-block slot per block, three blocks per CU, as k_init_edge); the first
+// embed_blocks blocks run the node embedding (16x16 k_node_embed arithmetic, kind-0 blob)
+template <bool GC>
+__global__ __attribute__((amdgpu_flat_work_group_size(1, InitX32Geo::THREADS), amdgpu_waves_per_eu(3, 3)))
+void k_init_x32(InitArgs a, EmbedArgs ea, int embed_blocks) {
+  using G = InitGeo<BF16T>;
+  static_assert(G::NW == InitX32Geo::NW, "one LDS slot layout for both block kinds");
+  __shared__ __attribute__((aligned(16))) u16 lds[G::CAP * BLK];
+  const int lane = lane_id();
+  if ((int)blockIdx.x < embed_blocks) {  // uniform per block
+    WPipe<u16, G::NW, false, G::CAP> epipe(lds);
+    embed_block<BF16T>(ea, epipe, blockIdx.x, lane, lane >> 4);
+    return;
+  }
+  const int h = lane >> 5;
+  const int r = ((int)blockIdx.x - embed_blocks) * InitX32Geo::ROWS + (threadIdx.x >> 6) * InitX32Geo::ROWS_PER_WAVE +
+                (lane & 31);
+  const bool valid = r < a.Et;
+  const int e = valid ? r : a.Et - 1;
+  const u16* W = reinterpret_cast<const u16*>(a.wmat);
+  WPipe<u16, G::NW, false, G::CAP> pipe(lds);
+  pipe.issue(W + IE_T0 * BLK, 8);
+  P32<2> gop;
+  geo_op32<GC>(gop, a.edge_f, e, h);
+  X32<4> acc;
+  init_acc_x32(acc, a, a.node_pos[a.src[e]], a.node_pos[a.dst[e]], h);
+  const bool with_fn = a.fn_out != nullptr;  // uniform
+  constexpr int NT = GC ? 2 : 4;
+  auto geo_t = [](int i) { return GC ? (i == 0 ? 1 : 4) : i + 1; };
+  // phase p's weights: wait for its stage, issue the next one
+  auto wt = [&](int p) -> const u16* {
+    const u16* w = pipe.next();
+    if (p == 0) pipe.issue(W + (IE_T0 + 40 * geo_t(0)) * BLK, 40);
+    else if (p < NT) pipe.issue(W + (IE_T0 + 40 * geo_t(p)) * BLK, 40);
+    else if (p == NT) pipe.issue(W + IE_GEO1 * BLK, 40);
+    else if (p == NT + 1) pipe.issue(W + IE_C1 * BLK, 16);
+    else if (with_fn) pipe.issue(W + IE_NBR * BLK, MAT128);
+    return w;
+  };
+  X32<4> f;
+  init_tile_x32<GC>(acc, gop, a.wvec, lane, h, wt, [](int t) { return 8 * t; }, f);
+  if (valid) store_row32(f, reinterpret_cast<u16*>(a.f_out) + (int64_t)e * HID, h);
+  if (!with_fn) return;
+  // layer-0 silu(nbr_linear(F)), applied once per edge and gathered by the conformation module
+  const u16* w = pipe.next();
+  P32<8> fop;
+  make_op32(fop, f);
+  X32<4> fn;
+  init_vec32(fn, a.wvec + IEV_NBR, h);
+  mma32<4, 8>(fn, fop, w, lane);
+#pragma unroll
+  for (int b = 0; b < 4; ++b) silu_blk(fn.v[b]);
+  if (valid) store_row32(fn, reinterpret_cast<u16*>(a.fn_out) + (int64_t)e * HID, h);
+}
+
+// resident weights (DI_GRAPH_GEO_REF, no Fn): the path's 128 blocks loaded once per CU into LDS
+// (layout of k_init_edge_res), one 12-wave block per CU, waves striding over 32-edge tiles with the
+// next tile's src/dst -> node_pos chain issued a tile ahead
+constexpr int IRX_NW = 12;
+__global__ __attribute__((amdgpu_flat_work_group_size(1, 64 * IRX_NW), amdgpu_waves_per_eu(IRX_NW / 4, IRX_NW / 4)))
+void k_init_res_x32(InitArgs a, int ntiles) {
+  __shared__ __attribute__((aligned(16))) u16 w[IR_NBLK * BLK];
+  const u16* W = reinterpret_cast<const u16*>(a.wmat);
+  dma_blocks<IRX_NW>(w + IR_T0 * BLK, W + IE_T0 * BLK, 8);
+  dma_blocks<IRX_NW>(w + IR_DIST * BLK, W + (IE_T0 + 40 * 1) * BLK, 40);
+  dma_blocks<IRX_NW>(w + IR_AMIDE * BLK, W + (IE_T0 + 40 * 4) * BLK, 40);
+  dma_blocks<IRX_NW>(w + IR_GATE * BLK, W + IE_GEO1 * BLK, 16);               // em1, dist1
+  dma_blocks<IRX_NW>(w + (IR_GATE + 16) * BLK, W + (IE_GEO1 + 32) * BLK, 8);  // amide1
+  dma_blocks<IRX_NW>(w + IR_C * BLK, W + IE_C1 * BLK, 16);                    // combined_linear_1, _2
+  lds_dma_wait();
+  __syncthreads();
+  const int lane = lane_id(), h = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int stride = gridDim.x * IRX_NW;
+  auto edge_of = [&](int t) {
+    const int r = t * 32 + (lane & 31);
+    return r < a.Et ? r : a.Et - 1;
+  };
+  int tile = blockIdx.x * IRX_NW + wave;
+  int ps = 0, pd = 0;
+  if (tile < ntiles) {
+    const int e = edge_of(tile);
+    ps = a.node_pos[a.src[e]];
+    pd = a.node_pos[a.dst[e]];
+  }
+  auto wt = [&](int p) -> const u16* {
+    return w + (p == 0 ? IR_T0 : p == 1 ? IR_DIST : p == 2 ? IR_AMIDE : p == 3 ? IR_GATE : IR_C) * BLK;
+  };
+  auto gate_off = [](int t) { return t == 0 ? 0 : (t == 1 ? 8 : 16); };  // em1, dist1, amide1
+#pragma unroll 1
+  for (; tile < ntiles; tile += stride) {
+    const int r = tile * 32 + (lane & 31);
+    const bool valid = r < a.Et;
+    const int e = valid ? r : a.Et - 1;
+    P32<2> gop;
+    geo_op32<true>(gop, a.edge_f, e, h);
+    X32<4> acc;
+    init_acc_x32(acc, a, ps, pd, h);
+    const bool more = tile + stride < ntiles;  // uniform
+    if (more) {  // the next tile's positional-row indices
+      const int en = edge_of(tile + stride);
+      ps = a.node_pos[a.src[en]];
+      pd = a.node_pos[a.dst[en]];
+    }
+    X32<4> f;
+    init_tile_x32<true>(acc, gop, a.wvec, lane, h, wt, gate_off, f);
+    if (valid) store_row32(f, reinterpret_cast<u16*>(a.f_out) + (int64_t)e * HID, h);
+  }
+}
+
 // ================================================================ fused edge layer
 // Weight stage order of the edge layer: block offsets / sizes (csrc/layout.h) and the fp32
 // vector (bias) staged with each layer (-1: none).
@@ -744,14 +970,6 @@ struct Lean : KernelGeo<4> {
   static constexpr int GROUP_ROWS = ROWS;
   static constexpr int ROWS_ALL = GROUP_ROWS * LG;
 };
-// scheduling fence between row groups / phases (keeps the compiler from interleaving, and so
-// doubling the live state of, independent groups). The memory clobber also keeps the groups'
-// reads of the same LDS slot (A fragments, biases) from being merged into one live copy shared by
-// both groups.
-__device__ __forceinline__ void lean_fence() {
-  asm volatile("" ::: "memory");
-  __builtin_amdgcn_sched_barrier(0);
-}
 // Both row groups through one pass over the stage's A fragments: every LDS fragment read feeds
 // one MFMA per group. Both groups' accumulators are live across the loop.
 template <int NBO, int NS>
@@ -1895,14 +2113,6 @@ static inline int launch_status() {
 
 static inline bool dtype_ok(di_dtype dt) { return dt == DI_BF16 || dt == DI_F32; }
 
-// compute units of the current device (persistent grids)
-static int num_cus() {
-  int dev = 0, v = 0;
-  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0)
-    v = 256;
-  return v;
-}
-
 extern "C" int di_abi_version(void) { return DI_ABI_VERSION; }
 
 extern "C" int64_t di_blob_bytes(int kind, di_dtype dtype, int vec) {
@@ -1924,7 +2134,10 @@ extern "C" int64_t di_blob_bytes(int kind, di_dtype dtype, int vec) {
 
 extern "C" int di_blob_layout(int kind, di_dtype dtype) {
   if (!dtype_ok(dtype) || kind < 0 || kind > 6) return -1;
-  return (dtype == DI_BF16 && DI_EDGE_X32 && (kind == 2 || kind == 3)) ? 32 : 16;
+  if (dtype != DI_BF16) return 16;
+  if (kind == 2 || kind == 3) return DI_EDGE_X32 ? 32 : 16;
+  if (kind == 1) return DI_INIT_X32 ? 32 : 16;
+  return 16;
 }
 
 extern "C" int di_node_embed(const di_graph* g, di_dtype dt, int32_t in_dim, const float* node_f, const void* wmat,
@@ -1954,7 +2167,10 @@ extern "C" int di_init_edge(const di_graph* g, di_dtype dt, const float* edge_f,
   const dim3 gb = grid_of<InitGeo<BF16T>>(a.Et), bb = block_of<InitGeo<BF16T>>();
   const dim3 gf = grid_of<InitGeo<F32T>>(a.Et), bf = block_of<InitGeo<F32T>>();
   const EmbedArgs ne{};
-  if (dt == DI_BF16 && gc) hipLaunchKernelGGL((k_init_edge<BF16T, true>), gb, bb, 0, s, a, ne, 0);
+  const dim3 gx((unsigned)((a.Et + InitX32Geo::ROWS - 1) / InitX32Geo::ROWS)), bx(InitX32Geo::THREADS);
+  if (dt == DI_BF16 && DI_INIT_X32 && gc) hipLaunchKernelGGL((k_init_x32<true>), gx, bx, 0, s, a, ne, 0);
+  else if (dt == DI_BF16 && DI_INIT_X32) hipLaunchKernelGGL((k_init_x32<false>), gx, bx, 0, s, a, ne, 0);
+  else if (dt == DI_BF16 && gc) hipLaunchKernelGGL((k_init_edge<BF16T, true>), gb, bb, 0, s, a, ne, 0);
   else if (dt == DI_BF16) hipLaunchKernelGGL((k_init_edge<BF16T, false>), gb, bb, 0, s, a, ne, 0);
   else if (gc) hipLaunchKernelGGL((k_init_edge<F32T, true>), gf, bf, 0, s, a, ne, 0);
   else hipLaunchKernelGGL((k_init_edge<F32T, false>), gf, bf, 0, s, a, ne, 0);
@@ -1965,6 +2181,11 @@ template <class DT>
 static void launch_embed_init(const InitArgs& a, const EmbedArgs& ea, hipStream_t s) {
   using G = InitGeo<DT>;
   const int eb = (ea.Nt + G::ROWS - 1) / G::ROWS;
+  if (DT::kBF16 && DI_INIT_X32) {
+    const int ib = (a.Et + InitX32Geo::ROWS - 1) / InitX32Geo::ROWS;
+    hipLaunchKernelGGL((k_init_x32<true>), dim3((unsigned)(eb + ib)), dim3(InitX32Geo::THREADS), 0, s, a, ea, eb);
+    return;
+  }
   const int ib = (a.Et + G::ROWS - 1) / G::ROWS;
   hipLaunchKernelGGL((k_init_edge<DT, true>), dim3((unsigned)(eb + ib)), block_of<G>(), 0, s, a, ea, eb);
 }
@@ -1992,9 +2213,16 @@ extern "C" int di_init_edge_resident(const di_graph* g, const float* edge_f, con
     return DI_EINVAL;
   InitArgs a{g->num_edges, edge_f, g->src, g->dst, g->node_pos, wmat, wvec, pos_src_tab, pos_dst_tab, f_out, nullptr};
   // one block per CU holding the path's weights; never more blocks than the tiles need
+  const int cus = device_cus();
+  if (DI_INIT_X32) {
+    const int ntiles = (a.Et + 31) / 32;
+    const int need = (ntiles + IRX_NW - 1) / IRX_NW;
+    hipLaunchKernelGGL(k_init_res_x32, dim3((unsigned)(need < cus ? need : cus)), dim3(64 * IRX_NW), 0,
+                       (hipStream_t)stream, a, ntiles);
+    return launch_status();
+  }
   const int ntiles = (a.Et + ROWS_PER_WAVE - 1) / ROWS_PER_WAVE;
   const int need = (ntiles + IR_NW - 1) / IR_NW;
-  const int cus = num_cus();
   hipLaunchKernelGGL(k_init_edge_res, dim3((unsigned)(need < cus ? need : cus)), block_of<InitResGeo>(), 0,
                      (hipStream_t)stream, a, ntiles);
   return launch_status();

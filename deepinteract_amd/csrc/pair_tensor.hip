@@ -303,16 +303,6 @@ void k_pair_lines(const di_pair_desc* __restrict__ descs, int hidden, const T* _
 
 using namespace di;
 
-static int pair_num_cus() {
-  static const int n = [] {
-    int dev = 0, v = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0)
-      v = 256;
-    return v;
-  }();
-  return n;
-}
-
 // a * b <= limit for non-negative a, b, without forming the (possibly overflowing) product
 static inline bool mul_le(int64_t a, int64_t b, int64_t limit) { return a == 0 || b <= limit / a; }
 
@@ -361,7 +351,7 @@ extern "C" int di_pair_tensor(di_dtype dt, const di_pair_desc* descs, int32_t nu
   if (kernel == DI_PAIR_AUTO) kernel = aligned >= 1 ? DI_PAIR_ROWS : 0;
   if (kernel == DI_PAIR_LINES && aligned < 2) return DI_EINVAL;  // whole-line stores need 128-B planes
   if ((kernel == DI_PAIR_ROWS || kernel == DI_PAIR_VECTOR) && aligned < 1) return DI_EINVAL;
-  const int max_blocks = L.blocks > 0 ? L.blocks : pair_num_cus();
+  const int max_blocks = L.blocks > 0 ? L.blocks : device_cus();
   const int waves = L.waves_per_block > 0 ? L.waves_per_block : 4;
   const bool beside = L.beside != 0;
   hipStream_t s = (hipStream_t)stream;

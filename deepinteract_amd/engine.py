@@ -79,23 +79,28 @@ class GeoTEngine:
         self.device = gpu_device(device)
         self.lib = _lib.load()
         self.dtype, self.cfg = dtype, cfg
-        # fragment order of the edge-layer blobs this library build reads (ABI 5)
+        # fragment order of the edge-layer / InitEdge blobs this library build reads (ABI 5)
         layout = self.lib.di_blob_layout(2, _DI_DT[dtype])
-        if layout not in (16, 32) or layout != self.lib.di_blob_layout(3, _DI_DT[dtype]):
-            raise RuntimeError(f"unexpected edge-blob layout {layout}")
-        self.packed = PackedGeoT(state_dict, dtype, cfg, self.device, edge_layout=layout)
+        init_layout = self.lib.di_blob_layout(1, _DI_DT[dtype])
+        if layout not in (16, 32) or layout != self.lib.di_blob_layout(3, _DI_DT[dtype]) or init_layout not in (16, 32):
+            raise RuntimeError(f"unexpected blob layouts {layout} / {init_layout}")
+        self.packed = PackedGeoT(state_dict, dtype, cfg, self.device, edge_layout=layout, init_layout=init_layout)
         self._check_blob_sizes()
         self._ws = {}
         self._ws_views = {}
-        # node layer as two launches (di_node_aggregate + di_node_update; equal to the fused
-        # di_node_layer up to fp32 summation order): the segment reduction one wave per
-        # destination at full occupancy instead of inside the MFMA kernel's one-block-per-CU grid
+        # node layer as two launches (di_node_aggregate + di_node_update; bit-identical to the fused
+        # di_node_layer): the segment reduction (16 lanes per destination) at full occupancy instead
+        # of inside the MFMA kernel's one-block-per-CU grid
         self.split_node = True
         # optional side stream for the node embedding (concurrent with InitEdge)
         self.embed_stream = None
         # reference-featurised batches: node embedding as the first blocks of the InitEdge launch
         # (di_embed_init_edge, bf16 or fp32) instead of a separate launch
         self.fuse_embed_init = False
+        # optional stream for the node layers (bench --node-cus: CU-masked to the CUs the pair-tensor
+        # stream does not use); None: the launch stream
+        self.node_stream = None
+        self._ev_edge, self._ev_node = torch.cuda.Event(), torch.cuda.Event()
 
     def _check_blob_sizes(self):
         p, dt = self.packed, _DI_DT[self.dtype]
@@ -230,20 +235,29 @@ class GeoTEngine:
                                          _ptr(None if final else f[nxt]), _ptr(None if final else fn[nxt]),
                                          st), "di_edge_layer")
             nm, nv = p.node[li]
+            ns = st
+            if self.node_stream is not None:
+                # node layer on its own (e.g. CU-masked) stream, ordered between the edge layers
+                self._ev_edge.record(torch.cuda.current_stream())
+                self.node_stream.wait_event(self._ev_edge)
+                ns = ctypes.c_void_p(self.node_stream.cuda_stream)
             if self.split_node:
                 # CSR segment reduction of the attention messages, then O_node / FFN / next Q,K,V
                 tick("node_aggr")
-                _lib.check(lib.di_node_aggregate(g, dt, _ptr(alpha), _ptr(qkv[cur]), _ptr(ws["attn"]), st),
+                _lib.check(lib.di_node_aggregate(g, dt, _ptr(alpha), _ptr(qkv[cur]), _ptr(ws["attn"]), ns),
                            "di_node_aggregate")
                 tick("node_layer_final" if final else "node_layer")
                 _lib.check(lib.di_node_update(g, dt, int(final), _ptr(ws["attn"]), _ptr(h[cur]), _ptr(nm), _ptr(nv),
                                               _ptr(h[nxt]), _ptr(None if final else qkv[nxt]),
-                                              _ptr(ws["hT"] if final else None), st), "di_node_update")
+                                              _ptr(ws["hT"] if final else None), ns), "di_node_update")
             else:
                 tick("node_layer_final" if final else "node_layer")
                 _lib.check(lib.di_node_layer(g, dt, int(final), _ptr(alpha), _ptr(h[cur]), _ptr(qkv[cur]),
                                              _ptr(nm), _ptr(nv), _ptr(h[nxt]), _ptr(None if final else qkv[nxt]),
-                                             _ptr(ws["hT"] if final else None), st), "di_node_layer")
+                                             _ptr(ws["hT"] if final else None), ns), "di_node_layer")
+            if self.node_stream is not None:
+                self._ev_node.record(self.node_stream)
+                torch.cuda.current_stream().wait_event(self._ev_node)
             if not final:
                 f_out = nxt
             cur = nxt

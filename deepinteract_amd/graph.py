@@ -181,6 +181,8 @@ class GraphBatch:
             self.geo_ref = bool(_trusted_geo_ref) and self.num_edges > 0
         elif geo_ref is None:
             self.geo_ref = edge_feats_geo_ref(edge_f)
+        elif geo_ref and self.num_edges == 0:
+            self.geo_ref = False  # no edges: nothing to skip (as the trusted path does)
         elif geo_ref:
             if not edge_feats_geo_ref(edge_f):
                 raise ValueError("geo_ref=True but the edge features do not carry the reference featuriser's "

@@ -113,7 +113,9 @@ class InitEdgeModule(_Base):
 
     def load_reference_state_dict(self, sd):
         full = {f"M.{k}": v for k, v in sd.items()}
-        mat, vec, ps, pd = init_blob(full, self.dtype, p="M", nbr=None)
+        # the fragment order this library build reads for the init blob (kind 1)
+        layout = self.lib.di_blob_layout(1, _DI_DT[self.dtype])
+        mat, vec, ps, pd = init_blob(full, self.dtype, p="M", nbr=None, layout=layout)
         self.blob = tuple(t.to(self.device).contiguous() for t in (mat, vec, ps, pd))
         return self
 

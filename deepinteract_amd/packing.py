@@ -42,6 +42,10 @@ def _np(t):
     return t.detach().cpu().to(torch.float64).numpy()
 
 
+def _bf16_round(x):
+    return torch.from_numpy(np.asarray(x, dtype=np.float64)).to(torch.float32).to(torch.bfloat16).to(torch.float64).numpy()
+
+
 def pad2(w, rows, cols):
     out = np.zeros((rows, cols), dtype=np.float64)
     out[:w.shape[0], :w.shape[1]] = w
@@ -219,10 +223,11 @@ def _geo_rows(w, kind):
 
 
 def init_blob(sd, dtype, p="gnn_module.0.init_edge_module",
-              nbr="gnn_module.0.gt_block.0.conformation_module.nbr_linear"):
+              nbr="gnn_module.0.gt_block.0.conformation_module.nbr_linear", layout=16):
     """nbr=None: no following layer (standalone InitEdgeModule): the fused silu(nbr_linear)
-    output is computed with zero weights and ignored."""
-    bb = BlobBuilder(dtype, IE_NBLK, IEV_N)
+    output is computed with zero weights and ignored. layout: fragment order (16, or 32 for the
+    bf16 32x32x16 InitEdge kernels)."""
+    bb = BlobBuilder(dtype, IE_NBLK, IEV_N, layout)
     sc = _l2e(dtype)  # log2-unit SiLU: geometric projections, combined logits and gates (silu2)
     wc0 = _np(sd[f"{p}.combined_linear_0.weight"])  # [128, 896]
     for t, kind in enumerate(GEO_ORDER):
@@ -251,8 +256,20 @@ def init_blob(sd, dtype, p="gnn_module.0.init_edge_module",
     t_or = GEO_ORDER.index("orient")
     o0 = _np(sd[f"{p}.orient_linear_0.weight"])[:, 3]
     o1 = _np(sd[f"{p}.orient_linear_1.weight"])[:, 3]
-    bb.putv(128, (wc0[:, 256 + 128 * t_or: 384 + 128 * t_or] @ silu(o0)) * sc)
+    orc = (wc0[:, 256 + 128 * t_or: 384 + 128 * t_or] @ silu(o0)) * sc
+    bb.putv(128, orc)
     bb.putv(256, silu(o1) * sc)
+    if layout == 32:
+        # the 32x32 kernels take the orientation constant through the collapsed message map: columns
+        # 28 / 29 (padding of the 28 edge features) hold it as a bf16 hi + lo pair, and the GEO_REF
+        # kernels set geometric features 28 / 29 to 1 (the general path leaves them 0); every other
+        # geometric matrix is zero in those columns
+        hi = _bf16_round(orc)
+        t0 = _geo_rows(wc0[:, 256:384] @ _np(sd[f"{p}.edge_messages_linear_0.weight"]), "edge_messages") * sc
+        t0[:, 28] = hi
+        t0[:, 29] = orc - hi
+        bb.used[0:8] = False
+        bb.put(0, t0)
     mat, vec = bb.finish()
     emb = _np(sd[f"{p}.node_embedding.weight"])
     pos_src = torch.from_numpy(emb @ wc0[:, 0:128].T * sc).to(torch.float32)
@@ -352,25 +369,28 @@ def node_blob(sd, li, final, dtype):
     return bb.finish()
 
 
-# fragment order of the edge-layer blobs the shipped library expects (di_blob_layout(2 / 3, dtype))
+# fragment order of the edge-layer and InitEdge blobs the shipped library expects (di_blob_layout(1 / 2 / 3, dtype))
 EDGE_LAYOUT_DEFAULT = {"bf16": 32, "f32": 16}
 
 
 class PackedGeoT:
     """All device-ready weight blobs of one DGLGeometricTransformer (+ node_in_embedding)."""
 
-    def __init__(self, sd, dtype: str = "f32", cfg: GeoTConfig = GeoTConfig(), device="cpu", edge_layout=None):
-        """edge_layout: fragment order of the edge-layer blobs (the library's di_blob_layout(2, dt));
-        None: this build's default (32 for bf16, 16 for fp32)."""
+    def __init__(self, sd, dtype: str = "f32", cfg: GeoTConfig = GeoTConfig(), device="cpu", edge_layout=None,
+                 init_layout=None):
+        """edge_layout / init_layout: fragment order of the edge-layer / InitEdge blobs (the library's
+        di_blob_layout(2 / 1, dt)); None: this build's default (32 for bf16, 16 for fp32)."""
         assert dtype in ("f32", "bf16")
         if edge_layout is None:
             edge_layout = EDGE_LAYOUT_DEFAULT[dtype]
-        self.dtype, self.cfg, self.edge_layout = dtype, cfg, edge_layout
+        if init_layout is None:
+            init_layout = EDGE_LAYOUT_DEFAULT[dtype]
+        self.dtype, self.cfg, self.edge_layout, self.init_layout = dtype, cfg, edge_layout, init_layout
         L = cfg.num_gnn_layers
         dev = torch.device(device)
         mv = lambda pair: tuple(x.to(dev).contiguous() for x in pair)  # noqa: E731
         self.embed = mv(embed_blob(sd, dtype))
-        im, iv, ps, pd = init_blob(sd, dtype)
+        im, iv, ps, pd = init_blob(sd, dtype, layout=init_layout)
         self.init = mv((im, iv))
         self.pos_src, self.pos_dst = ps.to(dev).contiguous(), pd.to(dev).contiguous()
         self.edge = [mv(edge_blob(sd, li, li == L - 1, dtype, cfg, layout=edge_layout)) for li in range(L)]

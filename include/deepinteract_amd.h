@@ -104,8 +104,8 @@ int di_abi_version(void);
 int64_t di_blob_bytes(int kind, di_dtype dtype, int vec);
 /* MFMA fragment order of a kind's matrix blob in this build (ABI 5): 16 = blocks of 16 output rows
  * x 32 input features (v_mfma_f32_16x16x32_bf16 / 16x16x4_f32 A fragments), 32 = blocks of 32
- * output rows x 16 input features (v_mfma_f32_32x32x16_bf16: the bf16 edge-layer blobs, kinds 2
- * and 3); -1 for an unknown kind or dtype. Both orders hold the same number of 512-element blocks at
+ * output rows x 16 input features (v_mfma_f32_32x32x16_bf16: the bf16 InitEdge and edge-layer
+ * blobs, kinds 1, 2 and 3); -1 for an unknown kind or dtype. Both orders hold the same number of 512-element blocks at
  * the same block offsets (deepinteract_amd/packing.py: pack_matrix / pack_matrix32). */
 int di_blob_layout(int kind, di_dtype dtype);
 
@@ -150,8 +150,8 @@ int di_node_layer(const di_graph* g, di_dtype dt, int final_layer, const float* 
  * (copy_e, sum) + wV / (z + 1e-6), deepinteract_modules.py:93-96, 116):
  *   attn_out[v, :] = sum_{e: dst(e) = v} alpha[e, head] * V[src(e), :] / (sum_e alpha[e, head] + 1e-6)
  * (fp32 [Nt, 128]; V = columns 256..383 of qkv), then O_node + residual + FFN (+ next layer's
- * Q/K/V, + optional transposed copy) from those rows. Equal to di_node_layer up to the fp32
- * summation order of the in-edges (one wave per destination, four interleaved partial sums). */
+ * Q/K/V, + optional transposed copy) from those rows. Bit-identical to di_node_layer: the same
+ * products added one in-edge at a time in edge order (16 lanes per destination). */
 int di_node_aggregate(const di_graph* g, di_dtype dt, const float* alpha /*[Et,4]*/, const void* qkv /*[Nt,384]*/,
                       float* attn_out /*[Nt,128]*/, void* stream);
 int di_node_update(const di_graph* g, di_dtype dt, int final_layer, const float* attn /*[Nt,128]*/,

@@ -45,7 +45,12 @@ class Emu:
         self.u = np.log(2.0) if packed.dtype == "bf16" else 1.0  # silu = silu2 * u
 
     def M(self, blob, off, nout, kin):
-        layout = self.p.edge_layout if any(blob is e for e in self.p.edge) else 16
+        if any(blob is e for e in self.p.edge):
+            layout = self.p.edge_layout
+        elif blob is self.p.init:
+            layout = self.p.init_layout
+        else:
+            layout = 16
         return _unpack(blob[0], off, nout, kin, self.dt, layout)
 
     def geot(self, g):

@@ -34,7 +34,7 @@ def test_abi_version_and_blob_sizes():
     # fragment order (ABI 5): the bf16 edge-layer blobs are packed for v_mfma_f32_32x32x16_bf16
     for kind in range(7):
         assert lib.di_blob_layout(kind, _lib.DI_F32) == 16
-        assert lib.di_blob_layout(kind, _lib.DI_BF16) == (32 if kind in (2, 3) else 16)
+        assert lib.di_blob_layout(kind, _lib.DI_BF16) == (32 if kind in (1, 2, 3) else 16)
     assert lib.di_blob_layout(7, _lib.DI_BF16) == -1 and lib.di_blob_layout(2, 5) == -1
 
 

@@ -117,3 +117,18 @@ def test_init_edge_orientation_constants():
     dirf = torch.zeros(1, 3, dtype=torch.float64)
     assert torch.count_nonzero(F.silu(dirf @ sd64[f"{p}.dir_linear_0.weight"].T)) == 0
     assert torch.count_nonzero(F.silu(dirf @ sd64[f"{p}.dir_linear_1.weight"].T)) == 0
+
+
+def test_geo_ref_claim_on_a_batch_without_edges():
+    """geo_ref=True on a batch with no edges takes the flag as False (nothing to skip), as the
+    package-internal trusted path does, instead of raising."""
+    import torch
+    from deepinteract_amd.graph import GraphBatch
+    n = 4
+    empty = torch.zeros(0, dtype=torch.int32)
+    gb = GraphBatch(empty, empty, torch.zeros(0, 4, dtype=torch.int32), torch.zeros(n, 113), torch.zeros(0, 28),
+                    [n], [0], geo_ref=True)
+    assert gb.geo_ref is False and gb.c_graph.flags == 0
+    trusted = GraphBatch(empty, empty, torch.zeros(0, 4, dtype=torch.int32), torch.zeros(n, 113), torch.zeros(0, 28),
+                         [n], [0], _trusted_geo_ref=True)
+    assert trusted.geo_ref == gb.geo_ref

@@ -153,7 +153,7 @@ def test_blob_sizes_match_layout():
     assert p.pos_src.shape == (2304, 128)
     pb = packing.PackedGeoT(sd, "bf16")
     assert pb.edge[0][0].dtype == torch.bfloat16
-    assert pb.edge_layout == 32 and p.edge_layout == 16
+    assert pb.edge_layout == 32 and p.edge_layout == 16 and pb.init_layout == 32 and p.init_layout == 16
     assert pb.edge[0][0].numel() == sizes[2][0] * 512 and pb.edge[1][0].numel() == sizes[3][0] * 512
 
 

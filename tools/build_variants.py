@@ -17,6 +17,8 @@ VARIANTS = {
     "f32exact": ["DI_F32_FAST_SILU=0"],
     # round 4: the bf16 edge layers on the round-3 16x16x32 kernel (k_edge_lean, 16-row blobs)
     "lean16": ["DI_EDGE_X32=0"],
+    # round 4: the bf16 InitEdge kernels on 16x16x32 (k_init_edge / k_init_edge_res, 16-row blob)
+    "init16": ["DI_INIT_X32=0"],
 }
 # New experiments add their -D knob to csrc (defaulting to the shipped value) and an entry here;
 # round 2's knobs (edge ring / persistent tiles / XCD tile order / DMA pumping / f16 ResBlocks / pair
