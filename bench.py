@@ -370,6 +370,55 @@ class Schedule:
         if prev is not None:
             self._launch_pair(*prev, events=events)
 
+    def capture(self):
+        """The whole step (both streams, every micro-batch) captured once into a HIP graph (torch.cuda.
+        CUDAGraph over hipStreamBeginCapture): the timed region then issues ONE graph launch per step
+        instead of ~10 launches and ~4 event operations per micro-batch. Every kernel still runs on
+        every replay (same inputs, same work). Cross-step slot reuse needs no event: a graph launch
+        starts after the previous one has completed on its stream."""
+        sg = self.geot_streams[0]
+        if len(self.geot_streams) > 1 or self.only or self.overlap == 2:
+            raise SystemExit("--graph supports the default schedule (one GeoT stream, overlap 0/1)")
+        self.done = [None] * self.n_slots
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=sg):
+            self.step()
+            # join the pair stream back into the capturing stream
+            for ev in self.done:
+                if ev is not None:
+                    sg.wait_event(ev)
+        self.done = [None] * self.n_slots
+        return g
+
+    def timed_graph(self, steps, warmup, ws=1):
+        """As timed(), the step replayed from its graph; per-kernel events from one eager step after."""
+        for _ in range(warmup):
+            self.step()
+        torch.cuda.synchronize()
+        g = self.capture()
+        sg = self.geot_streams[0]
+        with torch.cuda.stream(sg):
+            g.replay()
+        torch.cuda.synchronize()
+        barrier(ws)
+        t0 = time.perf_counter()
+        with torch.cuda.stream(sg):
+            for _ in range(steps):
+                g.replay()
+        self.host_issue_s = time.perf_counter() - t0
+        torch.cuda.synchronize()
+        barrier(ws)
+        elapsed = max_over_ranks(ws, time.perf_counter() - t0)
+        events = {}
+        self.step(events, events)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        with torch.cuda.stream(sg):
+            g.replay()
+        self.host_issue_idle_s = time.perf_counter() - t1
+        torch.cuda.synchronize()
+        return elapsed, events
+
     def timed(self, steps, warmup, ws=1, kernel_events="dominant"):
         """(elapsed seconds of `steps` steps, bracketed by barrier + synchronize, max over ranks;
         per-kernel HIP event pairs).
@@ -557,6 +606,9 @@ def main():
                     help="diagnostic (not the metric): run only the GeoT stream or only the pair-tensor stream")
     ap.add_argument("--geo-ref", type=int, default=1, choices=[0, 1],
                     help="0: clear DI_GRAPH_GEO_REF on every batch (the general path; diagnostic)")
+    ap.add_argument("--graph", action="store_true",
+                    help="capture one step (both streams) into a HIP graph and replay it in the timed region; "
+                         "per-kernel events from an eager step after it")
     ap.add_argument("--dist", action="store_true",
                     help="create the RCCL process group even at world size 1 (runs the contact-map "
                          "all-gather record on one GPU)")
@@ -676,11 +728,15 @@ def main():
         if args.node_cus:
             eng.node_stream = masked_stream(dev, cus_rest, num_cus)
     else:
-        s_geot = torch.cuda.current_stream(dev)
+        # graph capture needs a non-default stream
+        s_geot = torch.cuda.Stream(dev) if args.graph else torch.cuda.current_stream(dev)
         s_pair = torch.cuda.Stream(dev) if args.overlap else s_geot
     sch = Schedule(eng, pair, mbs, h1r, h2r, l1, l2, pair_buf, s_geot, s_pair, args.overlap, args.slots,
                    args.geot_streams, args.only)
-    elapsed, events = sch.timed(args.steps, args.warmup, ws, args.kernel_events)
+    if args.graph:
+        elapsed, events = sch.timed_graph(args.steps, args.warmup, ws)
+    else:
+        elapsed, events = sch.timed(args.steps, args.warmup, ws, args.kernel_events)
     total = args.complexes * args.steps * ws
     value = total / elapsed
 
@@ -731,7 +787,8 @@ def main():
                       ("; node embedding on a side stream" if args.embed_stream else ""))
                    + (f"; {args.slots} workspace slots" if args.overlap else "")
                    + (f"; {args.geot_streams} GeoT streams" if args.geot_streams > 1 else "")
-                   + ("; HIP events around every launch in the timed region" if args.kernel_events == "all" else
+                   + ("; step replayed from a HIP graph (kernel events from an untimed eager step)" if args.graph else
+                      "; HIP events around every launch in the timed region" if args.kernel_events == "all" else
                       "; HIP events around the pair-tensor launches only (GeoT kernel events from an untimed step)")
                    + f"; edge-layer kernel {EDGE_KERNEL[args.dtype]}"},
         "host_issue_ms_per_step": round(sch.host_issue_s / args.steps * 1e3, 3),

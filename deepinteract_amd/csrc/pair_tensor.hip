@@ -38,6 +38,11 @@ constexpr int PAIR_THREADS = 256;   // k_pair_vec / k_pair_flat
 constexpr int PAIR_CHUNK = 65536;   // elements per k_pair_vec / k_pair_flat work item
 constexpr int PAIR_UNROLL = 4;
 constexpr int PAIR_INFLIGHT = 3;    // stores in flight per wave when beside GeoT
+// beside GeoT: the partial 128-B lines at row boundaries as plain stores, the rest non-temporal
+// (round 4 experiment; 0 = every store non-temporal, the round-3 form)
+#ifndef DI_PAIR_EDGE_PLAIN
+#define DI_PAIR_EDGE_PLAIN 0
+#endif
 constexpr int PAIR_SEG = 128;       // 16-B chunks per row segment of k_pair_rows (2 per lane)
 constexpr int PAIR_MAX_PLANE_ROWS = 1 << 20;  // k_pair_vec / k_pair_flat row index from an fp32 quotient
 
@@ -217,10 +222,29 @@ void k_pair_rows(const di_pair_desc* __restrict__ descs, int hidden, const T* __
           v0 = __builtin_bit_cast(V, (uintx4){b, b, b, b});
           v1 = v0;
         }
-        if (k0 < nch)
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uintx4, v0), r, k0 * 16, soff, pair_cpol<BESIDE>());
-        if (two && k1 < nch)
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uintx4, v1), r, k1 * 16, soff, pair_cpol<BESIDE>());
+        if constexpr (BESIDE && DI_PAIR_EDGE_PLAIN) {
+          // the row's first / last 128-B line is shared with the neighbouring row when the row does
+          // not start / end on a line: those chunks go out as plain stores (the two halves of the line
+          // merge in L2), every other chunk non-temporal -- nt stores write both halves through
+          const uint32_t rb = (uint32_t)(uintptr_t)o + (uint32_t)soff;  // the row's address (line phase only)
+          const uint32_t head = (128u - (rb & 127u)) & 127u;                    // bytes before the first line boundary
+          const uint32_t tail = (rb + pitch) & 127u;                            // bytes after the last one
+          const bool e0 = (uint32_t)(k0 * 16) < head || (uint32_t)(k0 * 16) >= pitch - tail;
+          const bool e1 = (uint32_t)(k1 * 16) < head || (uint32_t)(k1 * 16) >= pitch - tail;
+          if (k0 < nch && !e0)
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uintx4, v0), r, k0 * 16, soff, 2);
+          if (k0 < nch && e0)
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uintx4, v0), r, k0 * 16, soff, 0);
+          if (two && k1 < nch && !e1)
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uintx4, v1), r, k1 * 16, soff, 2);
+          if (two && k1 < nch && e1)
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uintx4, v1), r, k1 * 16, soff, 0);
+        } else {
+          if (k0 < nch)
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uintx4, v0), r, k0 * 16, soff, pair_cpol<BESIDE>());
+          if (two && k1 < nch)
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uintx4, v1), r, k1 * 16, soff, pair_cpol<BESIDE>());
+        }
         pair_bound<BESIDE>();
       }
     }

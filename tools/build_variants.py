@@ -19,6 +19,8 @@ VARIANTS = {
     "lean16": ["DI_EDGE_X32=0"],
     # round 4: the bf16 InitEdge kernels on 16x16x32 (k_init_edge / k_init_edge_res, 16-row blob)
     "init16": ["DI_INIT_X32=0"],
+    # round 4: pair stores beside GeoT with the row-boundary partial lines as plain stores
+    "pairedge": ["DI_PAIR_EDGE_PLAIN=1"],
 }
 # New experiments add their -D knob to csrc (defaulting to the shipped value) and an entry here;
 # round 2's knobs (edge ring / persistent tiles / XCD tile order / DMA pumping / f16 ResBlocks / pair

@@ -14,7 +14,6 @@ PH="${1:-ab}"
 if [[ "$PH" == *a* ]]; then
 "$R/tools/gpu_run.sh" \
   "pytest_gpu:600:python -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread -p no:cacheprovider" \
-  "t_node2:200:DI_TEST_VARIANT=$R/deepinteract_amd/lib/variants/node2/libdeepinteract_amd.so python -u -m pytest tests/test_gpu_node_aggr.py -q -rf --timeout 180 --timeout-method thread -p no:cacheprovider" \
   "smoke:200:python __graft_entry__.py smoke" \
   "bench:400:python bench.py --steps 20 --warmup 5 > $O/bench.json" \
   "bench_serial:300:python bench.py --overlap 0 --no-cpu > $O/bench_serial.json" \
