@@ -564,8 +564,13 @@ __device__ __forceinline__ void geo_op32(P32<2>& gop, const float* edge_f, int e
 
 // staged weights (one 40-block slot per block, three blocks per CU, as k_init_edge); the first
 // embed_blocks blocks run the node embedding (16x16 k_node_embed arithmetic, kind-0 blob)
+// <= 160 VGPRs (amdgpu_num_vgpr counts register pairs): three waves per SIMD hold 480 of the 512
+// registers, leaving exactly one 32-register pair-tensor wave room beside them. At 161 (168 allocated)
+// the pair kernel's persistent blocks found no SIMD with room while InitEdge ran and the overlapped
+// pair tensor slowed from ~1050 to ~1540 us per micro-batch (round 4)
 template <bool GC>
-__global__ __attribute__((amdgpu_flat_work_group_size(1, InitX32Geo::THREADS), amdgpu_waves_per_eu(3, 3)))
+__global__ __attribute__((amdgpu_flat_work_group_size(1, InitX32Geo::THREADS), amdgpu_waves_per_eu(3, 3),
+                          amdgpu_num_vgpr(80)))
 void k_init_x32(InitArgs a, EmbedArgs ea, int embed_blocks) {
   using G = InitGeo<BF16T>;
   static_assert(G::NW == InitX32Geo::NW, "one LDS slot layout for both block kinds");

@@ -21,6 +21,8 @@ VARIANTS = {
     "init16": ["DI_INIT_X32=0"],
     # round 4: pair stores beside GeoT with the row-boundary partial lines as plain stores
     "pairedge": ["DI_PAIR_EDGE_PLAIN=1"],
+    # round 4: both InitEdge and the edge layers on 16x16x32 (the round-3 kernels)
+    "x16": ["DI_EDGE_X32=0", "DI_INIT_X32=0"],
 }
 # New experiments add their -D knob to csrc (defaulting to the shipped value) and an entry here;
 # round 2's knobs (edge ring / persistent tiles / XCD tile order / DMA pumping / f16 ResBlocks / pair
