@@ -363,7 +363,10 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* g) {
 // fences between steps, so at most MMA_DEPTH fragments (4 VGPRs each) are live: bounds register
 // pressure for the two-waves-per-SIMD kernels (the compiler otherwise hoists most of a layer's
 // ds_reads). Measured depth 3 / 6 vs 4 (C3, overlapped): 7330 / 7286 vs 7307 complexes/s (noise).
-constexpr int MMA_DEPTH = 4;
+#ifndef DI_MMA_DEPTH
+#define DI_MMA_DEPTH 4
+#endif
+constexpr int MMA_DEPTH = DI_MMA_DEPTH;
 template <int NBO, int NS>
 __device__ __forceinline__ void mma_ring(Act<NBO>& out, const Op<BF16T, NS>& op, const u16* w, int lane) {
   constexpr int G = NBO < 2 ? NBO : 2;

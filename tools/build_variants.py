@@ -23,6 +23,10 @@ VARIANTS = {
     "pairedge": ["DI_PAIR_EDGE_PLAIN=1"],
     # round 4: both InitEdge and the edge layers on 16x16x32 (the round-3 kernels)
     "x16": ["DI_EDGE_X32=0", "DI_INIT_X32=0"],
+    # round 4: k_edge_x32 epilogue density (VALU per MFMA) and fragment prefetch depth
+    "nv4": ["DI_PIPE32_NV=4"],
+    "nv12": ["DI_PIPE32_NV=12"],
+    "depth6": ["DI_MMA_DEPTH=6"],
 }
 # New experiments add their -D knob to csrc (defaulting to the shipped value) and an entry here;
 # round 2's knobs (edge ring / persistent tiles / XCD tile order / DMA pumping / f16 ResBlocks / pair
