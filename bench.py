@@ -649,9 +649,10 @@ def main():
     if args.embed_stream is None:
         args.embed_stream = 1 if args.overlap else 0
     if args.init_kernel is None:
-        # overlapped: InitEdge 157-160 vs 171-173 us per micro-batch beside the pair stream, 7516-7621 vs
-        # 7485-7573 complexes/s (round 3); alone the resident InitEdge after the embedding is as fast
-        args.init_kernel = "fused" if args.overlap else "split"
+        # the node embedding as the first blocks of the InitEdge launch: overlapped InitEdge 157-160 vs
+        # 171-173 us beside the pair stream (round 3); serial (round 4, 32x32 InitEdge) 101 us for both vs
+        # 19 + 108 us (embedding, then the resident InitEdge): 5489 vs 5399 complexes/s
+        args.init_kernel = "fused"
     ws, rank, local = dist_setup(args.dist)
     dev = torch.device("cuda", local)
     if half_cu_pair_grid and args.pair_beside and not args.pair_blocks:

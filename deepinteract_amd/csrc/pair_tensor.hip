@@ -40,6 +40,9 @@ constexpr int PAIR_UNROLL = 4;
 constexpr int PAIR_INFLIGHT = 3;    // stores in flight per wave when beside GeoT
 // beside GeoT: the partial 128-B lines at row boundaries as plain stores, the rest non-temporal
 // (round 4 experiment; 0 = every store non-temporal, the round-3 form)
+#ifndef DI_PAIR_PRIO
+#define DI_PAIR_PRIO 0
+#endif
 #ifndef DI_PAIR_EDGE_PLAIN
 #define DI_PAIR_EDGE_PLAIN 0
 #endif
@@ -191,6 +194,9 @@ void k_pair_rows(const di_pair_desc* __restrict__ descs, int hidden, const T* __
   const int rows_per_item = (int)blockDim.x;  // 64 per wave
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // beside GeoT: the store wave's few instructions (one store per 1 KiB) win the SIMD's issue
+  // arbitration against the co-resident, VALU-dense GeoT waves (round 4 experiment)
+  if constexpr (BESIDE && DI_PAIR_PRIO > 0) __builtin_amdgcn_s_setprio(DI_PAIR_PRIO);
   for (int item = blockIdx.x; item < items; item += gridDim.x) {
     const int rb = item % rblocks;
     const int rest = item / rblocks;

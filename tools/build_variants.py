@@ -21,6 +21,9 @@ VARIANTS = {
     "init16": ["DI_INIT_X32=0"],
     # round 4: pair stores beside GeoT with the row-boundary partial lines as plain stores
     "pairedge": ["DI_PAIR_EDGE_PLAIN=1"],
+    # round 4: pair-store waves at raised issue priority beside GeoT
+    "pprio1": ["DI_PAIR_PRIO=1"],
+    "pprio3": ["DI_PAIR_PRIO=3"],
     # round 4: both InitEdge and the edge layers on 16x16x32 (the round-3 kernels)
     "x16": ["DI_EDGE_X32=0", "DI_INIT_X32=0"],
     # round 4: k_edge_x32 epilogue density (VALU per MFMA) and fragment prefetch depth
