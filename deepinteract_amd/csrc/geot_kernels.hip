@@ -1471,6 +1471,9 @@ void k_edge_lean(EdgeArgs a) {
 #ifndef DI_EDGE_X32
 #define DI_EDGE_X32 1
 #endif
+#ifndef DI_EDGE_PRIO
+#define DI_EDGE_PRIO 0
+#endif
 struct EdgeX32Geo {
   static constexpr int NW = 4, THREADS = 64 * NW, ROWS_PER_WAVE = 32, ROWS = ROWS_PER_WAVE * NW;
 };
@@ -1523,6 +1526,9 @@ void k_edge_x32(EdgeArgs a) {
   constexpr int NS = (FINAL ? EL_NSTAGE_FINAL : EL_NSTAGE) - (GC ? (FINAL ? 2 : 3) : 0);
   __shared__ __attribute__((aligned(16))) char lds[2 * LeanPipe::SLOT_BYTES];
   const int lane = lane_id(), h = lane >> 5;
+  // round 4 experiment: static issue priority for every other block (0 = off)
+  if constexpr (DI_EDGE_PRIO > 0)
+    if (blockIdx.x & 1) __builtin_amdgcn_s_setprio(DI_EDGE_PRIO);
   const int r = blockIdx.x * EdgeX32Geo::ROWS + (threadIdx.x >> 6) * EdgeX32Geo::ROWS_PER_WAVE + (lane & 31);
   const bool valid = r < a.Et;
   const int e = valid ? r : a.Et - 1;

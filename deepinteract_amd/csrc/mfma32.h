@@ -190,6 +190,9 @@ __device__ __forceinline__ void mma32(X32<NBO>& out, const P32<NS>& op, const u1
 // instructions after each MFMA, then the step's LDS fragment read (sched_group_barrier). Block 3's
 // epilogue follows the loop. A 32x32x16 MFMA leaves 24 of its 32 issue cycles to the wave's vector
 // work (MI355X_MICROARCH.md, cycle constants).
+#ifndef DI_PIPE32_LEAD
+#define DI_PIPE32_LEAD 1
+#endif
 #ifndef DI_PIPE32_NV
 #define DI_PIPE32_NV 8
 #endif
@@ -212,11 +215,14 @@ __device__ __forceinline__ void lin32_pipe(X32<4>& out, const P32<NS>& op, const
       if (i + D < N) fr[i % D] = afrag(w, i + D, lane);
     }
     if (ob > 0) epi(ob - 1);
+    // the first DI_PIPE32_LEAD MFMAs of block ob go out before any of epi(ob - 1)'s VALU, which reads
+    // the accumulator block ob - 1's last MFMA is still writing
+    __builtin_amdgcn_sched_group_barrier(0x008, DI_PIPE32_LEAD, 0);  // MFMA
 #pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);             // MFMA
+    for (int s = DI_PIPE32_LEAD; s < NS + DI_PIPE32_LEAD; ++s) {
       __builtin_amdgcn_sched_group_barrier(0x402, DI_PIPE32_NV, 0);  // VALU | TRANS
       __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);             // DS read
+      if (s < NS) __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
     }
     __builtin_amdgcn_sched_barrier(0);
   }

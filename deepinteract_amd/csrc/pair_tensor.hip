@@ -38,11 +38,12 @@ constexpr int PAIR_THREADS = 256;   // k_pair_vec / k_pair_flat
 constexpr int PAIR_CHUNK = 65536;   // elements per k_pair_vec / k_pair_flat work item
 constexpr int PAIR_UNROLL = 4;
 constexpr int PAIR_INFLIGHT = 3;    // stores in flight per wave when beside GeoT
-// beside GeoT: the partial 128-B lines at row boundaries as plain stores, the rest non-temporal
-// (round 4 experiment; 0 = every store non-temporal, the round-3 form)
+// beside GeoT: the store waves' s_setprio (round 4 experiment; 0 = the default priority)
 #ifndef DI_PAIR_PRIO
 #define DI_PAIR_PRIO 0
 #endif
+// beside GeoT: the partial 128-B lines at row boundaries as plain stores, the rest non-temporal
+// (round 4 experiment; 0 = every store non-temporal, the round-3 form)
 #ifndef DI_PAIR_EDGE_PLAIN
 #define DI_PAIR_EDGE_PLAIN 0
 #endif

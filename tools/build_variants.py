@@ -30,6 +30,9 @@ VARIANTS = {
     "nv4": ["DI_PIPE32_NV=4"],
     "nv12": ["DI_PIPE32_NV=12"],
     "depth6": ["DI_MMA_DEPTH=6"],
+    # round 4: epi(ob - 1)'s VALU after 2 of block ob's MFMAs; static s_setprio 1 for odd edge blocks
+    "lead2": ["DI_PIPE32_LEAD=2"],
+    "eprio": ["DI_EDGE_PRIO=1"],
 }
 # New experiments add their -D knob to csrc (defaulting to the shipped value) and an entry here;
 # round 2's knobs (edge ring / persistent tiles / XCD tile order / DMA pumping / f16 ResBlocks / pair
