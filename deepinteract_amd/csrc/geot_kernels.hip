@@ -1102,7 +1102,18 @@ struct LeanStages {
     pipe.issue(W + EL_ORDER[si] * BLK, EL_SIZE[si], vo >= 0 ? V + vo : nullptr, 128);
   }
   __device__ const u16* next() {
+    const u16* w = DI_DIAG_NOSYNC ? pipe.next_nosync() : pipe.next();
+    if (i + 1 < NS) issue(i + 1);
+    ++i;
+    return w;
+  }
+  // next() with the wave's own row loads `ld` issued between the stage barrier and the next stage's
+  // DMA: the barrier's vmcnt(0) does not wait for them, and a later wait for them (vmcnt in order)
+  // does not wait for the DMA issued after them
+  template <class F>
+  __device__ const u16* next(F&& ld) {
     const u16* w = pipe.next();
+    ld();
     if (i + 1 < NS) issue(i + 1);
     ++i;
     return w;
@@ -1474,6 +1485,12 @@ void k_edge_lean(EdgeArgs a) {
 #ifndef DI_EDGE_PRIO
 #define DI_EDGE_PRIO 0
 #endif
+// round 4: the edge row re-reads and the K/Q gathers issued after a stage barrier (one stage early
+// where registers allow: stage 1, the final gate) instead of just before it, so the barrier's
+// vmcnt(0) does not wait for them
+#ifndef DI_X32_ROWLD
+#define DI_X32_ROWLD 0
+#endif
 struct EdgeX32Geo {
   static constexpr int NW = 4, THREADS = 64 * NW, ROWS_PER_WAVE = 32, ROWS = ROWS_PER_WAVE * NW;
 };
@@ -1618,7 +1635,8 @@ void k_edge_x32(EdgeArgs a) {
         for (int k = 0; k < 16; ++k) s.v[b][k] += silu2<true>(y.v[b][k]) * gate.v[b][k];
       pin(s);
     }
-    w = st.next();  // stage 1: upward_proj [4x4] (+ orig_msg_linear bias)
+    if constexpr (DI_X32_ROWLD) w = st.next([&] { fr.load(f_row, h); });  // stage 1: upward_proj [4x4]
+    else w = st.next();  // stage 1: upward_proj [4x4] (+ orig_msg_linear bias)
     {
       P32<4> sop;
       make_op32(sop, s);
@@ -1633,7 +1651,7 @@ void k_edge_x32(EdgeArgs a) {
       }
       pin(x);
     }
-    fr.load(f_row, h);
+    if constexpr (!DI_X32_ROWLD) fr.load(f_row, h);
     w = st.next();  // stage 2: orig_msg_linear(res) + nbr
   }
   {
@@ -1644,12 +1662,17 @@ void k_edge_x32(EdgeArgs a) {
   }
   x32_res_block(x, st, lane, h);
   x32_res_block(x, st, lane, h);
-  fr.load(f_row, h);
-  w = st.next();  // res_connect_linear: x = F + silu(rc(x))
+  if constexpr (DI_X32_ROWLD) {
+    w = st.next([&] { fr.load(f_row, h); });  // res_connect_linear: x = F + silu(rc(x))
+  } else {
+    fr.load(f_row, h);
+    w = st.next();  // res_connect_linear: x = F + silu(rc(x))
+  }
   x32_f_residual(x, w, st.v(), fr, lane, h);
   x32_res_block(x, st, lane, h);
   x32_res_block(x, st, lane, h);
-  w = st.next();  // final geometric gate [4x2]
+  if constexpr (DI_X32_ROWLD) w = st.next([&] { fr.load(f_row, h); });  // final geometric gate [4x2]
+  else w = st.next();  // final geometric gate [4x2]
   {
     X32<4> fg;
     zero(fg);
@@ -1658,15 +1681,22 @@ void k_edge_x32(EdgeArgs a) {
     for (int b = 0; b < 4; ++b) x.v[b] *= fg.v[b];
     pin(x);
   }
-  fr.load(f_row, h);
+  if constexpr (!DI_X32_ROWLD) fr.load(f_row, h);
   w = st.next();  // final_linear: x = F + silu(final(x)) = conformation output
   x32_f_residual(x, w, st.v(), fr, lane, h);
 
   // ---- attention scores (propagate_attention :76-91): head hd = features 32 hd .. 32 hd + 31 = block hd
-  R32<4> kr, qr;  // K[src], Q[dst]: issued before the stage barrier
-  kr.load(qkv + (int64_t)a.src[e] * 3 * HID + HID, h);
-  qr.load(qkv + (int64_t)a.dst[e] * 3 * HID, h);
-  w = st.next();  // edge_feats_projection(BN1e(conf))
+  R32<4> kr, qr;  // K[src], Q[dst]
+  const auto ldkq = [&] {
+    kr.load(qkv + (int64_t)a.src[e] * 3 * HID + HID, h);
+    qr.load(qkv + (int64_t)a.dst[e] * 3 * HID, h);
+  };
+  if constexpr (DI_X32_ROWLD) {
+    w = st.next(ldkq);  // edge_feats_projection(BN1e(conf))
+  } else {
+    ldkq();  // issued before the stage barrier
+    w = st.next();
+  }
   X32<4> p;
   {
     P32<8> xop;
@@ -1699,8 +1729,12 @@ void k_edge_x32(EdgeArgs a) {
     P32<8> pop;
     make_op32(pop, p);
     pin(pop);
-    fr.load(f_row, h);  // O_edge: re-read
-    w = st.next();      // O_edge_feats
+    if constexpr (DI_X32_ROWLD) {
+      w = st.next([&] { fr.load(f_row, h); });  // O_edge_feats (+ the edge row re-read)
+    } else {
+      fr.load(f_row, h);  // O_edge: re-read
+      w = st.next();      // O_edge_feats
+    }
     X32<4> e1;
     init_vec32_lds(e1, st.v(), h);
     mma32<4, 8>(e1, pop, w, lane);

@@ -151,9 +151,13 @@ __device__ __forceinline__ void settle(const R32<NB>& r) {
   for (int i = 0; i < 4 * NB; ++i) asm volatile("" ::"v"(r.u[i].x), "v"(r.u[i].y));
 }
 
+// DI_DIAG_NOSILU (timing diagnostic only, wrong results): the block activation as a plain multiply
+#ifndef DI_DIAG_NOSILU
+#define DI_DIAG_NOSILU 0
+#endif
 __device__ __forceinline__ void silu2_blk(floatx16& v) {
 #pragma unroll
-  for (int k = 0; k < 16; ++k) v[k] = silu2<true>(v[k]);
+  for (int k = 0; k < 16; ++k) v[k] = DI_DIAG_NOSILU ? v[k] * 0.5f : silu2<true>(v[k]);
 }
 __device__ __forceinline__ void silu_blk(floatx16& v) {
 #pragma unroll

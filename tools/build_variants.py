@@ -33,6 +33,11 @@ VARIANTS = {
     # round 4: epi(ob - 1)'s VALU after 2 of block ob's MFMAs; static s_setprio 1 for odd edge blocks
     "lead2": ["DI_PIPE32_LEAD=2"],
     "eprio": ["DI_EDGE_PRIO=1"],
+    # round 4: k_edge_x32's row re-reads / K,Q gathers issued after the stage barriers
+    "rowld": ["DI_X32_ROWLD=1"],
+    # timing diagnostics (wrong results; bench only): no SiLU transcendentals / no stage waits
+    "nosilu": ["DI_DIAG_NOSILU=1"],
+    "nosync": ["DI_DIAG_NOSYNC=1"],
 }
 # New experiments add their -D knob to csrc (defaulting to the shipped value) and an entry here;
 # round 2's knobs (edge ring / persistent tiles / XCD tile order / DMA pumping / f16 ResBlocks / pair
