@@ -1535,6 +1535,101 @@ __device__ __forceinline__ void x32_f_residual(X32<4>& x, const u16* w, const fl
   pin(x);
 }
 
+// ---- DI_X32_DEFER (round 4 experiment): each linear's block-3 epilogue deferred under the next
+// linear's first MFMAs (lin32_pipe_d). The chain carries x with block 3 pending: pa = the last
+// linear's raw block-3 accumulator, PK = what is owed to x.v[3] --
+//   0 nothing; 1 x.v[3] += ln2 * silu2(pa) (ResBlock); 2 x.v[3] = F + ln2 * silu2(pa) (F residual).
+#ifndef DI_X32_DEFER
+#define DI_X32_DEFER 0
+#endif
+template <int PK>
+__device__ __forceinline__ void x32_settle3(X32<4>& x, floatx16& pa, const R32<4>& fr) {
+  if constexpr (PK == 1) {
+    silu2_blk(pa);
+    x.v[3] += silu2_unit<true>() * pa;
+  } else if constexpr (PK == 2) {
+    silu2_blk(pa);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) set_quad(x.v[3], q, unpack4(fr.u[12 + q]) + silu2_unit<true>() * quad(pa, q));
+  }
+}
+
+// x32_res_block with deferred block-3 epilogues: enters owing PK to x.v[3], leaves owing 1
+template <int PK, int NS, bool GC>
+__device__ __forceinline__ void x32_res_block_d(X32<4>& x, floatx16& pa, const R32<4>& fr, LeanStages<NS, GC>& st,
+                                                int lane, int h) {
+  P32<8> op0, op1, op2;
+#pragma unroll
+  for (int b = 0; b < 3; ++b) pack_blk(op0.f[2 * b], op0.f[2 * b + 1], x.v[b]);
+  {
+    const u16* w = st.next();
+    X32<4> t;
+    lin32_pipe_d<8>(
+        t, op0, w, st.v(), lane, h,
+        [&] {
+          x32_settle3<PK>(x, pa, fr);
+          pack_blk(op0.f[6], op0.f[7], x.v[3]);
+        },
+        [&](int b) {
+          silu2_blk(t.v[b]);
+          pack_blk(op1.f[2 * b], op1.f[2 * b + 1], t.v[b]);
+        });
+    pa = t.v[3];
+  }
+  {
+    const u16* w = st.next();
+    X32<4> t;
+    lin32_pipe_d<8>(
+        t, op1, w, st.v(), lane, h,
+        [&] {
+          silu2_blk(pa);
+          pack_blk(op1.f[6], op1.f[7], pa);
+        },
+        [&](int b) {
+          silu2_blk(t.v[b]);
+          pack_blk(op2.f[2 * b], op2.f[2 * b + 1], t.v[b]);
+        });
+    pa = t.v[3];
+  }
+  const u16* w = st.next();
+  X32<4> t;
+  lin32_pipe_d<8>(
+      t, op2, w, st.v(), lane, h,
+      [&] {
+        silu2_blk(pa);
+        pack_blk(op2.f[6], op2.f[7], pa);
+      },
+      [&](int b) {
+        silu2_blk(t.v[b]);
+        x.v[b] += silu2_unit<true>() * t.v[b];
+      });
+  pa = t.v[3];
+}
+
+// x32_f_residual with deferred block-3 epilogues: enters owing PK, leaves owing 2 (fr = the edge's
+// F row, the same row every F residual reads)
+template <int PK>
+__device__ __forceinline__ void x32_f_residual_d(X32<4>& x, floatx16& pa, const u16* w, const float* v,
+                                                 const R32<4>& fr, int lane, int h) {
+  P32<8> op;
+#pragma unroll
+  for (int b = 0; b < 3; ++b) pack_blk(op.f[2 * b], op.f[2 * b + 1], x.v[b]);
+  X32<4> y;
+  lin32_pipe_d<8>(
+      y, op, w, v, lane, h,
+      [&] {
+        x32_settle3<PK>(x, pa, fr);
+        pack_blk(op.f[6], op.f[7], x.v[3]);
+      },
+      [&](int b) {
+        silu2_blk(y.v[b]);
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          set_quad(x.v[b], q, unpack4(fr.u[4 * b + q]) + silu2_unit<true>() * quad(y.v[b], q));
+      });
+  pa = y.v[3];
+}
+
 template <int MODE, bool GC>
 __global__ __attribute__((amdgpu_flat_work_group_size(1, EdgeX32Geo::THREADS), amdgpu_waves_per_eu(2, 2),
                           amdgpu_num_vgpr(120)))
@@ -1660,30 +1755,71 @@ void k_edge_x32(EdgeArgs a) {
     mma32<4, 8>(x, fop, w, lane);
     pin(x);
   }
-  x32_res_block(x, st, lane, h);
-  x32_res_block(x, st, lane, h);
-  if constexpr (DI_X32_ROWLD) {
-    w = st.next([&] { fr.load(f_row, h); });  // res_connect_linear: x = F + silu(rc(x))
-  } else {
-    fr.load(f_row, h);
-    w = st.next();  // res_connect_linear: x = F + silu(rc(x))
-  }
-  x32_f_residual(x, w, st.v(), fr, lane, h);
-  x32_res_block(x, st, lane, h);
-  x32_res_block(x, st, lane, h);
-  if constexpr (DI_X32_ROWLD) w = st.next([&] { fr.load(f_row, h); });  // final geometric gate [4x2]
-  else w = st.next();  // final geometric gate [4x2]
-  {
-    X32<4> fg;
-    zero(fg);
-    mma32<4, 2>(fg, gop, w, lane);
+  if constexpr (DI_X32_DEFER) {
+    floatx16 pa;
+    x32_res_block_d<0>(x, pa, fr, st, lane, h);
+    x32_res_block_d<1>(x, pa, fr, st, lane, h);
+    if constexpr (DI_X32_DEFER == 2) {  // F residuals not deferred
+      x32_settle3<1>(x, pa, fr);
+      lean_fence();  // not hoisted over the chain (would pin 32 registers)
+      fr.load(f_row, h);
+      w = st.next();  // res_connect_linear: x = F + silu(rc(x))
+      x32_f_residual(x, w, st.v(), fr, lane, h);
+      x32_res_block_d<0>(x, pa, fr, st, lane, h);
+    } else {
+      lean_fence();  // not hoisted over the chain (would pin 32 registers)
+      fr.load(f_row, h);
+      w = st.next();  // res_connect_linear: x = F + silu(rc(x))
+      x32_f_residual_d<1>(x, pa, w, st.v(), fr, lane, h);
+      x32_res_block_d<2>(x, pa, fr, st, lane, h);
+    }
+    x32_res_block_d<1>(x, pa, fr, st, lane, h);
+    w = st.next();  // final geometric gate [4x2]
+    {
+      X32<4> fg;
+      zero(fg);
+      mma32<4, 2>(fg, gop, w, lane);
+      x32_settle3<1>(x, pa, fr);
 #pragma unroll
-    for (int b = 0; b < 4; ++b) x.v[b] *= fg.v[b];
-    pin(x);
+      for (int b = 0; b < 4; ++b) x.v[b] *= fg.v[b];
+      pin(x);
+    }
+    lean_fence();  // not hoisted over the chain (would pin 32 registers)
+      fr.load(f_row, h);
+    w = st.next();  // final_linear: x = F + silu(final(x)) = conformation output
+    if constexpr (DI_X32_DEFER == 2) {
+      x32_f_residual(x, w, st.v(), fr, lane, h);
+    } else {
+      x32_f_residual_d<0>(x, pa, w, st.v(), fr, lane, h);
+      x32_settle3<2>(x, pa, fr);
+      pin(x);
+    }
+  } else {
+    x32_res_block(x, st, lane, h);
+    x32_res_block(x, st, lane, h);
+    if constexpr (DI_X32_ROWLD) {
+      w = st.next([&] { fr.load(f_row, h); });  // res_connect_linear: x = F + silu(rc(x))
+    } else {
+      fr.load(f_row, h);
+      w = st.next();  // res_connect_linear: x = F + silu(rc(x))
+    }
+    x32_f_residual(x, w, st.v(), fr, lane, h);
+    x32_res_block(x, st, lane, h);
+    x32_res_block(x, st, lane, h);
+    if constexpr (DI_X32_ROWLD) w = st.next([&] { fr.load(f_row, h); });  // final geometric gate [4x2]
+    else w = st.next();  // final geometric gate [4x2]
+    {
+      X32<4> fg;
+      zero(fg);
+      mma32<4, 2>(fg, gop, w, lane);
+#pragma unroll
+      for (int b = 0; b < 4; ++b) x.v[b] *= fg.v[b];
+      pin(x);
+    }
+    if constexpr (!DI_X32_ROWLD) fr.load(f_row, h);
+    w = st.next();  // final_linear: x = F + silu(final(x)) = conformation output
+    x32_f_residual(x, w, st.v(), fr, lane, h);
   }
-  if constexpr (!DI_X32_ROWLD) fr.load(f_row, h);
-  w = st.next();  // final_linear: x = F + silu(final(x)) = conformation output
-  x32_f_residual(x, w, st.v(), fr, lane, h);
 
   // ---- attention scores (propagate_attention :76-91): head hd = features 32 hd .. 32 hd + 31 = block hd
   R32<4> kr, qr;  // K[src], Q[dst]

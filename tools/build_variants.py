@@ -35,6 +35,8 @@ VARIANTS = {
     "eprio": ["DI_EDGE_PRIO=1"],
     # round 4: k_edge_x32's row re-reads / K,Q gathers issued after the stage barriers
     "rowld": ["DI_X32_ROWLD=1"],
+    # round 4: each linear's block-3 epilogue under the next linear's first MFMAs (k_edge_x32 chain)
+    "defer": ["DI_X32_DEFER=1"],
     # timing diagnostics (wrong results; bench only): no SiLU transcendentals / no stage waits
     "nosilu": ["DI_DIAG_NOSILU=1"],
     "nosync": ["DI_DIAG_NOSYNC=1"],

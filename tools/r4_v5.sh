@@ -4,7 +4,5 @@
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"; cd "$R"
 V=deepinteract_amd/lib/variants
 L() { echo "--lib $V/$1/libdeepinteract_amd.so"; }
-tools/ab.sh 2 "x32|" "pp1|$(L pprio1)" "pp3|$(L pprio3)" "ld2|$(L lead2)" "ep|$(L eprio)" "rl|$(L rowld)" &&
-tools/ab.sh 1 "ns|$(L nosilu)" "ny|$(L nosync)" "nss|--overlap 0 $(L nosilu)" "nys|--overlap 0 $(L nosync)" \
-  "xs|--overlap 0" "pc64|--pair-cus 64 --pair-blocks 64 --pair-waves 8" \
-  "pc96|--pair-cus 96 --pair-blocks 96 --pair-waves 8" "pc64b|--pair-cus 64 --pair-blocks 128 --pair-waves 4 --pair-beside 1"
+tools/ab.sh 2 "x32|" "pp1|$(L pprio1)" "pp3|$(L pprio3)" "ld2|$(L lead2)" "ep|$(L eprio)" "rl|$(L rowld)" "df|$(L defer)" &&
+tools/ab.sh 1 "ns|$(L nosilu)" "ny|$(L nosync)" "pc64|--pair-cus 64 --pair-blocks 64 --pair-waves 8"
