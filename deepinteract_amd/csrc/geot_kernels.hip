@@ -1542,6 +1542,11 @@ __device__ __forceinline__ void x32_f_residual(X32<4>& x, const u16* w, const fl
 #ifndef DI_X32_DEFER
 #define DI_X32_DEFER 0
 #endif
+// the operand blocks a deferred linear has produced (k-steps 0-5; 6-7 come from the next pre())
+__device__ __forceinline__ void pin6(P32<8>& o) {
+#pragma unroll
+  for (int s = 0; s < 6; ++s) asm volatile("" : "+v"(o.f[s]));
+}
 template <int PK>
 __device__ __forceinline__ void x32_settle3(X32<4>& x, floatx16& pa, const R32<4>& fr) {
   if constexpr (PK == 1) {
@@ -1575,6 +1580,7 @@ __device__ __forceinline__ void x32_res_block_d(X32<4>& x, floatx16& pa, const R
           pack_blk(op1.f[2 * b], op1.f[2 * b + 1], t.v[b]);
         });
     pa = t.v[3];
+    pin6(op1);
   }
   {
     const u16* w = st.next();
@@ -1590,6 +1596,7 @@ __device__ __forceinline__ void x32_res_block_d(X32<4>& x, floatx16& pa, const R
           pack_blk(op2.f[2 * b], op2.f[2 * b + 1], t.v[b]);
         });
     pa = t.v[3];
+    pin6(op2);
   }
   const u16* w = st.next();
   X32<4> t;
@@ -1604,6 +1611,8 @@ __device__ __forceinline__ void x32_res_block_d(X32<4>& x, floatx16& pa, const R
         x.v[b] += silu2_unit<true>() * t.v[b];
       });
   pa = t.v[3];
+#pragma unroll
+  for (int b = 0; b < 3; ++b) asm volatile("" : "+v"(x.v[b]));
 }
 
 // x32_f_residual with deferred block-3 epilogues: enters owing PK, leaves owing 2 (fr = the edge's
@@ -1628,6 +1637,8 @@ __device__ __forceinline__ void x32_f_residual_d(X32<4>& x, floatx16& pa, const 
           set_quad(x.v[b], q, unpack4(fr.u[4 * b + q]) + silu2_unit<true>() * quad(y.v[b], q));
       });
   pa = y.v[3];
+#pragma unroll
+  for (int b = 0; b < 3; ++b) asm volatile("" : "+v"(x.v[b]));
 }
 
 template <int MODE, bool GC>
