@@ -1482,6 +1482,9 @@ void k_edge_lean(EdgeArgs a) {
 #ifndef DI_EDGE_X32
 #define DI_EDGE_X32 1
 #endif
+#ifndef DI_DIAG_REREAD0
+#define DI_DIAG_REREAD0 0
+#endif
 #ifndef DI_EDGE_PRIO
 #define DI_EDGE_PRIO 0
 #endif
@@ -1656,6 +1659,8 @@ void k_edge_x32(EdgeArgs a) {
   const bool valid = r < a.Et;
   const int e = valid ? r : a.Et - 1;
   const u16* f_row = reinterpret_cast<const u16*>(a.f_in) + (int64_t)e * HID;
+  // DI_DIAG_REREAD0 (timing diagnostic only, wrong results): the row re-reads from row 0 (L2-resident)
+  const u16* f_rr = DI_DIAG_REREAD0 ? reinterpret_cast<const u16*>(a.f_in) : f_row;
   const u16* qkv = reinterpret_cast<const u16*>(a.qkv);
   LeanPipe pipe(lds);
   LeanStages<NS, GC> st{pipe, reinterpret_cast<const u16*>(a.wmat), a.wvec, 0};
@@ -1741,7 +1746,7 @@ void k_edge_x32(EdgeArgs a) {
         for (int k = 0; k < 16; ++k) s.v[b][k] += silu2<true>(y.v[b][k]) * gate.v[b][k];
       pin(s);
     }
-    if constexpr (DI_X32_ROWLD) w = st.next([&] { fr.load(f_row, h); });  // stage 1: upward_proj [4x4]
+    if constexpr (DI_X32_ROWLD) w = st.next([&] { fr.load(f_rr, h); });  // stage 1: upward_proj [4x4]
     else w = st.next();  // stage 1: upward_proj [4x4] (+ orig_msg_linear bias)
     {
       P32<4> sop;
@@ -1757,7 +1762,7 @@ void k_edge_x32(EdgeArgs a) {
       }
       pin(x);
     }
-    if constexpr (!DI_X32_ROWLD) fr.load(f_row, h);
+    if constexpr (!DI_X32_ROWLD) fr.load(f_rr, h);
     w = st.next();  // stage 2: orig_msg_linear(res) + nbr
   }
   {
@@ -1773,13 +1778,13 @@ void k_edge_x32(EdgeArgs a) {
     if constexpr (DI_X32_DEFER == 2) {  // F residuals not deferred
       x32_settle3<1>(x, pa, fr);
       lean_fence();  // not hoisted over the chain (would pin 32 registers)
-      fr.load(f_row, h);
+      fr.load(f_rr, h);
       w = st.next();  // res_connect_linear: x = F + silu(rc(x))
       x32_f_residual(x, w, st.v(), fr, lane, h);
       x32_res_block_d<0>(x, pa, fr, st, lane, h);
     } else {
       lean_fence();  // not hoisted over the chain (would pin 32 registers)
-      fr.load(f_row, h);
+      fr.load(f_rr, h);
       w = st.next();  // res_connect_linear: x = F + silu(rc(x))
       x32_f_residual_d<1>(x, pa, w, st.v(), fr, lane, h);
       x32_res_block_d<2>(x, pa, fr, st, lane, h);
@@ -1796,7 +1801,7 @@ void k_edge_x32(EdgeArgs a) {
       pin(x);
     }
     lean_fence();  // not hoisted over the chain (would pin 32 registers)
-      fr.load(f_row, h);
+      fr.load(f_rr, h);
     w = st.next();  // final_linear: x = F + silu(final(x)) = conformation output
     if constexpr (DI_X32_DEFER == 2) {
       x32_f_residual(x, w, st.v(), fr, lane, h);
@@ -1809,15 +1814,15 @@ void k_edge_x32(EdgeArgs a) {
     x32_res_block(x, st, lane, h);
     x32_res_block(x, st, lane, h);
     if constexpr (DI_X32_ROWLD) {
-      w = st.next([&] { fr.load(f_row, h); });  // res_connect_linear: x = F + silu(rc(x))
+      w = st.next([&] { fr.load(f_rr, h); });  // res_connect_linear: x = F + silu(rc(x))
     } else {
-      fr.load(f_row, h);
+      fr.load(f_rr, h);
       w = st.next();  // res_connect_linear: x = F + silu(rc(x))
     }
     x32_f_residual(x, w, st.v(), fr, lane, h);
     x32_res_block(x, st, lane, h);
     x32_res_block(x, st, lane, h);
-    if constexpr (DI_X32_ROWLD) w = st.next([&] { fr.load(f_row, h); });  // final geometric gate [4x2]
+    if constexpr (DI_X32_ROWLD) w = st.next([&] { fr.load(f_rr, h); });  // final geometric gate [4x2]
     else w = st.next();  // final geometric gate [4x2]
     {
       X32<4> fg;
@@ -1827,7 +1832,7 @@ void k_edge_x32(EdgeArgs a) {
       for (int b = 0; b < 4; ++b) x.v[b] *= fg.v[b];
       pin(x);
     }
-    if constexpr (!DI_X32_ROWLD) fr.load(f_row, h);
+    if constexpr (!DI_X32_ROWLD) fr.load(f_rr, h);
     w = st.next();  // final_linear: x = F + silu(final(x)) = conformation output
     x32_f_residual(x, w, st.v(), fr, lane, h);
   }
@@ -1877,9 +1882,9 @@ void k_edge_x32(EdgeArgs a) {
     make_op32(pop, p);
     pin(pop);
     if constexpr (DI_X32_ROWLD) {
-      w = st.next([&] { fr.load(f_row, h); });  // O_edge_feats (+ the edge row re-read)
+      w = st.next([&] { fr.load(f_rr, h); });  // O_edge_feats (+ the edge row re-read)
     } else {
-      fr.load(f_row, h);  // O_edge: re-read
+      fr.load(f_rr, h);  // O_edge: re-read
       w = st.next();      // O_edge_feats
     }
     X32<4> e1;

@@ -40,6 +40,7 @@ VARIANTS = {
     # timing diagnostics (wrong results; bench only): no SiLU transcendentals / no stage waits
     "nosilu": ["DI_DIAG_NOSILU=1"],
     "nosync": ["DI_DIAG_NOSYNC=1"],
+    "reread0": ["DI_DIAG_REREAD0=1"],
 }
 # New experiments add their -D knob to csrc (defaulting to the shipped value) and an entry here;
 # round 2's knobs (edge ring / persistent tiles / XCD tile order / DMA pumping / f16 ResBlocks / pair

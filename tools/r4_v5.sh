@@ -5,4 +5,4 @@ R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"; cd "$R"
 V=deepinteract_amd/lib/variants
 L() { echo "--lib $V/$1/libdeepinteract_amd.so"; }
 tools/ab.sh 2 "x32|" "pp1|$(L pprio1)" "pp3|$(L pprio3)" "ld2|$(L lead2)" "ep|$(L eprio)" "rl|$(L rowld)" "df|$(L defer)" &&
-tools/ab.sh 1 "ns|$(L nosilu)" "ny|$(L nosync)" "pc64|--pair-cus 64 --pair-blocks 64 --pair-waves 8"
+tools/ab.sh 1 "ns|$(L nosilu)" "ny|$(L nosync)" "r0|$(L reread0)" "pc64|--pair-cus 64 --pair-blocks 64 --pair-waves 8"
