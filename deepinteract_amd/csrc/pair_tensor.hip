@@ -69,9 +69,14 @@ template <bool BESIDE>
 __device__ __forceinline__ void pair_bound() {
   if constexpr (BESIDE) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PAIR_INFLIGHT) : "memory");
 }
-// CPol bits of the 16-B buffer stores: non-temporal beside GeoT, plain alone
+// CPol bits of the 16-B buffer stores: non-temporal beside GeoT, plain alone. DI_PAIR_CPOL (round 4
+// experiment) replaces the beside value: 16 = sc1, 17 = sc0 sc1, 18 = sc1 nt (sc1 stores drop the
+// line from the XCD's L2 instead of keeping it, MI355X_MICROARCH.md, store flavours)
+#ifndef DI_PAIR_CPOL
+#define DI_PAIR_CPOL 2
+#endif
 template <bool BESIDE>
-constexpr int pair_cpol() { return BESIDE ? 2 : 0; }
+constexpr int pair_cpol() { return BESIDE ? DI_PAIR_CPOL : 0; }
 
 // (row, column) of flat plane position q: the fp32 quotient is within one of q / l2 for
 // q / l2 < 2^20 (PAIR_MAX_PLANE_ROWS) and corrected with two selects; the remainder is exact

@@ -24,6 +24,10 @@ VARIANTS = {
     # round 4: pair-store waves at raised issue priority beside GeoT
     "pprio1": ["DI_PAIR_PRIO=1"],
     "pprio3": ["DI_PAIR_PRIO=3"],
+    # round 4: pair stores beside GeoT as sc1 / sc0 sc1 / sc1 nt (dropped from L2) instead of nt
+    "cpol16": ["DI_PAIR_CPOL=16"],
+    "cpol17": ["DI_PAIR_CPOL=17"],
+    "cpol18": ["DI_PAIR_CPOL=18"],
     # round 4: both InitEdge and the edge layers on 16x16x32 (the round-3 kernels)
     "x16": ["DI_EDGE_X32=0", "DI_INIT_X32=0"],
     # round 4: k_edge_x32 epilogue density (VALU per MFMA) and fragment prefetch depth
