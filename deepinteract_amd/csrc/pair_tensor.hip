@@ -44,6 +44,14 @@ constexpr int PAIR_INFLIGHT = 3;    // stores in flight per wave when beside Geo
 #endif
 // beside GeoT: the partial 128-B lines at row boundaries as plain stores, the rest non-temporal
 // (round 4 experiment; 0 = every store non-temporal, the round-3 form)
+// chain-1 planes as contiguous whole-line runs (round 4 experiment; 0 = row streaming) and the
+// cache policy of those stores beside GeoT
+#ifndef DI_PAIR_C1RUN
+#define DI_PAIR_C1RUN 0
+#endif
+#ifndef DI_PAIR_C1CPOL
+#define DI_PAIR_C1CPOL DI_PAIR_CPOL
+#endif
 #ifndef DI_PAIR_EDGE_PLAIN
 #define DI_PAIR_EDGE_PLAIN 0
 #endif
@@ -218,6 +226,31 @@ void k_pair_rows(const di_pair_desc* __restrict__ descs, int hidden, const T* __
     const bool second = c >= hidden;
     uint32_t hv = 0;  // chain 1: lane l holds the value of row r0 + l
     if (!second && r0 + lane < r1) hv = pair_bcast_bits<T>(h + (d.h1_row + r0 + lane) * hidden + c);
+    if constexpr (DI_PAIR_C1RUN) {
+      // chain 1 (round 4 experiment): the wave's rows as ONE contiguous run of 1-KiB stores, so every
+      // 128-B line inside the run is written whole by one instruction (no row-boundary partial
+      // lines); a store spans at most two rows (pitch >= 1 KiB), whose values come by readlane
+      if (!second && pitch >= 1024u) {  // uniform
+        const uint32_t nr = (uint32_t)(r1 - r0), run = nr * pitch;
+        const int base = (int)((uint32_t)r0 * pitch);
+        uint32_t lo = 0, bnd = pitch;  // first row of the store, run offset where row lo + 1 starts
+        for (uint32_t off = 0; off < run; off += 1024u) {
+          if (bnd <= off) {
+            ++lo;
+            bnd += pitch;
+          }
+          const uint32_t va = (uint32_t)__builtin_amdgcn_readlane((int)hv, (int)lo);
+          const uint32_t vb = lo + 1 < nr ? (uint32_t)__builtin_amdgcn_readlane((int)hv, (int)lo + 1) : va;
+          const uint32_t my = off + 16u * (uint32_t)lane;
+          const uint32_t v = my < bnd ? va : vb;
+          if (my < run)
+            __builtin_amdgcn_raw_buffer_store_b128((uintx4){v, v, v, v}, r, 16 * lane, base + (int)off,
+                                                   BESIDE ? DI_PAIR_C1CPOL : 0);
+          pair_bound<BESIDE>();
+        }
+        continue;
+      }
+    }
     const T* src = hT + (int64_t)(c - hidden) * nrows + d.h2_row;
     for (int seg = 0; seg < nch; seg += PAIR_SEG) {
       const int k0 = seg + lane, k1 = seg + 64 + lane;  // this lane's chunks of the segment

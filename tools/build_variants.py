@@ -28,6 +28,9 @@ VARIANTS = {
     "cpol16": ["DI_PAIR_CPOL=16"],
     "cpol17": ["DI_PAIR_CPOL=17"],
     "cpol18": ["DI_PAIR_CPOL=18"],
+    # round 4: chain-1 pair planes as contiguous whole-line runs (nt / sc1 beside GeoT)
+    "c1run": ["DI_PAIR_C1RUN=1"],
+    "c1run16": ["DI_PAIR_C1RUN=1", "DI_PAIR_C1CPOL=16"],
     # round 4: both InitEdge and the edge layers on 16x16x32 (the round-3 kernels)
     "x16": ["DI_EDGE_X32=0", "DI_INIT_X32=0"],
     # round 4: k_edge_x32 epilogue density (VALU per MFMA) and fragment prefetch depth
