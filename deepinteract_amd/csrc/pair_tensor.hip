@@ -49,6 +49,9 @@ constexpr int PAIR_INFLIGHT = 3;    // stores in flight per wave when beside Geo
 #ifndef DI_PAIR_C1RUN
 #define DI_PAIR_C1RUN 0
 #endif
+#ifndef DI_PAIR_C1BOUND
+#define DI_PAIR_C1BOUND 1
+#endif
 #ifndef DI_PAIR_C1CPOL
 #define DI_PAIR_C1CPOL DI_PAIR_CPOL
 #endif
@@ -246,7 +249,8 @@ void k_pair_rows(const di_pair_desc* __restrict__ descs, int hidden, const T* __
           if (my < run)
             __builtin_amdgcn_raw_buffer_store_b128((uintx4){v, v, v, v}, r, 16 * lane, base + (int)off,
                                                    BESIDE ? DI_PAIR_C1CPOL : 0);
-          pair_bound<BESIDE>();
+          // the bound after every DI_PAIR_C1BOUND-th store (row streaming: after each row's two)
+          if (((off >> 10) + 1) % DI_PAIR_C1BOUND == 0) pair_bound<BESIDE>();
         }
         continue;
       }
