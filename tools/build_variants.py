@@ -33,6 +33,7 @@ VARIANTS = {
     "c1run16": ["DI_PAIR_C1RUN=1", "DI_PAIR_C1CPOL=16"],
     "c1runb2": ["DI_PAIR_C1RUN=1", "DI_PAIR_C1BOUND=2"],
     "c1runb3": ["DI_PAIR_C1RUN=1", "DI_PAIR_C1BOUND=3"],
+    "c1runp3": ["DI_PAIR_C1RUN=1", "DI_PAIR_PRIO=3"],
     # round 4: both InitEdge and the edge layers on 16x16x32 (the round-3 kernels)
     "x16": ["DI_EDGE_X32=0", "DI_INIT_X32=0"],
     # round 4: k_edge_x32 epilogue density (VALU per MFMA) and fragment prefetch depth
