@@ -1499,8 +1499,21 @@ struct EdgeX32Geo {
 };
 
 // x through one ResBlock: two silu2(W . + b) layers packed as the next operand, then x += ln2 * silu2(W . + b)
+// DI_X32_PREFETCH (round 4 experiment): one dword per lane of the edge row (lane l: row l & 31,
+// 128-B line l >> 5) loaded one stage ahead of each re-read, so the row's two lines are back in L2
+// when the re-read comes (the pair stores cycle the XCD L2s in a few us); the value is only kept
+// alive past the next stage barrier, whose vmcnt(0) retires it
+#ifndef DI_X32_PREFETCH
+#define DI_X32_PREFETCH 0
+#endif
+__device__ __forceinline__ uint32_t x32_touch(const u16* f_row, int h) {
+  return *reinterpret_cast<const uint32_t*>(f_row + 64 * h);
+}
+__device__ __forceinline__ void x32_keep(uint32_t v) { asm volatile("" ::"v"(v)); }
+
 template <int NS, bool GC>
-__device__ __forceinline__ void x32_res_block(X32<4>& x, LeanStages<NS, GC>& st, int lane, int h) {
+__device__ __forceinline__ void x32_res_block(X32<4>& x, LeanStages<NS, GC>& st, int lane, int h,
+                                              const u16* touch = nullptr, uint32_t* touched = nullptr) {
   P32<8> op;
   make_op32(op, x);
 #pragma unroll 1
@@ -1516,6 +1529,7 @@ __device__ __forceinline__ void x32_res_block(X32<4>& x, LeanStages<NS, GC>& st,
     pin(op);
   }
   const u16* w = st.next();
+  if (touch) *touched = x32_touch(touch, h);
   X32<4> t;
   lin32_pipe<8>(t, op, w, st.v(), lane, h, [&](int b) {
     silu2_blk(t.v[b]);
@@ -1811,19 +1825,23 @@ void k_edge_x32(EdgeArgs a) {
       pin(x);
     }
   } else {
+    uint32_t pf = 0;
+    constexpr bool PF = DI_X32_PREFETCH;
     x32_res_block(x, st, lane, h);
-    x32_res_block(x, st, lane, h);
+    x32_res_block(x, st, lane, h, PF ? f_rr : nullptr, &pf);
     if constexpr (DI_X32_ROWLD) {
       w = st.next([&] { fr.load(f_rr, h); });  // res_connect_linear: x = F + silu(rc(x))
     } else {
       fr.load(f_rr, h);
       w = st.next();  // res_connect_linear: x = F + silu(rc(x))
     }
+    if constexpr (PF) x32_keep(pf);
     x32_f_residual(x, w, st.v(), fr, lane, h);
     x32_res_block(x, st, lane, h);
     x32_res_block(x, st, lane, h);
     if constexpr (DI_X32_ROWLD) w = st.next([&] { fr.load(f_rr, h); });  // final geometric gate [4x2]
     else w = st.next();  // final geometric gate [4x2]
+    if constexpr (PF) pf = x32_touch(f_rr, h);
     {
       X32<4> fg;
       zero(fg);
@@ -1834,6 +1852,7 @@ void k_edge_x32(EdgeArgs a) {
     }
     if constexpr (!DI_X32_ROWLD) fr.load(f_rr, h);
     w = st.next();  // final_linear: x = F + silu(final(x)) = conformation output
+    if constexpr (PF) x32_keep(pf);
     x32_f_residual(x, w, st.v(), fr, lane, h);
   }
 
@@ -1849,6 +1868,8 @@ void k_edge_x32(EdgeArgs a) {
     ldkq();  // issued before the stage barrier
     w = st.next();
   }
+  uint32_t pfo = 0;
+  if constexpr (DI_X32_PREFETCH && !FINAL) pfo = x32_touch(f_rr, h);
   X32<4> p;
   {
     P32<8> xop;
@@ -1887,6 +1908,7 @@ void k_edge_x32(EdgeArgs a) {
       fr.load(f_rr, h);  // O_edge: re-read
       w = st.next();      // O_edge_feats
     }
+    if constexpr (DI_X32_PREFETCH) x32_keep(pfo);
     X32<4> e1;
     init_vec32_lds(e1, st.v(), h);
     mma32<4, 8>(e1, pop, w, lane);

@@ -47,6 +47,8 @@ VARIANTS = {
     "rowld": ["DI_X32_ROWLD=1"],
     # round 4: each linear's block-3 epilogue under the next linear's first MFMAs (k_edge_x32 chain)
     "defer": ["DI_X32_DEFER=1"],
+    # round 4: the edge row's lines touched one stage ahead of each re-read (L2 prefetch)
+    "pfetch": ["DI_X32_PREFETCH=1"],
     # timing diagnostics (wrong results; bench only): no SiLU transcendentals / no stage waits
     "nosilu": ["DI_DIAG_NOSILU=1"],
     "nosync": ["DI_DIAG_NOSYNC=1"],
