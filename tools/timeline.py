@@ -18,7 +18,8 @@ KINDS = [("k_pair_rows", "pair"), ("k_pair_lines", "pair"), ("k_pair_vec", "pair
          ("k_init_edge", "init"), ("k_node_layer<di::BF16T, false", "node0"), ("k_node_layer<di::BF16T, true", "node1"),
          ("k_node_layer<di::F32T, false", "node0"), ("k_node_layer<di::F32T, true", "node1"),
          ("k_node_aggr", "aggr"), ("k_node_update_ring<false", "node0"), ("k_node_update_ring<true", "node1"),
-         ("k_node_embed", "embed")]
+         ("k_node_embed", "embed"), ("k_edge_x32<0", "edge0"), ("k_edge_x32<1", "edge1"), ("k_init_x32", "init"),
+         ("k_init_res_x32", "init")]
 
 
 def kind(name):
