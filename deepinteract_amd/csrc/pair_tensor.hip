@@ -37,7 +37,10 @@ namespace di {
 constexpr int PAIR_THREADS = 256;   // k_pair_vec / k_pair_flat
 constexpr int PAIR_CHUNK = 65536;   // elements per k_pair_vec / k_pair_flat work item
 constexpr int PAIR_UNROLL = 4;
-constexpr int PAIR_INFLIGHT = 3;    // stores in flight per wave when beside GeoT
+#ifndef DI_PAIR_INFLIGHT
+#define DI_PAIR_INFLIGHT 3
+#endif
+constexpr int PAIR_INFLIGHT = DI_PAIR_INFLIGHT;  // stores in flight per wave when beside GeoT
 // beside GeoT: the store waves' s_setprio (round 4 experiment; 0 = the default priority)
 #ifndef DI_PAIR_PRIO
 #define DI_PAIR_PRIO 0

@@ -34,6 +34,9 @@ VARIANTS = {
     "c1runb2": ["DI_PAIR_C1RUN=1", "DI_PAIR_C1BOUND=2"],
     "c1runb3": ["DI_PAIR_C1RUN=1", "DI_PAIR_C1BOUND=3"],
     "c1runp3": ["DI_PAIR_C1RUN=1", "DI_PAIR_PRIO=3"],
+    # round 4: pair stores in flight per wave beside GeoT (default 3)
+    "infl4": ["DI_PAIR_INFLIGHT=4"],
+    "infl5": ["DI_PAIR_INFLIGHT=5"],
     # round 4: both InitEdge and the edge layers on 16x16x32 (the round-3 kernels)
     "x16": ["DI_EDGE_X32=0", "DI_INIT_X32=0"],
     # round 4: k_edge_x32 epilogue density (VALU per MFMA) and fragment prefetch depth
