@@ -25,6 +25,8 @@ VARIANTS = {
     "pprio1": ["DI_PAIR_PRIO=1"],
     "pprio3": ["DI_PAIR_PRIO=3"],
     # round 4: pair stores beside GeoT as sc1 / sc0 sc1 / sc1 nt (dropped from L2) instead of nt
+    "cpol0": ["DI_PAIR_CPOL=0"],
+    "cpol1": ["DI_PAIR_CPOL=1"],
     "cpol16": ["DI_PAIR_CPOL=16"],
     "cpol17": ["DI_PAIR_CPOL=17"],
     "cpol18": ["DI_PAIR_CPOL=18"],
