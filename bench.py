@@ -300,160 +300,67 @@ def allgather_record(ws, rank, complexes, n_res, k, dev, reps=3, per_rank=4):
             "collective": "all_gather_into_tensor (RCCL), real contact maps tiled to the metric's size"}
 
 
-class Schedule:
-    """The timed unit's schedule over resident micro-batches: GeoT of micro-batch m (compute-bound,
-    stream A) overlapped with the pair-tensor stores of m-1 (HBM-bound, stream B); workspace slots
-    carry the node features between them (slot m % slots).
+class SerialSchedule:
+    """--overlap 0: GeoT and the pair tensor of each micro-batch one after the other on ONE stream
+    (di_pair_tensor, plain stores): the baseline the overlapped schedule is measured against."""
 
-    overlap 0: one stream; 1: pair tensor of m-1 beside GeoT of m; 2: as 1, the pair tensor started
-    once InitEdge of m has been issued."""
-
-    def __init__(self, eng, pair, mbs, h1r, h2r, l1, l2, pair_buf, s_geot, s_pair, overlap, slots=2,
-                 geot_streams=1, only=None):
+    def __init__(self, eng, pair, mbs, h1r, h2r, l1, l2, pair_buf):
         self.eng, self.pair, self.mbs = eng, pair, mbs
         self.h1r, self.h2r, self.l1, self.l2, self.pair_buf = h1r, h2r, l1, l2, pair_buf
-        self.s_pair, self.overlap, self.only = s_pair, overlap, only
-        self.n_slots = slots if overlap else 1
-        dev = eng.device
-        self.geot_streams = [s_geot] + [torch.cuda.Stream(dev) for _ in range(geot_streams - 1)]
-        self.embed_streams = [eng.embed_stream] + [torch.cuda.Stream(dev) if eng.embed_stream is not None else None
-                                                   for _ in range(geot_streams - 1)]
-        if geot_streams > 1 and self.n_slots < 4:
-            raise SystemExit("--geot-streams 2 needs --slots 4 (two GeoT micro-batches + the pair tensor's in flight)")
-        self.done = [None] * self.n_slots  # per slot: event after the pair tensor that last read it
-        self.pair_only_inputs = {}         # --only pair: each slot's GeoT outputs, computed in the warm-up
-        # the cross-stream events, created once and re-recorded (a wait enqueued before a re-record
-        # waits for the record it saw): no event creation on the issue path
-        self.ev_done = [torch.cuda.Event() for _ in range(self.n_slots)]
-        self.ev_ready = [torch.cuda.Event() for _ in range(self.n_slots)]
-        self.ev_after = [torch.cuda.Event() for _ in range(self.n_slots)]
 
-    def _launch_pair(self, h, hT, ready, slot, after=None, events=None):
-        with torch.cuda.stream(self.s_pair):
-            self.s_pair.wait_event(ready)
-            if after is not None:
-                self.s_pair.wait_event(after)
-            self.pair(h, self.h1r, self.h2r, self.l1, self.l2, out=self.pair_buf, events=events, hT=hT)
-            ev = self.ev_done[slot]
-            ev.record(self.s_pair)
-            self.done[slot] = ev
+    def step(self, events=None, geot_events=None):
+        for gb in self.mbs:
+            h, _ = self.eng.forward(gb, clone=False, events=geot_events)
+            self.pair(h, self.h1r, self.h2r, self.l1, self.l2, out=self.pair_buf, events=events, hT=self.eng.last_hT)
 
-    def step(self, events=None, geot_events="same"):
-        if geot_events == "same":
-            geot_events = events
-        eng, prev = self.eng, None
-        for m, gb in enumerate(self.mbs):
-            slot = m % self.n_slots
-            after = self.ev_after[slot] if self.overlap == 2 else None
-            sg = self.geot_streams[m % len(self.geot_streams)]
-            eng.embed_stream = self.embed_streams[m % len(self.geot_streams)]
-            with torch.cuda.stream(sg):
-                if self.done[slot] is not None:
-                    sg.wait_event(self.done[slot])
-                if self.only == "pair" and slot in self.pair_only_inputs:
-                    h, hT = self.pair_only_inputs[slot]
-                else:
-                    h, _ = eng.forward(gb, clone=False, events=geot_events, slot=slot, after_init=after)
-                    hT = eng.last_hT
-                    if self.only == "pair":
-                        self.pair_only_inputs[slot] = (h, hT)
-                ready = self.ev_ready[slot]
-                ready.record(sg)
-            if self.only == "geot":
-                continue
-            if self.overlap == 2:
-                if prev is not None:
-                    self._launch_pair(*prev, after=after, events=events)
-                prev = (h, hT, ready, slot)
-            else:
-                self._launch_pair(h, hT, ready, slot, events=events)
-        if prev is not None:
-            self._launch_pair(*prev, events=events)
+    def finish(self):
+        pass
 
-    def capture(self):
-        """The whole step (both streams, every micro-batch) captured once into a HIP graph (torch.cuda.
-        CUDAGraph over hipStreamBeginCapture): the timed region then issues ONE graph launch per step
-        instead of ~10 launches and ~4 event operations per micro-batch. Every kernel still runs on
-        every replay (same inputs, same work). Cross-step slot reuse needs no event: a graph launch
-        starts after the previous one has completed on its stream."""
-        sg = self.geot_streams[0]
-        if len(self.geot_streams) > 1 or self.only or self.overlap == 2:
-            raise SystemExit("--graph supports the default schedule (one GeoT stream, overlap 0/1)")
-        self.done = [None] * self.n_slots
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, stream=sg):
-            self.step()
-            # join the pair stream back into the capturing stream
-            for ev in self.done:
-                if ev is not None:
-                    sg.wait_event(ev)
-        self.done = [None] * self.n_slots
-        return g
 
-    def timed_graph(self, steps, warmup, ws=1):
-        """As timed(), the step replayed from its graph; per-kernel events from one eager step after."""
-        for _ in range(warmup):
-            self.step()
-        torch.cuda.synchronize()
-        g = self.capture()
-        sg = self.geot_streams[0]
-        with torch.cuda.stream(sg):
-            g.replay()
-        torch.cuda.synchronize()
-        barrier(ws)
-        t0 = time.perf_counter()
-        with torch.cuda.stream(sg):
-            for _ in range(steps):
-                g.replay()
-        self.host_issue_s = time.perf_counter() - t0
-        torch.cuda.synchronize()
-        barrier(ws)
-        elapsed = max_over_ranks(ws, time.perf_counter() - t0)
-        events = {}
-        self.step(events, events)
-        torch.cuda.synchronize()
-        t1 = time.perf_counter()
-        with torch.cuda.stream(sg):
-            g.replay()
-        self.host_issue_idle_s = time.perf_counter() - t1
-        torch.cuda.synchronize()
-        return elapsed, events
+def timed(sch, steps, warmup, ws=1, kernel_events="dominant"):
+    """(elapsed seconds of `steps` steps, bracketed by barrier + synchronize, max over ranks;
+    per-kernel HIP event pairs). The overlapped schedule's drain (finish) is inside the timed region.
 
-    def timed(self, steps, warmup, ws=1, kernel_events="dominant"):
-        """(elapsed seconds of `steps` steps, bracketed by barrier + synchronize, max over ranks;
-        per-kernel HIP event pairs).
-
-        kernel_events "dominant" (default): inside the timed region only the dominant kernel (the
-        pair tensor, on its own stream) is bracketed by HIP events -- its roofline is measured live;
-        every GeoT kernel's event pairs come from one untimed step of the same schedule after it.
-        "all": every launch in the timed region is bracketed (round 1-3 behaviour: 16 extra event
-        records per micro-batch on the issue path)."""
-        for _ in range(warmup):
-            self.step()
-        events = {}
-        barrier(ws)
+    kernel_events "dominant" (default): inside the timed region only the pair-tensor launches are
+    bracketed by HIP events (the overlapped schedule: ONE pair-stream launch per step), so the dominant
+    kernel's roofline is measured live; the GeoT kernels' event pairs come from one untimed step after
+    it. "all": every launch in the timed region is bracketed."""
+    for _ in range(warmup):
+        sch.step()
+    sch.finish()
+    events = {}
+    barrier(ws)
+    torch.cuda.synchronize()
+    c0 = sch.check() if hasattr(sch, "check") else None
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        sch.step(events, events if kernel_events == "all" else None)
+    sch.finish()
+    # host time to issue the timed steps (every launch is asynchronous; includes any wait for room in
+    # the HIP queues, i.e. back-pressure from the GPU)
+    host_issue_s = time.perf_counter() - t0
+    torch.cuda.synchronize()
+    barrier(ws)
+    elapsed = max_over_ranks(ws, time.perf_counter() - t0)
+    c1 = sch.check() if hasattr(sch, "check") else None
+    if kernel_events != "all":
+        sch.step(None, events)
+        sch.finish()
         torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(steps):
-            self.step(events, events if kernel_events == "all" else None)
-        # host time to issue the timed steps (every launch is asynchronous; includes any wait for
-        # room in the HIP queues, i.e. back-pressure from the GPU)
-        self.host_issue_s = time.perf_counter() - t0
-        torch.cuda.synchronize()
-        barrier(ws)
-        elapsed = max_over_ranks(ws, time.perf_counter() - t0)
-        if kernel_events != "all":
-            self.step(None, events)
-            torch.cuda.synchronize()
-        # pure host cost of issuing one step, apart from back-pressure: the same step issued onto idle
-        # streams (drained first), timed to the end of its issue; nothing it issues waits for the GPU
-        # unless a queue fills, so with host_issue_idle_s << elapsed / steps the host never delays a launch
-        torch.cuda.synchronize()
-        t1 = time.perf_counter()
-        self.step()
-        self.host_issue_idle_s = time.perf_counter() - t1
-        torch.cuda.synchronize()
-        return elapsed, events
+    # pure host cost of issuing one step, apart from back-pressure: the same step issued onto idle
+    # streams (drained first), timed to the end of its issue
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    sch.step()
+    host_issue_idle_s = time.perf_counter() - t1
+    sch.finish()
+    torch.cuda.synchronize()
+    queue = None
+    if c0 is not None:
+        sch.check()
+        queue = {"stream_bytes": c1["stream_bytes"] - c0["stream_bytes"], "help_bytes": c1["help_bytes"] - c0["help_bytes"],
+                 "gave_up": c1["gave_up"] - c0["gave_up"]}
+    return elapsed, events, {"host_issue_s": host_issue_s, "host_issue_idle_s": host_issue_idle_s, "queue": queue}
 
 
 def kernel_table(events, nodes, edges, l1l2, esz, dtype, geo_ref):
@@ -499,23 +406,52 @@ def rounded(kern):
     return {n: {kk: round(v, 4) if isinstance(v, float) else v for kk, v in r.items()} for n, r in kern.items()}
 
 
-def make_pair(dev, args):
+def make_schedule(args, eng, mbs, h1r, h2r, l1, l2, tdt, dev, s_geot, s_pair):
+    """The timed unit's schedule: overlapped (pair queue beside GeoT, deepinteract_amd.pipeline) or
+    serial (--overlap 0)."""
+    numel = sum(2 * H * a * b for a, b in zip(l1, l2))
+    if args.overlap:
+        from deepinteract_amd.pipeline import OverlappedSchedule
+        sinks = [torch.empty(numel, dtype=tdt, device=dev) for _ in range(2)]
+        sch = OverlappedSchedule(eng, mbs, h1r, h2r, l1, l2, sinks, s_geot, s_pair, ring=args.ring,
+                                 help_every=args.help_every, stream_blocks=args.pair_blocks,
+                                 stream_waves=args.pair_waves, patience_ms=args.patience_ms,
+                                 jobs_per_launch=args.jobs_per_launch)
+        return sch
     from deepinteract_amd.engine import PairTensorOp
-    if args.pair_cus:
-        return PairTensorOp(dev, kernel=args.pair_kernel, blocks=args.pair_cus, waves_per_block=8)
-    return PairTensorOp(dev, kernel=args.pair_kernel, blocks=args.pair_blocks, waves_per_block=args.pair_waves,
-                        beside=bool(args.pair_beside))
+    pair = PairTensorOp(dev, kernel=args.pair_kernel, blocks=args.pair_blocks, waves_per_block=args.pair_waves)
+    return SerialSchedule(eng, pair, mbs, h1r, h2r, l1, l2, torch.empty(numel, dtype=tdt, device=dev))
+
+
+def pair_bytes_per_launch(sch, info, kern, l1l2):
+    """Algorithmic bytes of one launch of the dominant (pair-tensor) kernel: the overlapped schedule's
+    pair-stream launch covers a step's jobs, of which it writes the bytes the queue counted for it (the
+    help launches on the GeoT stream write the rest); the serial kernel writes one micro-batch."""
+    if info["queue"] is None:
+        return l1l2
+    launches = kern.get("pair_tensor", {}).get("launches", 0)
+    return info["queue"]["stream_bytes"] / launches if launches else None
+
+
+def finish_kernel_table(kern, pair_bytes):
+    rec = kern.get("pair_tensor")
+    if rec is not None:
+        if pair_bytes:
+            rec["bytes_per_launch"] = pair_bytes
+            rec["gbs"] = pair_bytes / (rec["avg_us"] * 1e-6) / 1e9
+        else:
+            rec.pop("gbs", None)
+    return kern
 
 
 def sub_record(what, dtype, geo_ref, complexes, pool_gb, P, M, n_res, k, args, dev, sd, cfg, s_geot, s_pair,
                steps=3, warmup=1):
-    """Supplementary C3 line outside the metric: the same overlapped schedule on `complexes`
-    complexes in `dtype`, with DI_GRAPH_GEO_REF set or cleared on every batch."""
+    """Supplementary C3 line outside the metric: the same schedule on `complexes` complexes in
+    `dtype`, with DI_GRAPH_GEO_REF set or cleared on every batch."""
     from deepinteract_amd.engine import GeoTEngine
     from deepinteract_amd.graph import select_graphs
     eng = GeoTEngine(sd, dtype, cfg, device=dev)
     eng.split_node = args.node_kernel == "split"
-    eng.embed_stream = torch.cuda.Stream(dev) if args.embed_stream else None
     eng.fuse_embed_init = args.init_kernel == "fused"
     mbs = [select_graphs(pool_gb, [2 * ((m * M + j) % P) + s for j in range(M) for s in (0, 1)]).with_geo_ref(geo_ref)
            for m in range(complexes // M)]
@@ -524,12 +460,12 @@ def sub_record(what, dtype, geo_ref, complexes, pool_gb, P, M, n_res, k, args, d
     h2r = [gb0.node_off[2 * j + 1] for j in range(M)]
     tdt = torch.bfloat16 if dtype == "bf16" else torch.float32
     esz = 2 if dtype == "bf16" else 4
-    pair_buf = torch.empty(M * 2 * H * n_res * n_res, dtype=tdt, device=dev)
-    sch = Schedule(eng, make_pair(dev, args), mbs, h1r, h2r, [n_res] * M, [n_res] * M, pair_buf, s_geot, s_pair,
-                   args.overlap, args.slots)
-    elapsed, events = sch.timed(steps, warmup)
+    sch = make_schedule(args, eng, mbs, h1r, h2r, [n_res] * M, [n_res] * M, tdt, dev, s_geot, s_pair)
+    elapsed, events, info = timed(sch, steps, warmup)
     value = complexes * steps / elapsed
-    kern = kernel_table(events, gb0.num_nodes, gb0.num_edges, M * 2 * H * n_res * n_res * esz, esz, dtype, geo_ref)
+    l1l2 = M * 2 * H * n_res * n_res * esz
+    kern = kernel_table(events, gb0.num_nodes, gb0.num_edges, l1l2, esz, dtype, geo_ref)
+    kern = finish_kernel_table(kern, pair_bytes_per_launch(sch, info, kern, l1l2))
     flops_c = algorithmic_flops_per_complex(n_res, n_res, k, args.layers)
     xflops_c = executed_flops_per_complex(n_res, n_res, k, args.layers, geo_ref)
     out = {"what": what, "value": round(value, 2), "unit": "complexes/s", "dtype": dtype,
@@ -539,8 +475,8 @@ def sub_record(what, dtype, geo_ref, complexes, pool_gb, P, M, n_res, k, args, d
            "mfma_frac_of_peak_executed": round(xflops_c * value / (MFMA_PEAK_TFLOPS[dtype] * 1e12), 4),
            "hbm_frac_of_peak": round(algorithmic_bytes_per_complex(n_res, n_res, k, esz) * value / (HBM_PEAK_GBS * 1e9), 4),
            "roofline": roofline_of(kern, dtype), "roofline_geot": roofline_of(kern, dtype, mfma_only=True),
-           "kernels": rounded(kern)}
-    del pair_buf, mbs, sch, eng
+           "pair_queue": info["queue"], "kernels": rounded(kern)}
+    del mbs, sch, eng
     torch.cuda.empty_cache()
     return out
 
@@ -561,25 +497,21 @@ def main():
     ap.add_argument("--no-prologue", action="store_true", help="skip the supplementary fused-head-prologue line")
     ap.add_argument("--no-sub", action="store_true",
                     help="skip the supplementary fp32 and general-path (geo_ref off) C3 sub-records")
-    ap.add_argument("--pair-cus", type=int, default=0,
-                    help="K > 0: pair tensor on a CU-masked stream of K dedicated CUs (K blocks x 8 waves), "
-                         "GeoT on the other CUs (needs --overlap 1)")
-    ap.add_argument("--cu-layout", default="stride", choices=["stride", "contig"])
-    ap.add_argument("--pair-mask", type=int, default=0,
-                    help="K > 0: the pair-tensor stream CU-masked to K CUs (its default grid unchanged), GeoT "
-                         "on every CU; with --node-cus the node layers on a stream masked to the other CUs")
-    ap.add_argument("--node-cus", type=int, default=0, choices=[0, 1],
-                    help="1 (needs --pair-mask): node layers on a stream CU-masked to the CUs the pair stream "
-                         "does not use")
+    ap.add_argument("--overlap", type=int, default=1, choices=[0, 1],
+                    help="1: GeoT on one stream, the pair tensors on the device-queue pair stream beside it "
+                         "(deepinteract_amd.pipeline); 0: both on one stream, one after the other")
     ap.add_argument("--pair-kernel", default="auto", choices=["auto", "lines", "rows", "vector"],
-                    help="pair-tensor kernel (auto: row streaming for 16-B aligned planes, per-vector otherwise)")
-    ap.add_argument("--pair-blocks", type=int, default=0)
-    ap.add_argument("--pair-waves", type=int, default=0, help="waves per pair block (default 4; beside GeoT on CUs/2 blocks)")
-    ap.add_argument("--pair-beside", type=int, default=None, choices=[0, 1],
-                    help="bounded store queue + non-temporal stores (default: 1 when overlapped)")
-    ap.add_argument("--overlap", type=int, default=1, choices=[0, 1, 2],
-                    help="0: one stream; 1: pair tensor of micro-batch m-1 on its own stream beside GeoT of m; "
-                         "2: as 1, started after InitEdge of m")
+                    help="--overlap 0: the per-micro-batch pair-tensor kernel (auto: row streaming)")
+    ap.add_argument("--pair-blocks", type=int, default=0,
+                    help="pair-stream blocks (0: half the CUs; --overlap 0: resident blocks, 0 = one per CU)")
+    ap.add_argument("--pair-waves", type=int, default=0, help="waves per pair block (0: 4)")
+    ap.add_argument("--ring", type=int, default=16, help="hT ring slots of the overlapped schedule")
+    ap.add_argument("--help-every", type=int, default=4,
+                    help="the GeoT stream issues a pair help launch every this many micro-batches")
+    ap.add_argument("--jobs-per-launch", type=int, default=0,
+                    help="micro-batches per pair-stream launch (0: one launch per step)")
+    ap.add_argument("--patience-ms", type=float, default=20.0,
+                    help="a pair-stream wave waits at most this long for a micro-batch's signal")
     ap.add_argument("--config", default="c3", choices=["c3", "c5"],
                     help="c3: the metric's workload (BASELINE configs[2]); c5: the 2x4000-residue, k=30, "
                          "4-layer sizing stress (BASELINE configs[4]; no oracle at N > 2304)")
@@ -589,31 +521,19 @@ def main():
     ap.add_argument("--node-kernel", default=None, choices=["split", "fused"],
                     help="node layer as di_node_aggregate + di_node_update (split) or one di_node_layer (fused). "
                          "Default: fused when overlapped, split otherwise")
-    ap.add_argument("--embed-stream", type=int, default=None, choices=[0, 1],
-                    help="1: node embedding on a side stream, concurrent with InitEdge (default when overlapped)")
-    ap.add_argument("--init-kernel", default=None, choices=["fused", "split"],
+    ap.add_argument("--init-kernel", default="fused", choices=["fused", "split"],
                     help="fused: the node embedding as the first blocks of the InitEdge launch (reference-"
-                         "featurised batches); split: separate launches (the embedding on a side stream when "
-                         "--embed-stream 1). Default: fused when overlapped, split otherwise")
+                         "featurised batches); split: the embedding, then the resident InitEdge")
     ap.add_argument("--kernel-events", default="dominant", choices=["all", "dominant"],
-                    help="HIP events only around the dominant (pair-tensor) kernel in the timed region, the "
-                         "GeoT kernels timed in one untimed step after it (dominant, default), or around "
-                         "every launch in the timed region (all)")
-    ap.add_argument("--geot-streams", type=int, default=1, choices=[1, 2],
-                    help="GeoT streams (2: micro-batches alternate, needs --slots 4)")
-    ap.add_argument("--slots", type=int, default=2, choices=[2, 3, 4], help="GeoT workspace slots when overlapped")
-    ap.add_argument("--only", default=None, choices=["geot", "pair"],
-                    help="diagnostic (not the metric): run only the GeoT stream or only the pair-tensor stream")
+                    help="HIP events only around the pair-tensor launches in the timed region, the GeoT kernels "
+                         "timed in one untimed step after it (dominant, default), or around every launch (all)")
     ap.add_argument("--geo-ref", type=int, default=1, choices=[0, 1],
                     help="0: clear DI_GRAPH_GEO_REF on every batch (the general path; diagnostic)")
-    ap.add_argument("--graph", action="store_true",
-                    help="capture one step (both streams) into a HIP graph and replay it in the timed region; "
-                         "per-kernel events from an eager step after it")
     ap.add_argument("--dist", action="store_true",
                     help="create the RCCL process group even at world size 1 (runs the contact-map "
                          "all-gather record on one GPU)")
-    ap.add_argument("--lib", default=None, help="tuning: a variant build of the HIP library "
-                                                 "(deepinteract_amd.build.build_variant)")
+    ap.add_argument("--lib", default=None, help="a variant build of the HIP library (deepinteract_amd.build."
+                                                 "build_variant; tests and diagnostics)")
     args = ap.parse_args()
     if args.lib:
         from deepinteract_amd import _lib
@@ -634,30 +554,10 @@ def main():
         args.no_cpu = args.no_prologue = args.no_sub = True
     args.layers = args.layers or 2
     args.node_limit = args.node_limit or 2304
-    if args.pair_beside is None:
-        args.pair_beside = 1 if args.overlap and not args.pair_cus else 0
-    half_cu_pair_grid = False
-    if not args.pair_waves:
-        # beside GeoT: 4-wave blocks on half the CUs (every SIMD of such a CU gets one store wave, the
-        # other CUs none: 7482-7800 vs 7344-7740 complexes/s for 2-wave blocks on every CU, round 3);
-        # 4-wave blocks on every CU starve InitEdge
-        args.pair_waves = 4
-        # pair_blocks: half this rank's CUs, set after dist_setup from its own device
-        half_cu_pair_grid = True
     if args.node_kernel is None:
         args.node_kernel = "fused" if args.overlap else "split"
-    if args.embed_stream is None:
-        args.embed_stream = 1 if args.overlap else 0
-    if args.init_kernel is None:
-        # the node embedding as the first blocks of the InitEdge launch: overlapped InitEdge 157-160 vs
-        # 171-173 us beside the pair stream (round 3); serial (round 4, 32x32 InitEdge) 101 us for both vs
-        # 19 + 108 us (embedding, then the resident InitEdge): 5489 vs 5399 complexes/s
-        args.init_kernel = "fused"
     ws, rank, local = dist_setup(args.dist)
     dev = torch.device("cuda", local)
-    if half_cu_pair_grid and args.pair_beside and not args.pair_blocks:
-        # beside GeoT: 4-wave blocks on half of THIS rank's CUs
-        args.pair_blocks = max(1, torch.cuda.get_device_properties(dev).multi_processor_count // 2)
     from deepinteract_amd import synth
     from deepinteract_amd.builder import build_graph_batch
     from deepinteract_amd.config import GeoTConfig
@@ -671,13 +571,7 @@ def main():
     sd = seeded_state_dict(0, cfg, with_head=False)
     eng = GeoTEngine(sd, args.dtype, cfg, device=dev)
     eng.split_node = args.node_kernel == "split"
-    if args.embed_stream:
-        eng.embed_stream = torch.cuda.Stream(dev)
     eng.fuse_embed_init = args.init_kernel == "fused"
-    num_cus = torch.cuda.get_device_properties(dev).multi_processor_count
-    if args.pair_cus and not args.overlap:
-        raise SystemExit("--pair-cus needs --overlap 1 or 2")
-    pair = make_pair(dev, args)
 
     # ---- inputs: a pool of distinct complexes built on the device (kNN + features + ids) ----
     P = min(args.pool, args.complexes)
@@ -714,30 +608,11 @@ def main():
     l2 = [n_res] * M
     tdt = torch.bfloat16 if args.dtype == "bf16" else torch.float32
     esz = 2 if args.dtype == "bf16" else 4
-    pair_buf = torch.empty(M * 2 * H * n_res * n_res, dtype=tdt, device=dev)
 
-    if args.pair_cus:
-        from deepinteract_amd.streams import masked_stream, split_cus
-        cus_pair, cus_geot = split_cus(num_cus, args.pair_cus, args.cu_layout)
-        s_geot = masked_stream(dev, cus_geot, num_cus)
-        s_pair = masked_stream(dev, cus_pair, num_cus)
-    elif args.pair_mask:
-        from deepinteract_amd.streams import masked_stream, split_cus
-        cus_pair, cus_rest = split_cus(num_cus, args.pair_mask, args.cu_layout)
-        s_geot = torch.cuda.current_stream(dev)
-        s_pair = masked_stream(dev, cus_pair, num_cus)
-        if args.node_cus:
-            eng.node_stream = masked_stream(dev, cus_rest, num_cus)
-    else:
-        # graph capture needs a non-default stream
-        s_geot = torch.cuda.Stream(dev) if args.graph else torch.cuda.current_stream(dev)
-        s_pair = torch.cuda.Stream(dev) if args.overlap else s_geot
-    sch = Schedule(eng, pair, mbs, h1r, h2r, l1, l2, pair_buf, s_geot, s_pair, args.overlap, args.slots,
-                   args.geot_streams, args.only)
-    if args.graph:
-        elapsed, events = sch.timed_graph(args.steps, args.warmup, ws)
-    else:
-        elapsed, events = sch.timed(args.steps, args.warmup, ws, args.kernel_events)
+    s_geot = torch.cuda.current_stream(dev)
+    s_pair = torch.cuda.Stream(dev) if args.overlap else s_geot
+    sch = make_schedule(args, eng, mbs, h1r, h2r, l1, l2, tdt, dev, s_geot, s_pair)
+    elapsed, events, info = timed(sch, args.steps, args.warmup, ws, args.kernel_events)
     total = args.complexes * args.steps * ws
     value = total / elapsed
 
@@ -747,10 +622,11 @@ def main():
     nodes, edges = gb0.num_nodes, gb0.num_edges
     l1l2 = sum(2 * H * a * b * esz for a, b in zip(l1, l2))
     kern = kernel_table(events, nodes, edges, l1l2, esz, args.dtype, gb0.geo_ref)
+    kern = finish_kernel_table(kern, pair_bytes_per_launch(sch, info, kern, l1l2))
     # the committed PMC summary was collected on the default workload (C3, micro-batch 8, bf16, the
-    # default kernels): any other shape reports traffic null rather than borrowing those bytes
-    pmc_shape = (args.config, M, n_res, k, args.layers, args.dtype, args.pair_kernel, args.geo_ref) == \
-        ("c3", 8, 1000, 20, 2, "bf16", "auto", 1)
+    # default schedule): any other shape reports traffic null rather than borrowing those bytes
+    pmc_shape = (args.config, M, n_res, k, args.layers, args.dtype, args.overlap, args.geo_ref) == \
+        ("c3", 8, 1000, 20, 2, "bf16", 1, 1)
     roof = roofline_of(kern, args.dtype)
     roof["traffic"] = load_pmc_traffic(roof["kernel"]) if pmc_shape else None
     bytes_c = algorithmic_bytes_per_complex(n_res, n_res, k, esz)
@@ -759,6 +635,20 @@ def main():
     xflops_c = executed_flops_per_complex(n_res, n_res, k, args.layers, gb0.geo_ref)
     mfma_frac = flops_c * value / ws / (MFMA_PEAK_TFLOPS[args.dtype] * 1e12)
     xmfma_frac = xflops_c * value / ws / (MFMA_PEAK_TFLOPS[args.dtype] * 1e12)
+    if args.overlap:
+        streams = (f"GeoT || pair tensor: GeoT on one HIP stream (di_pair_signal after each micro-batch), the "
+                   f"pair tensors on ONE persistent di_pair_stream launch per step on a second stream "
+                   f"({args.pair_blocks or 'CUs/2'} blocks x {args.pair_waves or 4} waves, bounded nt stores, "
+                   f"device-queue tickets), di_pair_help on the GeoT stream every {args.help_every} micro-batches "
+                   f"(hT ring of {args.ring}) and a drain at the end of the timed steps; no host events between "
+                   f"the streams")
+    else:
+        streams = f"1 stream: GeoT then the pair tensor ({args.pair_kernel} kernel) per micro-batch"
+    queue = info["queue"]
+    if queue is not None:
+        tot = queue["stream_bytes"] + queue["help_bytes"]
+        queue = dict(queue, help_fraction=round(queue["help_bytes"] / tot, 4) if tot else None,
+                     pair_rate_GBs=round(tot / elapsed / 1e9, 1), help_launches_per_step=args.complexes // M // args.help_every)
 
     out = {
         "metric": METRIC if args.config == "c3" else METRIC_C5, "value": round(value, 2), "unit": "complexes/s", "n_gpus": ws,
@@ -771,34 +661,20 @@ def main():
                    "complexes_per_gpu_per_step": args.complexes, "micro_batch": M, "residues": [n_res, n_res],
                    "knn": k, "layers": args.layers, "max_num_graph_nodes": args.node_limit,
                    "parallelism": f"complex-sharded dp{ws}",
-                   "streams": ["1 stream", "GeoT || pair-tensor (2 HIP streams)",
-                               "GeoT || pair-tensor (2 HIP streams, pair after InitEdge)"][args.overlap]
-                   + (f"; pair on {args.pair_cus} dedicated CUs ({args.cu_layout}), GeoT on "
-                      f"{num_cus - args.pair_cus}" if args.pair_cus else "")
-                   + (f"; pair stream masked to {args.pair_mask} CUs ({args.cu_layout})"
-                      + ("; node layers masked to the other CUs" if args.node_cus else "") if args.pair_mask else "")
-                   + f"; pair kernel {args.pair_kernel} ({args.pair_waves}-wave blocks"
-                   + (f", {args.pair_blocks} resident" if args.pair_blocks else "")
-                   + (", bounded store queue, nt stores)" if args.pair_beside else ")")
-                   + (f"; DIAGNOSTIC: {args.only} stream only (not the metric)" if args.only else "")
+                   "streams": streams
                    + ("" if args.geo_ref else "; DI_GRAPH_GEO_REF cleared (general path)")
                    + f"; node layer {args.node_kernel}"
                    + ("; node embedding as the first blocks of the InitEdge launch"
-                      if args.init_kernel == "fused" and args.geo_ref else
-                      ("; node embedding on a side stream" if args.embed_stream else ""))
-                   + (f"; {args.slots} workspace slots" if args.overlap else "")
-                   + (f"; {args.geot_streams} GeoT streams" if args.geot_streams > 1 else "")
-                   + ("; step replayed from a HIP graph (kernel events from an untimed eager step)" if args.graph else
-                      "; HIP events around every launch in the timed region" if args.kernel_events == "all" else
+                      if args.init_kernel == "fused" and args.geo_ref else "")
+                   + ("; HIP events around every launch in the timed region" if args.kernel_events == "all" else
                       "; HIP events around the pair-tensor launches only (GeoT kernel events from an untimed step)")
                    + f"; edge-layer kernel {EDGE_KERNEL[args.dtype]}"},
-        # pure host cost of issuing one step (every launch and event of the step issued onto drained
-        # streams, to the end of its issue): the GPU cannot wait for the host while this stays well
-        # below ms_per_step
-        "host_issue_ms_per_step": round(sch.host_issue_idle_s * 1e3, 3),
+        # pure host cost of issuing one step (every launch of the step issued onto drained streams, to
+        # the end of its issue): the GPU cannot wait for the host while this stays well below ms_per_step
+        "host_issue_ms_per_step": round(info["host_issue_idle_s"] * 1e3, 3),
         # the timed loop's issue time per step; it includes waiting for room in the HIP queues
         # (back-pressure from the GPU), so on a long run it approaches ms_per_step by construction
-        "host_issue_timed_region_ms_per_step": round(sch.host_issue_s / args.steps * 1e3, 3),
+        "host_issue_timed_region_ms_per_step": round(info["host_issue_s"] / args.steps * 1e3, 3),
         "hbm_frac_of_peak": round(hbm_frac, 4),
         "mfma_frac_of_peak": round(mfma_frac, 4),
         "mfma_frac_of_peak_executed": round(xmfma_frac, 4),
@@ -806,6 +682,7 @@ def main():
                                     "mfma_peak_tflops": MFMA_PEAK_TFLOPS[args.dtype], "hbm_peak_gbs": HBM_PEAK_GBS},
         "roofline": roof,
         "roofline_geot": roofline_of(kern, args.dtype, mfma_only=True) if any("tflops" in r for r in kern.values()) else None,
+        "pair_queue": queue,
         "kernels": rounded(kern),
         "builder": {"complexes": P, "build_s": round(t_build, 4), "ms_per_complex": round(t_build / P * 1e3, 3),
                     "cold_build_s": round(t_builds[0], 4),
@@ -816,11 +693,11 @@ def main():
         out["head_prologue"] = prologue
     if gather is not None:
         out["contact_map_allgather"] = gather
-    if not args.no_sub and args.config == "c3" and not args.only and not args.pair_cus:
+    if not args.no_sub and args.config == "c3":
         # supplementary C3 lines outside the metric (same schedule and kernels): the reference's
         # precision (fp32, deepinteract_utils.py:1088) and the general path with the neighbour-edge
         # gathers live (DI_GRAPH_GEO_REF cleared, deepinteract_modules.py:384-418)
-        del pair_buf, sch
+        del sch
         torch.cuda.empty_cache()
         out["sub_records"] = [
             sub_record("fp32 C3 (the reference's precision), same schedule", "f32", True, 128, pool_gb, P, M,

@@ -39,7 +39,17 @@ class DiPairLaunch(ctypes.Structure):
 
 
 DI_PAIR_AUTO, DI_PAIR_ROWS, DI_PAIR_VECTOR, DI_PAIR_LINES = 0, 1, 2, 3
-ABI_VERSION = 5
+ABI_VERSION = 6
+
+
+class DiPairJob(ctypes.Structure):
+    _fields_ = [("hT", ctypes.c_void_p), ("descs", ctypes.c_void_p), ("out", ctypes.c_void_p),
+                ("num_rows", ctypes.c_int32), ("num_complexes", ctypes.c_int32), ("max_l1", ctypes.c_int32),
+                ("items", ctypes.c_int32)]
+
+
+# pair-queue words (include/deepinteract_amd.h, di_pair_queue_bytes)
+PQ_READY, PQ_ERROR, PQ_GAVE_UP, PQ_SBYTES, PQ_HBYTES = 0, 32, 33, 40, 42
 
 
 _P = ctypes.c_void_p
@@ -48,10 +58,10 @@ _SIGS = {
     "di_abi_version": ([], ctypes.c_int),
     "di_blob_bytes": ([ctypes.c_int, ctypes.c_int, ctypes.c_int], ctypes.c_int64),
     "di_blob_layout": ([ctypes.c_int, ctypes.c_int], ctypes.c_int),
-    "di_node_embed": ([ctypes.POINTER(DiGraph), _I, _I, _P, _P, _P, _P, _P, _P], ctypes.c_int),
+    "di_node_embed": ([ctypes.POINTER(DiGraph), _I, _I, _P, _P, _P, _P, _P, _P, _I, _P], ctypes.c_int),
     "di_init_edge": ([ctypes.POINTER(DiGraph), _I, _P, _P, _P, _P, _P, _P, _P, _P], ctypes.c_int),
     "di_init_edge_resident": ([ctypes.POINTER(DiGraph), _P, _P, _P, _P, _P, _P, _P], ctypes.c_int),
-    "di_embed_init_edge": ([ctypes.POINTER(DiGraph), _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
+    "di_embed_init_edge": ([ctypes.POINTER(DiGraph), _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _P],
                            ctypes.c_int),
     "di_edge_layer": ([ctypes.POINTER(DiGraph), _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
                       ctypes.c_int),
@@ -60,6 +70,11 @@ _SIGS = {
     "di_node_update": ([ctypes.POINTER(DiGraph), _I, _I, _P, _P, _P, _P, _P, _P, _P, _P], ctypes.c_int),
     "di_pair_tensor": ([_I, _P, _I, _I, _I, _I, _I, _P, _P, _I, ctypes.POINTER(DiPairLaunch), _P, _P], ctypes.c_int),
     "di_pair_tensor_check": ([_I, _I, _I, _I, _I, ctypes.POINTER(DiPairLaunch)], ctypes.c_int),
+    "di_pair_queue_bytes": ([_I], ctypes.c_int64),
+    "di_pair_job_items": ([_I, _I, _I], ctypes.c_int32),
+    "di_pair_signal": ([_P, _I, _P], ctypes.c_int),
+    "di_pair_stream": ([_I, _P, _I, _I, _I, _P, ctypes.POINTER(DiPairLaunch), ctypes.c_float, _P], ctypes.c_int),
+    "di_pair_help": ([_I, _P, _I, _I, _I, _P, ctypes.POINTER(DiPairLaunch), _I, _P], ctypes.c_int),
     "di_head_prologue": ([_I, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, ctypes.c_float, _P, _P, _P],
                          ctypes.c_int),
     "di_head_prologue_work_bytes": ([_I, _I, _I, _I], ctypes.c_int64),

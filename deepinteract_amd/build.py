@@ -8,6 +8,7 @@ from __future__ import annotations
 
 import concurrent.futures as cf
 import glob
+import json
 import os
 import subprocess
 import sys
@@ -28,14 +29,33 @@ def _sources():
 
 def _deps():
     return _sources() + sorted(glob.glob(os.path.join(CSRC, "*.h"))) + \
-        [os.path.join(os.path.dirname(HERE), "include", "deepinteract_amd.h")]
+        [os.path.join(os.path.dirname(HERE), "include", "deepinteract_amd.h"), os.path.abspath(__file__)]
+
+
+def _stamp(defines=(), link_flags=()) -> str:
+    """What a build of the library depends on besides the sources' contents: compiler, flags, arch,
+    the -D defines of a variant and the link flags (written next to every built library)."""
+    return json.dumps({"hipcc": HIPCC, "cflags": CFLAGS, "arch": ARCH, "defines": list(defines),
+                       "link": list(link_flags)}, sort_keys=True)
+
+
+def _fresh(lib_path: str, defines=(), link_flags=()) -> bool:
+    """lib_path exists, is newer than every source / header / this file, and was built with the
+    same compiler, flags and defines (its .stamp file)."""
+    if not os.path.exists(lib_path):
+        return False
+    try:
+        with open(lib_path + ".stamp") as fh:
+            if fh.read() != _stamp(defines, link_flags):
+                return False
+    except OSError:
+        return False
+    t = os.path.getmtime(lib_path)
+    return all(os.path.getmtime(p) <= t for p in _deps())
 
 
 def up_to_date() -> bool:
-    if not os.path.exists(LIB):
-        return False
-    t = os.path.getmtime(LIB)
-    return all(os.path.getmtime(p) <= t for p in _deps())
+    return _fresh(LIB)
 
 
 # Host-side AddressSanitizer + UndefinedBehaviorSanitizer build of the C ABI (argument validation,
@@ -55,11 +75,11 @@ def asan_runtime() -> str:
     return cands[-1]
 
 
+SAN_LINK = ["-fsanitize=address", "-fsanitize=undefined", "-shared-libsan"]
+
+
 def build_host_sanitized(force: bool = False) -> str:
-    if not force and os.path.exists(SAN_LIB) and all(os.path.getmtime(p) <= os.path.getmtime(SAN_LIB) for p in _deps()):
-        return SAN_LIB
-    return build(force=True, defines=SAN_FLAGS, out=SAN_LIB,
-                 link_flags=["-fsanitize=address", "-fsanitize=undefined", "-shared-libsan"])
+    return build(force=force, defines=SAN_FLAGS, out=SAN_LIB, link_flags=SAN_LINK)
 
 
 def build(force: bool = False, verbose: bool = True, defines=(), out: str | None = None, link_flags=()) -> str:
@@ -67,11 +87,8 @@ def build(force: bool = False, verbose: bool = True, defines=(), out: str | None
     compiler flags when an entry starts with '-') into its
     own directory, loaded with bench.py --lib <path> (launch-shape knobs compared in one GPU session)."""
     lib_path = out or LIB
-    if not force and not defines and out is None and up_to_date():
-        return LIB
-    if not force and out is not None and os.path.exists(out) and \
-            all(os.path.getmtime(p) <= os.path.getmtime(out) for p in _deps()):
-        return out  # a variant (fixed defines per output path) newer than every source
+    if not force and _fresh(lib_path, defines, link_flags):
+        return lib_path
     objdir = os.path.join(os.path.dirname(lib_path), "obj")
     os.makedirs(objdir, exist_ok=True)
     objs = []
@@ -90,6 +107,8 @@ def build(force: bool = False, verbose: bool = True, defines=(), out: str | None
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed:\n{r.stderr}")
+    with open(lib_path + ".stamp", "w") as fh:
+        fh.write(_stamp(defines, link_flags))
     if verbose:
         print(f"built {lib_path}", file=sys.stderr)
     return lib_path

@@ -362,16 +362,8 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* g) {
 // A fragments read MMA_DEPTH MFMAs ahead of their use through a register ring, with scheduling
 // fences between steps, so at most MMA_DEPTH fragments (4 VGPRs each) are live: bounds register
 // pressure for the two-waves-per-SIMD kernels (the compiler otherwise hoists most of a layer's
-// ds_reads). Measured depth 3 / 6 vs 4 (C3, overlapped): 7330 / 7286 vs 7307 complexes/s (noise).
-// DI_DIAG_NOSYNC (timing diagnostic only, wrong results): the edge kernels' stage switches without
-// the DMA wait and barrier (LeanStages::next)
-#ifndef DI_DIAG_NOSYNC
-#define DI_DIAG_NOSYNC 0
-#endif
-#ifndef DI_MMA_DEPTH
-#define DI_MMA_DEPTH 4
-#endif
-constexpr int MMA_DEPTH = DI_MMA_DEPTH;
+// ds_reads). Measured depth 3 / 6 vs 4 (C3, overlapped; rounds 2 and 4): noise.
+constexpr int MMA_DEPTH = 4;
 template <int NBO, int NS>
 __device__ __forceinline__ void mma_ring(Act<NBO>& out, const Op<BF16T, NS>& op, const u16* w, int lane) {
   constexpr int G = NBO < 2 ? NBO : 2;
@@ -526,11 +518,6 @@ struct WPipe {
       lds_dma_wait();
       __syncthreads();
     }
-    return slot_w(cur);
-  }
-  // timing diagnostic only (DI_DIAG_NOSYNC; wrong results): the slot switch without the wait
-  __device__ __forceinline__ const T* next_nosync() {
-    cur ^= 1;
     return slot_w(cur);
   }
   __device__ __forceinline__ const T* w() const { return slot_w(cur); }

@@ -18,6 +18,7 @@
 #include "common.h"
 #include "layout.h"
 #include "mfma32.h"
+#include "pair_queue.h"
 #include "../../include/deepinteract_amd.h"
 
 namespace di {
@@ -30,6 +31,8 @@ struct EmbedArgs {
   const float* wvec;
   void* h_out;
   void* qkv_out;
+  uint32_t* sig_q;  // optional pair queue: raise its READY to sig_job + 1 at launch start (pair_queue.h)
+  int sig_job;
 };
 
 struct InitArgs {
@@ -135,6 +138,7 @@ struct FRow<F32T> {
 using EmbedGeo = KernelGeo<4>;
 template <class DT>
 __global__ __launch_bounds__(EmbedGeo::THREADS) void k_node_embed(EmbedArgs a) {
+  pq_signal_at_start(a.sig_q, a.sig_job);
   using T = typename DT::T;
   __shared__ __attribute__((aligned(16))) T lds[2 * MAT128 * BLK];
   const int lane = lane_id(), g = lane >> 4;
@@ -240,6 +244,7 @@ template <class DT, bool GC>
 __global__ __attribute__((amdgpu_flat_work_group_size(1, InitGeo<DT>::THREADS),
                           amdgpu_waves_per_eu(InitGeo<DT>::WPE, InitGeo<DT>::WPE)))
 void k_init_edge(InitArgs a, EmbedArgs ea, int embed_blocks) {
+  pq_signal_at_start(ea.sig_q, ea.sig_job);
   using T = typename DT::T;
   using G = InitGeo<DT>;
   constexpr bool FAST = DT::kBF16;
@@ -336,115 +341,10 @@ void k_init_edge(InitArgs a, EmbedArgs ea, int embed_blocks) {
   }
 }
 
-// ---------------------------------------------------------------- InitEdge with resident weights
-// bf16, DI_GRAPH_GEO_REF batches without layer-0 Fn rows (the benchmark path): the weight blocks
-// this path reads -- the collapsed message map (8), the dist and amide projections + their
-// combined_linear_0 slices (2 x 40), the em / dist / amide gates (3 x 8) and combined_linear_1/2
-// (16) -- are 128 blocks = 128 KiB, so ONE block per CU loads them into LDS once and its waves then
-// stream 16-edge tiles with no weight stages, no stage barriers and no L2 weight traffic (the
-// staged kernel above re-streams 6 stages per 64 edges and meets its block at every stage barrier).
-// Waves are independent after the load: tile t = wave + k * (total waves). The arithmetic is the
-// same as k_init_edge<BF16T, true> (same operands, same order).
-// 12 waves = 3 per SIMD at 132 VGPRs; 16 waves (<= 128 VGPRs) measured 968 vs 165 us beside the pair
-// stream (the block no longer fits beside the pair kernel's waves)
-constexpr int IR_NW = 12;
+// Resident InitEdge weights (k_init_res_x32): the 128 weight blocks the GEO_REF path reads, at these
+// block offsets of the LDS copy
 constexpr int IR_NBLK = 128;  // resident weight blocks
 constexpr int IR_T0 = 0, IR_DIST = 8, IR_AMIDE = 48, IR_GATE = 88, IR_C = 112;
-using InitResGeo = KernelGeo<IR_NW>;
-__global__ __attribute__((amdgpu_flat_work_group_size(1, InitResGeo::THREADS), amdgpu_waves_per_eu(IR_NW / 4, IR_NW / 4)))
-void k_init_edge_res(InitArgs a, int ntiles) {
-  __shared__ __attribute__((aligned(16))) u16 w[IR_NBLK * BLK];
-  const u16* W = reinterpret_cast<const u16*>(a.wmat);
-  dma_blocks<IR_NW>(w + IR_T0 * BLK, W + IE_T0 * BLK, 8);
-  dma_blocks<IR_NW>(w + IR_DIST * BLK, W + (IE_T0 + 40 * 1) * BLK, 40);
-  dma_blocks<IR_NW>(w + IR_AMIDE * BLK, W + (IE_T0 + 40 * 4) * BLK, 40);
-  dma_blocks<IR_NW>(w + IR_GATE * BLK, W + IE_GEO1 * BLK, 16);               // em1, dist1
-  dma_blocks<IR_NW>(w + (IR_GATE + 16) * BLK, W + (IE_GEO1 + 32) * BLK, 8);  // amide1
-  dma_blocks<IR_NW>(w + IR_C * BLK, W + IE_C1 * BLK, 16);                    // combined_linear_1, _2
-  lds_dma_wait();
-  __syncthreads();
-  const int lane = lane_id(), g = lane >> 4;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  // positional-row indices one tile ahead: the src/dst -> node_pos chain of tile k+1 is issued during
-  // tile k, so a tile's start waits for one gather latency (its two positional rows), not three
-  const int stride = gridDim.x * IR_NW;
-  auto edge_of = [&](int t) {
-    const int r = t * ROWS_PER_WAVE + (lane & 15);
-    return r < a.Et ? r : a.Et - 1;
-  };
-  int tile = blockIdx.x * IR_NW + wave;
-  int ps = 0, pd = 0;
-  if (tile < ntiles) {
-    const int e = edge_of(tile);
-    ps = a.node_pos[a.src[e]];
-    pd = a.node_pos[a.dst[e]];
-  }
-#pragma unroll 1
-  for (; tile < ntiles; tile += stride) {
-    const int r = tile * ROWS_PER_WAVE + (lane & 15);
-    const bool valid = r < a.Et;
-    const int e = valid ? r : a.Et - 1;
-    Act<2> geo;
-    load_edge_geo(geo, a.edge_f + (int64_t)e * NFEAT_E, g);
-    Op<BF16T, 1> gop;
-    make_op(gop, geo);
-    // combined_linear_0 over [emb[src], emb[dst], em0, silu(d0), 0, orient const, silu(a0)]
-    Act<8> acc;
-    load_row(acc, a.pos_src + (int64_t)ps * HID, g);
-    add_row(acc, a.pos_dst + (int64_t)pd * HID, g);
-    add_vec(acc, a.wvec + IEV_ORC, g);
-    const bool more = tile + stride < ntiles;  // uniform
-    int sn = 0, dn = 0;
-    if (more) {
-      const int en = edge_of(tile + stride);
-      sn = a.src[en];
-      dn = a.dst[en];
-    }
-    mma_ring<8, 1>(acc, gop, w + IR_T0 * BLK, lane);
-#pragma unroll 1
-    for (int i = 0; i < 2; ++i) {
-      const u16* wt = w + (i == 0 ? IR_DIST : IR_AMIDE) * BLK;
-      Act<8> y;
-      zero(y);
-      mma_ring<8, 1>(y, gop, wt, lane);
-      silu2_<8, true>(y);
-      Op<BF16T, 4> yop;
-      make_op(yop, y);
-      mma_ring<8, 4>(acc, yop, wt + 8 * BLK, lane);
-    }
-    if (more) {  // the next tile's positional-row indices, from ids loaded a stage ago
-      ps = a.node_pos[sn];
-      pd = a.node_pos[dn];
-    }
-    silu2_<8, true>(acc);
-    // gating: (em1 + silu(d1) + 0 + orient const + silu(a1)) * c
-    {
-      Act<8> gs;
-      init_vec(gs, a.wvec + IEV_OGATE, g);
-#pragma unroll 1
-      for (int t = 0; t < 3; ++t) {
-        Act<8> y;
-        zero(y);
-        mma_ring<8, 1>(y, gop, w + (IR_GATE + 8 * t) * BLK, lane);
-        if (t > 0) silu2_<8, true>(y);
-        add_(gs, y);
-      }
-      mul_(acc, gs);
-    }
-    // combined_linear_2(combined_linear_1(.)) : 128 -> 28 (padded 32) -> 128
-    Act<2> z;
-    zero(z);
-    Op<BF16T, 4> aop;
-    make_op(aop, acc);
-    mma_ring<2, 4>(z, aop, w + IR_C * BLK, lane);
-    Act<8> f;
-    zero(f);
-    Op<BF16T, 1> zop;
-    make_op(zop, z);
-    mma_ring<8, 1>(f, zop, w + (IR_C + 8) * BLK, lane);
-    if (valid) store_edge_row(f, reinterpret_cast<u16*>(a.f_out) + (int64_t)e * HID, g);
-  }
-}
 
 // ================================================================ InitEdgeModule on 32x32x16 MFMA (bf16)
 // The arithmetic of k_init_edge<BF16T, GC> on 32-row tiles (csrc/mfma32.h): every 128-wide stage is
@@ -457,9 +357,6 @@ void k_init_edge_res(InitArgs a, int ntiles) {
 //   T0 (collapsed edge-message map, [128x32] 8 blk) -> geometric terms (dist, [dir, orient,] amide:
 //   [128x32] W_t0 + [128x128] combined_linear_0 slice, 40 blk each) -> gates (em1, dist1, [dir1,
 //   orient1,] amide1: [128x32] each) -> combined_linear_1/2 (8 + 8 blk) -> [layer-0 nbr_linear, 32 blk]
-#ifndef DI_INIT_X32
-#define DI_INIT_X32 1
-#endif
 struct InitX32Geo {
   static constexpr int NW = 4, THREADS = 64 * NW, ROWS_PER_WAVE = 32, ROWS = ROWS_PER_WAVE * NW;
 };
@@ -572,6 +469,7 @@ template <bool GC>
 __global__ __attribute__((amdgpu_flat_work_group_size(1, InitX32Geo::THREADS), amdgpu_waves_per_eu(3, 3),
                           amdgpu_num_vgpr(80)))
 void k_init_x32(InitArgs a, EmbedArgs ea, int embed_blocks) {
+  pq_signal_at_start(ea.sig_q, ea.sig_job);
   using G = InitGeo<BF16T>;
   static_assert(G::NW == InitX32Geo::NW, "one LDS slot layout for both block kinds");
   __shared__ __attribute__((aligned(16))) u16 lds[G::CAP * BLK];
@@ -623,7 +521,7 @@ void k_init_x32(InitArgs a, EmbedArgs ea, int embed_blocks) {
 }
 
 // resident weights (DI_GRAPH_GEO_REF, no Fn): the path's 128 blocks loaded once per CU into LDS
-// (layout of k_init_edge_res), one 12-wave block per CU, waves striding over 32-edge tiles with the
+// (block offsets IR_*), one 12-wave block per CU, waves striding over 32-edge tiles with the
 // next tile's src/dst -> node_pos chain issued a tile ahead
 constexpr int IRX_NW = 12;
 __global__ __attribute__((amdgpu_flat_work_group_size(1, 64 * IRX_NW), amdgpu_waves_per_eu(IRX_NW / 4, IRX_NW / 4)))
@@ -703,7 +601,7 @@ constexpr int EL_NSTAGE_CONF = 18, EL_NSTAGE_FINAL = 19, EL_NSTAGE = 25;
 constexpr int EL_CAP = 36;
 
 // k_edge_layer: 16 rows per wave, 4-wave blocks, two blocks per CU: the fp32 edge layers (the
-// reference's precision; double-buffered bf16 is k_edge_lean below) and the conformation module
+// reference's precision; the bf16 layers are k_edge_x32 below) and the conformation module
 // alone (di_conformation, both dtypes).
 template <class DT>
 using EdgePipe = WPipe<typename DT::T, Geo<DT>::NW, Geo<DT>::DBUF, EL_CAP, 128>;
@@ -956,143 +854,18 @@ void k_edge_layer(EdgeArgs a) {
   }
 }
 
-// ================================================================ fused edge layer, grouped form (bf16)
-// The same stage sequence and arithmetic as k_edge_layer<BF16T, 0/1>, with each wave carrying
-// TWO independent 16-row groups through every weight stage (128 rows per 4-wave block and weight
-// pass, so every LDS-DMA'd stage and every stage barrier serves twice the rows of k_edge_layer;
-// two blocks per CU as before). Every LDS A fragment feeds one MFMA per group (mma_ring2: half
-// the ds_reads per row; tools/diag/mfma_shape_bench.hip V1 vs V0: 336 vs 375 us on the bare
-// compute core).
-// Register diet (two waves per SIMD at 240 registers): one tile per block; the edge's own row F
-// is re-read (L2-hot) for each of its uses instead of being held; the dist gate is computed
-// k-step by k-step and multiplied straight into the packed downward_proj operand; the edge FFN
-// accumulates into the residual e1.
-// Measured alternatives (round 2): one group per wave at 2-4 waves per SIMD, 8-wave
-// blocks, single-slot stages at 3-4 blocks per CU, the ResBlocks in packed f16, F held in
-// registers, fragment depth 3 / 6, no scheduling fences -- all slower or equal.
-struct Lean : KernelGeo<4> {
-  static constexpr int LG = 2;  // 16-row groups per wave
-  static constexpr int GROUP_ROWS = ROWS;
-  static constexpr int ROWS_ALL = GROUP_ROWS * LG;
-};
-// Both row groups through one pass over the stage's A fragments: every LDS fragment read feeds
-// one MFMA per group. Both groups' accumulators are live across the loop.
-template <int NBO, int NS>
-__device__ __forceinline__ void mma_ring2(Act<NBO>& o0, Act<NBO>& o1, const Op<BF16T, NS>& a0, const Op<BF16T, NS>& a1,
-                                          const u16* w, int lane) {
-  constexpr int G = NBO < 2 ? NBO : 2;
-  constexpr int N = NBO * NS;
-  constexpr int D = MMA_DEPTH < N ? MMA_DEPTH : N;
-  auto blk = [](int i) { return (i / (G * NS)) * G + (i % G); };
-  auto kst = [](int i) { return (i % (G * NS)) / G; };
-  bf16x8 fr[D];
-#pragma unroll
-  for (int i = 0; i < D; ++i)
-    fr[i] = *reinterpret_cast<const bf16x8*>(w + (blk(i) * NS + kst(i)) * BLK + lane * 8);
-#pragma unroll
-  for (int i = 0; i < N; ++i) {
-    __builtin_amdgcn_sched_barrier(0);
-    const int bo = blk(i), s = kst(i);
-    o0.v[bo] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[i % D], a0.f[s], o0.v[bo], 0, 0, 0);
-    o1.v[bo] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[i % D], a1.f[s], o1.v[bo], 0, 0, 0);
-    if (i + D < N)
-      fr[i % D] = *reinterpret_cast<const bf16x8*>(w + (blk(i + D) * NS + kst(i + D)) * BLK + lane * 8);
-  }
-  __builtin_amdgcn_sched_barrier(0);
-}
-// out[q] (= bias or 0) += W . op[q] for both row groups
-template <int NBO, int NS>
-__device__ __forceinline__ void lin_groups(Act<NBO> (&out)[Lean::LG], const Op<BF16T, NS> (&op)[Lean::LG],
-                                           const u16* w, const float* bias, int lane, int g) {
-#pragma unroll
-  for (int q = 0; q < Lean::LG; ++q) {
-    if (bias) init_vec_lds(out[q], bias, g);
-    else zero(out[q]);
-  }
-  mma_ring2<NBO, NS>(out[0], out[1], op[0], op[1], w, lane);
-}
-// Pipelined form of lin_groups + epilogue, used by every stage with a SiLU: the stage's MFMAs run
-// output-block-pair major, and the epilogue of pair p-1 (SiLU, pack or residual: epi(q, p - 1) for
-// both groups) is issued BETWEEN the 16 MFMAs of pair p -- 4 VALU instructions per MFMA,
-// sched_group_barrier-placed -- so a wave's own SiLU work runs while its MFMAs are in the matrix
-// pipe instead of after them; pair 3's epilogue follows the loop. Measured (C3, round 3, same box):
-// edge layer alone 323 vs 331 us, final 258 vs 267 us; beside the pair stream 423-431 vs 429-437 us;
-// 2 / 3 / 5 VALU per MFMA within noise of 4. The gain is small because the edge layers are bound by
-// the SIMD's issue of SiLU VALU work (v_exp / v_rcp at 8 cycles) plus the MFMA's issue hold, not
-// by the two failing to overlap (tools/diag/silu_overlap_bench.hip).
-constexpr int PIPE_NV = 4;
-template <int NS, class Epi>
-__device__ __forceinline__ void lin_groups_pipe(Act<8> (&out)[Lean::LG], const Op<BF16T, NS> (&op)[Lean::LG],
-                                                const u16* w, const float* bias, int lane, int g, Epi&& epi) {
-  constexpr int NBO = 8, G = 2, N = NBO * NS, D = MMA_DEPTH < N ? MMA_DEPTH : N;
-  constexpr int PSTEPS = G * NS;  // fragment steps per output-block pair
-#pragma unroll
-  for (int q = 0; q < Lean::LG; ++q) {
-    if (bias) init_vec_lds(out[q], bias, g);
-    else zero(out[q]);
-  }
-  auto blk = [](int i) { return (i / (G * NS)) * G + (i % G); };
-  auto kst = [](int i) { return (i % (G * NS)) / G; };
-  bf16x8 fr[D];
-#pragma unroll
-  for (int i = 0; i < D; ++i)
-    fr[i] = *reinterpret_cast<const bf16x8*>(w + (blk(i) * NS + kst(i)) * BLK + lane * 8);
-  __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-  for (int p = 0; p < NBO / G; ++p) {
-#pragma unroll
-    for (int j = 0; j < PSTEPS; ++j) {
-      const int i = p * PSTEPS + j;
-      const int bo = blk(i), s = kst(i);
-      out[0].v[bo] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[i % D], op[0].f[s], out[0].v[bo], 0, 0, 0);
-      out[1].v[bo] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[i % D], op[1].f[s], out[1].v[bo], 0, 0, 0);
-      if (i + D < N)
-        fr[i % D] = *reinterpret_cast<const bf16x8*>(w + (blk(i + D) * NS + kst(i + D)) * BLK + lane * 8);
-    }
-    if (p > 0) {
-      epi(0, p - 1);
-      epi(1, p - 1);
-    }
-    // per fragment step: its two MFMAs, each followed by up to PIPE_NV VALU, then the step's LDS read
-#pragma unroll
-    for (int j = 0; j < PSTEPS; ++j) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x402, PIPE_NV, 0);  // VALU | TRANS
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x402, PIPE_NV, 0);  // VALU | TRANS
-      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-  }
-  epi(0, NBO / G - 1);
-  epi(1, NBO / G - 1);
-}
-
-// epilogue pieces on output-block pair p (blocks 2p, 2p+1) of an activation
-__device__ __forceinline__ void silu2_pair(Act<8>& a, int p) {
-#pragma unroll
-  for (int h = 0; h < 2; ++h)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) a.v[2 * p + h][r] = silu2<true>(a.v[2 * p + h][r]);
-}
-__device__ __forceinline__ void pack_pair(Op<BF16T, 4>& o, const Act<8>& a, int p) {
-  uint4 u;
-  u.x = pack_bf16x2(a.v[2 * p][0], a.v[2 * p][1]);
-  u.y = pack_bf16x2(a.v[2 * p][2], a.v[2 * p][3]);
-  u.z = pack_bf16x2(a.v[2 * p + 1][0], a.v[2 * p + 1][1]);
-  u.w = pack_bf16x2(a.v[2 * p + 1][2], a.v[2 * p + 1][3]);
-  o.f[p] = __builtin_bit_cast(bf16x8, u);
-}
-
-using LeanPipe = WPipe<u16, Lean::NW, true, EL_CAP, 128>;
+// ================================================================ weight stages of the bf16 edge layers
+// Double-buffered 36-block stage slots (plus the stage's bias vector) for a 4-wave block: the LDS-DMA
+// of stage i+1 runs under stage i's MFMAs.
+using X32Pipe = WPipe<u16, 4, true, EL_CAP, 128>;
 
 // stage sequencer of one tile: next() publishes stage i and issues the DMA of stage i + 1.
 // GC (DI_GRAPH_GEO_REF batches): the sequence starts at orig_msg_linear (stages 0-1, the neighbour
 // messages, are exactly zero), which then carries the orig_msg_linear bias, and (intermediate
 // layers) ends before the next layer's nbr_linear (its gathered rows are never needed).
 template <int NS, bool GC = false>
-struct LeanStages {
-  LeanPipe& pipe;
+struct X32Stages {
+  X32Pipe& pipe;
   const u16* W;
   const float* V;
   int i;
@@ -1102,18 +875,7 @@ struct LeanStages {
     pipe.issue(W + EL_ORDER[si] * BLK, EL_SIZE[si], vo >= 0 ? V + vo : nullptr, 128);
   }
   __device__ const u16* next() {
-    const u16* w = DI_DIAG_NOSYNC ? pipe.next_nosync() : pipe.next();
-    if (i + 1 < NS) issue(i + 1);
-    ++i;
-    return w;
-  }
-  // next() with the wave's own row loads `ld` issued between the stage barrier and the next stage's
-  // DMA: the barrier's vmcnt(0) does not wait for them, and a later wait for them (vmcnt in order)
-  // does not wait for the DMA issued after them
-  template <class F>
-  __device__ const u16* next(F&& ld) {
     const u16* w = pipe.next();
-    ld();
     if (i + 1 < NS) issue(i + 1);
     ++i;
     return w;
@@ -1121,399 +883,20 @@ struct LeanStages {
   __device__ const float* v() const { return pipe.v(); }
 };
 
-// y = W . x (+ bias from the stage's LDS slot); x as a packed operand
-template <int NBO, int NS>
-__device__ __forceinline__ void lin_op(Act<NBO>& y, const Op<BF16T, NS>& x, const u16* w, const float* bias, int lane,
-                                       int g) {
-  if (bias) init_vec_lds(y, bias, g);
-  else zero(y);
-  mma_ring<NBO, NS>(y, x, w, lane);
-}
-
-__device__ __forceinline__ void raw_op(Op<BF16T, 4>& o, const RawRow<u16>& r) {
-#pragma unroll
-  for (int k = 0; k < 4; ++k)
-    o.f[k] = __builtin_bit_cast(bf16x8, (uint4){r.u[2 * k].x, r.u[2 * k].y, r.u[2 * k + 1].x, r.u[2 * k + 1].y});
-}
-
-// per-group row state
-struct LeanRow {
-  int e;
-  bool valid;
-};
-
-template <int NS, bool GC>
-__device__ __forceinline__ void lean_res_block(Act<8> (&x)[Lean::LG], LeanStages<NS, GC>& st, int lane, int g) {
-  Op<BF16T, 4> op[Lean::LG];
-#pragma unroll
-  for (int q = 0; q < Lean::LG; ++q) make_op(op[q], x[q]);
-
-#pragma unroll 1
-  for (int l = 0; l < 2; ++l) {
-    const u16* w = st.next();
-    Act<8> t[Lean::LG];
-    Op<BF16T, 4> opn[Lean::LG];
-    // layers 0, 1: t = silu2(W op + b) packed as the next layer's operand
-    lin_groups_pipe<4>(t, op, w, st.v(), lane, g, [&](int q, int p) {
-      silu2_pair(t[q], p);
-      pack_pair(opn[q], t[q], p);
-    });
-#pragma unroll
-    for (int q = 0; q < Lean::LG; ++q) {
-      op[q] = opn[q];
-      pin(op[q]);
-    }
-  }
-  const u16* w = st.next();
-  Act<8> t[Lean::LG];
-  // layer 2: x += ln2 * silu2(W op + b)
-  lin_groups_pipe<4>(t, op, w, st.v(), lane, g, [&](int q, int p) {
-    silu2_pair(t[q], p);
-#pragma unroll
-    for (int h = 0; h < 2; ++h) x[q].v[2 * p + h] += silu2_unit<true>() * t[q].v[2 * p + h];
-  });
-#pragma unroll
-  for (int q = 0; q < Lean::LG; ++q) pin(x[q]);
-}
-
-// y = silu2(W x + b); x = F + ln2 * y  (res_connect_linear / final_linear residual)
-// F rows are loaded BEFORE the stage's barrier and DMA issue: vmcnt retires in order, so a load
-// issued after the stage's LDS-DMA pieces would make its use wait for the whole weight stage.
-__device__ __forceinline__ void load_f(RawRow<u16> (&fr)[Lean::LG], const u16* const (&f_row)[Lean::LG], int g) {
-#pragma unroll
-  for (int q = 0; q < Lean::LG; ++q) fr[q].load(f_row[q], g);
-}
-
-__device__ __forceinline__ void lean_f_residual(Act<8> (&x)[Lean::LG], const u16* w, const float* v,
-                                                const RawRow<u16> (&fr)[Lean::LG], int lane, int g) {
-  Op<BF16T, 4> op[Lean::LG];
-#pragma unroll
-  for (int q = 0; q < Lean::LG; ++q) make_op(op[q], x[q]);
-  Act<8> y[Lean::LG];
-  // x = F + ln2 * silu2(W x + b), pair by pair (F: the edge's own bf16 row, exact in fp32)
-  lin_groups_pipe<4>(y, op, w, v, lane, g, [&](int q, int p) {
-    silu2_pair(y[q], p);
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int b = 2 * p + h;
-      const uint2 u = fr[q].u[b];
-      const floatx4 f = {__builtin_bit_cast(float, u.x << 16), __builtin_bit_cast(float, u.x & 0xffff0000u),
-                         __builtin_bit_cast(float, u.y << 16), __builtin_bit_cast(float, u.y & 0xffff0000u)};
-      x[q].v[b] = f + silu2_unit<true>() * y[q].v[b];
-    }
-  });
-#pragma unroll
-  for (int q = 0; q < Lean::LG; ++q) pin(x[q]);
-}
-
-template <int MODE, bool GC>
-__global__ __attribute__((amdgpu_flat_work_group_size(1, Lean::THREADS), amdgpu_waves_per_eu(2, 2),
-                          amdgpu_num_vgpr(120)))
-void k_edge_lean(EdgeArgs a) {
-  constexpr bool FINAL = MODE == 1;
-  constexpr int NS = (FINAL ? EL_NSTAGE_FINAL : EL_NSTAGE) - (GC ? (FINAL ? 2 : 3) : 0);
-  constexpr int LG = Lean::LG;
-  __shared__ __attribute__((aligned(16))) char lds[2 * LeanPipe::SLOT_BYTES];
-  const int lane = lane_id(), g = lane >> 4;
-  const u16* fn_in = reinterpret_cast<const u16*>(a.fn_in);
-  const u16* qkv = reinterpret_cast<const u16*>(a.qkv);
-  LeanRow rw[LG];
-  const u16* f_row[LG];
-#pragma unroll
-  for (int q = 0; q < LG; ++q) {
-    lean_fence();
-    const int r = blockIdx.x * Lean::ROWS_ALL + q * Lean::GROUP_ROWS + (threadIdx.x >> 6) * ROWS_PER_WAVE + (threadIdx.x & 15);
-    rw[q].valid = r < a.Et;
-    rw[q].e = rw[q].valid ? r : a.Et - 1;
-    f_row[q] = reinterpret_cast<const u16*>(a.f_in) + (int64_t)rw[q].e * HID;
-  }
-
-  LeanPipe pipe(lds);
-  LeanStages<NS, GC> st{pipe, reinterpret_cast<const u16*>(a.wmat), a.wvec, 0};
-  st.issue(0);
-
-  Op<BF16T, 1> gop[LG];
-#pragma unroll
-  for (int q = 0; q < LG; ++q) {
-    lean_fence();
-    Act<2> geo;
-    load_edge_geo(geo, a.edge_f + (int64_t)rw[q].e * NFEAT_E, g);
-    make_op(gop[q], geo);
-  }
-  const u16* w;
-  Act<8> x[LG];
-  RawRow<u16> fr[LG];
-  if constexpr (GC) {
-    // DI_GRAPH_GEO_REF: the neighbour messages are multiplied by dir_linear_1(dir_linear_0(0)) = 0
-    // (:408), so x = orig_msg_linear(F) + b exactly; no gathered rows, no stages 0-1
-    load_f(fr, f_row, g);
-    w = st.next();  // orig_msg_linear (+ its bias)
-#pragma unroll
-    for (int q = 0; q < LG; ++q) init_vec_lds(x[q], st.v(), g);
-  } else {
-    RawRow<u16> xn;  // the gathered neighbour row in flight (group-major order: q, then j)
-    int4 nb = *reinterpret_cast<const int4*>(a.nbr + (int64_t)rw[0].e * 4);
-    xn.load(fn_in + (int64_t)nb.x * HID, g);
-
-    // ---- neighbour-edge messages (conformation_module_message_func :384-418)
-    w = st.next();  // stage 0: geometric gates + downward_proj
-    Act<4> s[LG];
-#pragma unroll
-    for (int q = 0; q < LG; ++q) {
-      lean_fence();
-      Act<4> gate;
-      {
-        Act<4> t1;
-        zero(gate);
-        mma_ring<4, 1>(gate, gop[q], w + 8 * BLK, lane);
-        zero(t1);
-        mma_ring<4, 1>(t1, gop[q], w + 12 * BLK, lane);
-        mul_(gate, t1);
-        zero(t1);
-        mma_ring<4, 1>(t1, gop[q], w + 16 * BLK, lane);
-        mul_(gate, t1);
-        pin(gate);
-      }
-      zero(s[q]);
-      const int4 nbq = nb;
-      if (q + 1 < LG) nb = *reinterpret_cast<const int4*>(a.nbr + (int64_t)rw[q + 1].e * 4);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        lean_fence();
-        // x = silu(nbr_linear(F))[nbr_j] * dist gate, packed k-step by k-step
-        Op<BF16T, 4> xop;
-#pragma unroll
-        for (int ks = 0; ks < 4; ++ks) {
-          // recomputed per neighbour (2 MFMAs per k-step) rather than held live across the loop:
-          // the memory clobber stops the compiler from merging the neighbours' copies (32 VGPRs)
-          lean_fence();
-          Act<2> dg;
-          zero(dg);
-          mma_ring<2, 1>(dg, gop[q], w + 2 * ks * BLK, lane);
-          // opaque until here: keeps the compiler from unpacking the whole gathered row to fp32 as
-          // soon as it lands (32 registers instead of 16)
-          asm volatile("" : "+v"(xn.u[2 * ks]), "+v"(xn.u[2 * ks + 1]));
-          const uint2 lo = xn.u[2 * ks], hi = xn.u[2 * ks + 1];
-          uint4 u;
-          u.x = pack_bf16x2(__builtin_bit_cast(float, lo.x << 16) * dg.v[0][0],
-                            __builtin_bit_cast(float, lo.x & 0xffff0000u) * dg.v[0][1]);
-          u.y = pack_bf16x2(__builtin_bit_cast(float, lo.y << 16) * dg.v[0][2],
-                            __builtin_bit_cast(float, lo.y & 0xffff0000u) * dg.v[0][3]);
-          u.z = pack_bf16x2(__builtin_bit_cast(float, hi.x << 16) * dg.v[1][0],
-                            __builtin_bit_cast(float, hi.x & 0xffff0000u) * dg.v[1][1]);
-          u.w = pack_bf16x2(__builtin_bit_cast(float, hi.y << 16) * dg.v[1][2],
-                            __builtin_bit_cast(float, hi.y & 0xffff0000u) * dg.v[1][3]);
-          xop.f[ks] = __builtin_bit_cast(bf16x8, u);
-        }
-        // the next gathered row, in flight under this one's downward_proj
-        if (j < 3) {
-          const int nx = j == 0 ? nbq.y : (j == 1 ? nbq.z : nbq.w);
-          xn.load(fn_in + (int64_t)nx * HID, g);
-        } else if (q + 1 < LG) {
-          xn.load(fn_in + (int64_t)nb.x * HID, g);
-        }
-        lean_fence();
-        Act<4> y;
-        zero(y);
-        mma_ring<4, 4>(y, xop, w + 20 * BLK, lane);  // downward_proj
-#pragma unroll
-        for (int b = 0; b < 4; ++b)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) s[q].v[b][r] += silu2<true>(y.v[b][r]) * gate.v[b][r];
-        pin(s[q]);
-      }
-    }
-    {
-      w = st.next();  // stage 1: upward_proj (+ orig_msg_linear bias)
-#pragma unroll
-      for (int q = 0; q < LG; ++q) {
-        lean_fence();
-        Op<BF16T, 2> sop;
-        make_op(sop, s[q]);
-        lin_op<8, 2>(x[q], sop, w, nullptr, lane, g);
-        silu2_<8, true>(x[q]);
-        Act<8> bo;
-        init_vec_lds(bo, st.v(), g);
-#pragma unroll
-        for (int b = 0; b < 8; ++b) x[q].v[b] = silu2_unit<true>() * x[q].v[b] + bo.v[b];
-        pin(x[q]);
-      }
-    }
-    load_f(fr, f_row, g);
-    w = st.next();  // stage 2: orig_msg_linear(res) + nbr
-  }
-  {
-    Op<BF16T, 4> fop[LG];
-#pragma unroll
-    for (int q = 0; q < LG; ++q) raw_op(fop[q], fr[q]);
-    mma_ring2<8, 4>(x[0], x[1], fop[0], fop[1], w, lane);
-#pragma unroll
-    for (int q = 0; q < LG; ++q) pin(x[q]);
-  }
-  lean_res_block(x, st, lane, g);
-  lean_res_block(x, st, lane, g);
-  // (round 3: holding the F rows in registers from orig_msg_linear to here instead of re-reading them
-  // -- 240 VGPRs, a 12-B spill -- measured equal: 7448 vs 7320-7456 complexes/s)
-  load_f(fr, f_row, g);
-  w = st.next();  // res_connect_linear: x = F + silu(rc(x))
-  lean_f_residual(x, w, st.v(), fr, lane, g);
-  lean_res_block(x, st, lane, g);
-  lean_res_block(x, st, lane, g);
-  w = st.next();  // final geometric gate
-#pragma unroll
-  for (int q = 0; q < LG; ++q) {
-    lean_fence();
-    Act<8> fg;
-    zero(fg);
-    mma_ring<8, 1>(fg, gop[q], w, lane);
-    mul_(x[q], fg);
-    pin(x[q]);
-  }
-  load_f(fr, f_row, g);
-  w = st.next();  // final_linear: x = F + silu(final(x)) = conformation output
-  lean_f_residual(x, w, st.v(), fr, lane, g);
-
-  // ---- attention scores (propagate_attention :76-91)
-  RawRow<u16> kr[LG], qr[LG];  // K[src], Q[dst]: issued before the stage barrier
-#pragma unroll
-  for (int q = 0; q < LG; ++q) {
-    lean_fence();
-    const int e = rw[q].e;
-    kr[q].load(qkv + (int64_t)a.src[e] * 3 * HID + HID, g);
-    qr[q].load(qkv + (int64_t)a.dst[e] * 3 * HID, g);
-  }
-  w = st.next();  // edge_feats_projection(BN1e(conf))
-  Op<BF16T, 4> pop[LG];
-  Act<8> pg[LG];
-  {
-    Op<BF16T, 4> xop[LG];
-#pragma unroll
-    for (int q = 0; q < LG; ++q) make_op(xop[q], x[q]);
-    lin_groups<8, 4>(pg, xop, w, st.v(), lane, g);
-  }
-#pragma unroll
-  for (int q = 0; q < LG; ++q) {
-    lean_fence();
-    const int e = rw[q].e;
-    Act<8> p = pg[q];
-    Act<8> kq, qd;
-    kr[q].to_act(kq);
-    qr[q].to_act(qd);
-#pragma unroll
-    for (int b = 0; b < 8; ++b)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float sc = (kq.v[b][r] * qd.v[b][r]) * (1.0f / 5.656854249492381f);  // / np.sqrt(32)
-        sc = fminf(fmaxf(sc, -5.f), 5.f);
-        p.v[b][r] = sc * p.v[b][r];  // score = e_out
-      }
-    floatx4 al;
-#pragma unroll
-    for (int h = 0; h < 4; ++h) al[h] = expf_<true>(fminf(fmaxf(head_sum(p, h), -5.f), 5.f));
-    if (rw[q].valid && g == 0) st4(a.alpha_out + (int64_t)e * 4, al);
-    if constexpr (!FINAL) {
-      make_op(pop[q], p);
-      pin(pop[q]);
-    }
-  }
-  if constexpr (!FINAL) {
-    // ---- edge output: e = in + O_e(e_out); e = e + FFN(BN2e(e)) (:697-724)
-    load_f(fr, f_row, g);  // O_edge: re-read (the attention stage has no room for it)
-    w = st.next();  // O_edge_feats
-    Act<8> e1[LG];
-    lin_groups<8, 4>(e1, pop, w, st.v(), lane, g);
-#pragma unroll
-    for (int q = 0; q < LG; ++q) {
-      lean_fence();
-      Act<8> fa;
-      fr[q].to_act(fa);
-      add_(e1[q], fa);
-      pin(e1[q]);
-    }
-    Op<BF16T, 4> eop[LG];
-#pragma unroll
-    for (int q = 0; q < LG; ++q) {
-      make_op(eop[q], e1[q]);
-      pin(eop[q]);
-    }
-#pragma unroll 1
-    for (int half = 0; half < 2; ++half) {
-      w = st.next();  // edge_feats_MLP.0 (BN2e folded), hidden half
-      Op<BF16T, 4> top[LG];
-      Act<8> t[LG];
-      lin_groups_pipe<4>(t, eop, w, st.v(), lane, g, [&](int q, int p) {
-        silu2_pair(t[q], p);
-        pack_pair(top[q], t[q], p);
-      });
-#pragma unroll
-      for (int q = 0; q < LG; ++q) pin(top[q]);
-      w = st.next();  // edge_feats_MLP.3, input half: accumulated into the residual
-      mma_ring2<8, 4>(e1[0], e1[1], top[0], top[1], w, lane);
-#pragma unroll
-      for (int q = 0; q < LG; ++q) pin(e1[q]);
-    }
-#pragma unroll
-    for (int q = 0; q < LG; ++q) {
-      lean_fence();
-      if (rw[q].valid) store_edge_row(e1[q], reinterpret_cast<u16*>(a.f_out) + (int64_t)rw[q].e * HID, g);
-      make_op(eop[q], e1[q]);
-    }
-    if constexpr (GC) return;  // the next layer gathers no silu(nbr_linear(F)) rows
-    w = st.next();  // next layer's silu(nbr_linear(.))
-    Act<8> fng[LG];
-    lin_groups<8, 4>(fng, eop, w, st.v(), lane, g);
-#pragma unroll
-    for (int q = 0; q < LG; ++q) {
-      lean_fence();
-      silu_<8, true>(fng[q]);
-      if (rw[q].valid) store_edge_row(fng[q], reinterpret_cast<u16*>(a.fn_out) + (int64_t)rw[q].e * HID, g);
-    }
-  }
-}
-
 // ================================================================ fused edge layer on 32x32x16 MFMA (bf16)
-// The stage sequence and arithmetic of k_edge_lean, with each wave's 32 rows as ONE 32x32 tile
-// (csrc/mfma32.h): a 128x128 linear is 32 v_mfma_f32_32x32x16_bf16 per wave instead of 64
-// v_mfma_f32_16x16x32_bf16, which halves the MFMAs' hold on the SIMD's vector issue (8 cycles per
-// instruction either way) -- the issue slots the SiLU epilogues of the edge layers are bound by.
-// Same weight stages (LDS-DMA double-buffered, one 36-block slot per stage), same block geometry
-// (4 waves, 128 edges per block, two blocks per CU at <= 240 VGPRs); the weight blobs are packed in
-// the 32x32 fragment order (packing.pack_matrix32, di_blob_layout() == 32).
-#ifndef DI_EDGE_X32
-#define DI_EDGE_X32 1
-#endif
-#ifndef DI_DIAG_REREAD0
-#define DI_DIAG_REREAD0 0
-#endif
-#ifndef DI_EDGE_PRIO
-#define DI_EDGE_PRIO 0
-#endif
-// round 4: the edge row re-reads and the K/Q gathers issued after a stage barrier (one stage early
-// where registers allow: stage 1, the final gate) instead of just before it, so the barrier's
-// vmcnt(0) does not wait for them
-#ifndef DI_X32_ROWLD
-#define DI_X32_ROWLD 0
-#endif
+// The stage sequence and arithmetic of k_edge_layer<BF16T, MODE, GC>, with each wave's 32 rows as ONE
+// 32x32 tile (csrc/mfma32.h): a 128x128 linear is 32 v_mfma_f32_32x32x16_bf16 per wave. Weight stages
+// LDS-DMA double-buffered (X32Pipe, one 36-block slot per stage), 4-wave blocks of 128 edges, two
+// blocks per CU at <= 240 VGPRs; the weight blobs are packed in the 32x32 fragment order
+// (packing.pack_matrix32, di_blob_layout() == 32).
 struct EdgeX32Geo {
   static constexpr int NW = 4, THREADS = 64 * NW, ROWS_PER_WAVE = 32, ROWS = ROWS_PER_WAVE * NW;
 };
+static_assert(EdgeX32Geo::NW == 4, "X32Pipe splits every stage's DMA pieces over 4 waves");
 
 // x through one ResBlock: two silu2(W . + b) layers packed as the next operand, then x += ln2 * silu2(W . + b)
-// DI_X32_PREFETCH (round 4 experiment): one dword per lane of the edge row (lane l: row l & 31,
-// 128-B line l >> 5) loaded one stage ahead of each re-read, so the row's two lines are back in L2
-// when the re-read comes (the pair stores cycle the XCD L2s in a few us); the value is only kept
-// alive past the next stage barrier, whose vmcnt(0) retires it
-#ifndef DI_X32_PREFETCH
-#define DI_X32_PREFETCH 0
-#endif
-__device__ __forceinline__ uint32_t x32_touch(const u16* f_row, int h) {
-  return *reinterpret_cast<const uint32_t*>(f_row + 64 * h);
-}
-__device__ __forceinline__ void x32_keep(uint32_t v) { asm volatile("" ::"v"(v)); }
-
 template <int NS, bool GC>
-__device__ __forceinline__ void x32_res_block(X32<4>& x, LeanStages<NS, GC>& st, int lane, int h,
-                                              const u16* touch = nullptr, uint32_t* touched = nullptr) {
+__device__ __forceinline__ void x32_res_block(X32<4>& x, X32Stages<NS, GC>& st, int lane, int h) {
   P32<8> op;
   make_op32(op, x);
 #pragma unroll 1
@@ -1529,7 +912,6 @@ __device__ __forceinline__ void x32_res_block(X32<4>& x, LeanStages<NS, GC>& st,
     pin(op);
   }
   const u16* w = st.next();
-  if (touch) *touched = x32_touch(touch, h);
   X32<4> t;
   lin32_pipe<8>(t, op, w, st.v(), lane, h, [&](int b) {
     silu2_blk(t.v[b]);
@@ -1552,132 +934,21 @@ __device__ __forceinline__ void x32_f_residual(X32<4>& x, const u16* w, const fl
   pin(x);
 }
 
-// ---- DI_X32_DEFER (round 4 experiment): each linear's block-3 epilogue deferred under the next
-// linear's first MFMAs (lin32_pipe_d). The chain carries x with block 3 pending: pa = the last
-// linear's raw block-3 accumulator, PK = what is owed to x.v[3] --
-//   0 nothing; 1 x.v[3] += ln2 * silu2(pa) (ResBlock); 2 x.v[3] = F + ln2 * silu2(pa) (F residual).
-#ifndef DI_X32_DEFER
-#define DI_X32_DEFER 0
-#endif
-// the operand blocks a deferred linear has produced (k-steps 0-5; 6-7 come from the next pre())
-__device__ __forceinline__ void pin6(P32<8>& o) {
-#pragma unroll
-  for (int s = 0; s < 6; ++s) asm volatile("" : "+v"(o.f[s]));
-}
-template <int PK>
-__device__ __forceinline__ void x32_settle3(X32<4>& x, floatx16& pa, const R32<4>& fr) {
-  if constexpr (PK == 1) {
-    silu2_blk(pa);
-    x.v[3] += silu2_unit<true>() * pa;
-  } else if constexpr (PK == 2) {
-    silu2_blk(pa);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) set_quad(x.v[3], q, unpack4(fr.u[12 + q]) + silu2_unit<true>() * quad(pa, q));
-  }
-}
-
-// x32_res_block with deferred block-3 epilogues: enters owing PK to x.v[3], leaves owing 1
-template <int PK, int NS, bool GC>
-__device__ __forceinline__ void x32_res_block_d(X32<4>& x, floatx16& pa, const R32<4>& fr, LeanStages<NS, GC>& st,
-                                                int lane, int h) {
-  P32<8> op0, op1, op2;
-#pragma unroll
-  for (int b = 0; b < 3; ++b) pack_blk(op0.f[2 * b], op0.f[2 * b + 1], x.v[b]);
-  {
-    const u16* w = st.next();
-    X32<4> t;
-    lin32_pipe_d<8>(
-        t, op0, w, st.v(), lane, h,
-        [&] {
-          x32_settle3<PK>(x, pa, fr);
-          pack_blk(op0.f[6], op0.f[7], x.v[3]);
-        },
-        [&](int b) {
-          silu2_blk(t.v[b]);
-          pack_blk(op1.f[2 * b], op1.f[2 * b + 1], t.v[b]);
-        });
-    pa = t.v[3];
-    pin6(op1);
-  }
-  {
-    const u16* w = st.next();
-    X32<4> t;
-    lin32_pipe_d<8>(
-        t, op1, w, st.v(), lane, h,
-        [&] {
-          silu2_blk(pa);
-          pack_blk(op1.f[6], op1.f[7], pa);
-        },
-        [&](int b) {
-          silu2_blk(t.v[b]);
-          pack_blk(op2.f[2 * b], op2.f[2 * b + 1], t.v[b]);
-        });
-    pa = t.v[3];
-    pin6(op2);
-  }
-  const u16* w = st.next();
-  X32<4> t;
-  lin32_pipe_d<8>(
-      t, op2, w, st.v(), lane, h,
-      [&] {
-        silu2_blk(pa);
-        pack_blk(op2.f[6], op2.f[7], pa);
-      },
-      [&](int b) {
-        silu2_blk(t.v[b]);
-        x.v[b] += silu2_unit<true>() * t.v[b];
-      });
-  pa = t.v[3];
-#pragma unroll
-  for (int b = 0; b < 3; ++b) asm volatile("" : "+v"(x.v[b]));
-}
-
-// x32_f_residual with deferred block-3 epilogues: enters owing PK, leaves owing 2 (fr = the edge's
-// F row, the same row every F residual reads)
-template <int PK>
-__device__ __forceinline__ void x32_f_residual_d(X32<4>& x, floatx16& pa, const u16* w, const float* v,
-                                                 const R32<4>& fr, int lane, int h) {
-  P32<8> op;
-#pragma unroll
-  for (int b = 0; b < 3; ++b) pack_blk(op.f[2 * b], op.f[2 * b + 1], x.v[b]);
-  X32<4> y;
-  lin32_pipe_d<8>(
-      y, op, w, v, lane, h,
-      [&] {
-        x32_settle3<PK>(x, pa, fr);
-        pack_blk(op.f[6], op.f[7], x.v[3]);
-      },
-      [&](int b) {
-        silu2_blk(y.v[b]);
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-          set_quad(x.v[b], q, unpack4(fr.u[4 * b + q]) + silu2_unit<true>() * quad(y.v[b], q));
-      });
-  pa = y.v[3];
-#pragma unroll
-  for (int b = 0; b < 3; ++b) asm volatile("" : "+v"(x.v[b]));
-}
-
 template <int MODE, bool GC>
 __global__ __attribute__((amdgpu_flat_work_group_size(1, EdgeX32Geo::THREADS), amdgpu_waves_per_eu(2, 2),
                           amdgpu_num_vgpr(120)))
 void k_edge_x32(EdgeArgs a) {
   constexpr bool FINAL = MODE == 1;
   constexpr int NS = (FINAL ? EL_NSTAGE_FINAL : EL_NSTAGE) - (GC ? (FINAL ? 2 : 3) : 0);
-  __shared__ __attribute__((aligned(16))) char lds[2 * LeanPipe::SLOT_BYTES];
+  __shared__ __attribute__((aligned(16))) char lds[2 * X32Pipe::SLOT_BYTES];
   const int lane = lane_id(), h = lane >> 5;
-  // round 4 experiment: static issue priority for every other block (0 = off)
-  if constexpr (DI_EDGE_PRIO > 0)
-    if (blockIdx.x & 1) __builtin_amdgcn_s_setprio(DI_EDGE_PRIO);
   const int r = blockIdx.x * EdgeX32Geo::ROWS + (threadIdx.x >> 6) * EdgeX32Geo::ROWS_PER_WAVE + (lane & 31);
   const bool valid = r < a.Et;
   const int e = valid ? r : a.Et - 1;
   const u16* f_row = reinterpret_cast<const u16*>(a.f_in) + (int64_t)e * HID;
-  // DI_DIAG_REREAD0 (timing diagnostic only, wrong results): the row re-reads from row 0 (L2-resident)
-  const u16* f_rr = DI_DIAG_REREAD0 ? reinterpret_cast<const u16*>(a.f_in) : f_row;
   const u16* qkv = reinterpret_cast<const u16*>(a.qkv);
-  LeanPipe pipe(lds);
-  LeanStages<NS, GC> st{pipe, reinterpret_cast<const u16*>(a.wmat), a.wvec, 0};
+  X32Pipe pipe(lds);
+  X32Stages<NS, GC> st{pipe, reinterpret_cast<const u16*>(a.wmat), a.wvec, 0};
   st.issue(0);
 
   // the edge's geometric features [28] (fp32 row) as a 32-feature operand, features 28..31 = 0
@@ -1693,7 +964,7 @@ void k_edge_x32(EdgeArgs a) {
     make_op32(gop, geo);
   }
   X32<4> x;
-  R32<4> fr;
+  R32<4> fr;  // the edge's own row F, re-read (L2) before each use: the stages have no room to hold it
   const u16* w;
   if constexpr (GC) {
     // DI_GRAPH_GEO_REF: the neighbour messages are multiplied by dir_linear_1(dir_linear_0(0)) = 0
@@ -1760,8 +1031,7 @@ void k_edge_x32(EdgeArgs a) {
         for (int k = 0; k < 16; ++k) s.v[b][k] += silu2<true>(y.v[b][k]) * gate.v[b][k];
       pin(s);
     }
-    if constexpr (DI_X32_ROWLD) w = st.next([&] { fr.load(f_rr, h); });  // stage 1: upward_proj [4x4]
-    else w = st.next();  // stage 1: upward_proj [4x4] (+ orig_msg_linear bias)
+    w = st.next();  // stage 1: upward_proj [4x4] (+ orig_msg_linear bias)
     {
       P32<4> sop;
       make_op32(sop, s);
@@ -1776,7 +1046,7 @@ void k_edge_x32(EdgeArgs a) {
       }
       pin(x);
     }
-    if constexpr (!DI_X32_ROWLD) fr.load(f_rr, h);
+    fr.load(f_row, h);
     w = st.next();  // stage 2: orig_msg_linear(res) + nbr
   }
   {
@@ -1785,91 +1055,33 @@ void k_edge_x32(EdgeArgs a) {
     mma32<4, 8>(x, fop, w, lane);
     pin(x);
   }
-  if constexpr (DI_X32_DEFER) {
-    floatx16 pa;
-    x32_res_block_d<0>(x, pa, fr, st, lane, h);
-    x32_res_block_d<1>(x, pa, fr, st, lane, h);
-    if constexpr (DI_X32_DEFER == 2) {  // F residuals not deferred
-      x32_settle3<1>(x, pa, fr);
-      lean_fence();  // not hoisted over the chain (would pin 32 registers)
-      fr.load(f_rr, h);
-      w = st.next();  // res_connect_linear: x = F + silu(rc(x))
-      x32_f_residual(x, w, st.v(), fr, lane, h);
-      x32_res_block_d<0>(x, pa, fr, st, lane, h);
-    } else {
-      lean_fence();  // not hoisted over the chain (would pin 32 registers)
-      fr.load(f_rr, h);
-      w = st.next();  // res_connect_linear: x = F + silu(rc(x))
-      x32_f_residual_d<1>(x, pa, w, st.v(), fr, lane, h);
-      x32_res_block_d<2>(x, pa, fr, st, lane, h);
-    }
-    x32_res_block_d<1>(x, pa, fr, st, lane, h);
-    w = st.next();  // final geometric gate [4x2]
-    {
-      X32<4> fg;
-      zero(fg);
-      mma32<4, 2>(fg, gop, w, lane);
-      x32_settle3<1>(x, pa, fr);
+  x32_res_block(x, st, lane, h);
+  x32_res_block(x, st, lane, h);
+  // F rows are loaded BEFORE the stage's barrier and DMA issue: vmcnt retires in order, so a load
+  // issued after the stage's LDS-DMA pieces would make its use wait for the whole weight stage
+  fr.load(f_row, h);
+  w = st.next();  // res_connect_linear: x = F + silu(rc(x))
+  x32_f_residual(x, w, st.v(), fr, lane, h);
+  x32_res_block(x, st, lane, h);
+  x32_res_block(x, st, lane, h);
+  w = st.next();  // final geometric gate [4x2]
+  {
+    X32<4> fg;
+    zero(fg);
+    mma32<4, 2>(fg, gop, w, lane);
 #pragma unroll
-      for (int b = 0; b < 4; ++b) x.v[b] *= fg.v[b];
-      pin(x);
-    }
-    lean_fence();  // not hoisted over the chain (would pin 32 registers)
-      fr.load(f_rr, h);
-    w = st.next();  // final_linear: x = F + silu(final(x)) = conformation output
-    if constexpr (DI_X32_DEFER == 2) {
-      x32_f_residual(x, w, st.v(), fr, lane, h);
-    } else {
-      x32_f_residual_d<0>(x, pa, w, st.v(), fr, lane, h);
-      x32_settle3<2>(x, pa, fr);
-      pin(x);
-    }
-  } else {
-    uint32_t pf = 0;
-    constexpr bool PF = DI_X32_PREFETCH;
-    x32_res_block(x, st, lane, h);
-    x32_res_block(x, st, lane, h, PF ? f_rr : nullptr, &pf);
-    if constexpr (DI_X32_ROWLD) {
-      w = st.next([&] { fr.load(f_rr, h); });  // res_connect_linear: x = F + silu(rc(x))
-    } else {
-      fr.load(f_rr, h);
-      w = st.next();  // res_connect_linear: x = F + silu(rc(x))
-    }
-    if constexpr (PF) x32_keep(pf);
-    x32_f_residual(x, w, st.v(), fr, lane, h);
-    x32_res_block(x, st, lane, h);
-    x32_res_block(x, st, lane, h);
-    if constexpr (DI_X32_ROWLD) w = st.next([&] { fr.load(f_rr, h); });  // final geometric gate [4x2]
-    else w = st.next();  // final geometric gate [4x2]
-    if constexpr (PF) pf = x32_touch(f_rr, h);
-    {
-      X32<4> fg;
-      zero(fg);
-      mma32<4, 2>(fg, gop, w, lane);
-#pragma unroll
-      for (int b = 0; b < 4; ++b) x.v[b] *= fg.v[b];
-      pin(x);
-    }
-    if constexpr (!DI_X32_ROWLD) fr.load(f_rr, h);
-    w = st.next();  // final_linear: x = F + silu(final(x)) = conformation output
-    if constexpr (PF) x32_keep(pf);
-    x32_f_residual(x, w, st.v(), fr, lane, h);
+    for (int b = 0; b < 4; ++b) x.v[b] *= fg.v[b];
+    pin(x);
   }
+  fr.load(f_row, h);
+  w = st.next();  // final_linear: x = F + silu(final(x)) = conformation output
+  x32_f_residual(x, w, st.v(), fr, lane, h);
 
   // ---- attention scores (propagate_attention :76-91): head hd = features 32 hd .. 32 hd + 31 = block hd
-  R32<4> kr, qr;  // K[src], Q[dst]
-  const auto ldkq = [&] {
-    kr.load(qkv + (int64_t)a.src[e] * 3 * HID + HID, h);
-    qr.load(qkv + (int64_t)a.dst[e] * 3 * HID, h);
-  };
-  if constexpr (DI_X32_ROWLD) {
-    w = st.next(ldkq);  // edge_feats_projection(BN1e(conf))
-  } else {
-    ldkq();  // issued before the stage barrier
-    w = st.next();
-  }
-  uint32_t pfo = 0;
-  if constexpr (DI_X32_PREFETCH && !FINAL) pfo = x32_touch(f_rr, h);
+  R32<4> kr, qr;  // K[src], Q[dst], issued before the stage barrier
+  kr.load(qkv + (int64_t)a.src[e] * 3 * HID + HID, h);
+  qr.load(qkv + (int64_t)a.dst[e] * 3 * HID, h);
+  w = st.next();  // edge_feats_projection(BN1e(conf))
   X32<4> p;
   {
     P32<8> xop;
@@ -1902,13 +1114,8 @@ void k_edge_x32(EdgeArgs a) {
     P32<8> pop;
     make_op32(pop, p);
     pin(pop);
-    if constexpr (DI_X32_ROWLD) {
-      w = st.next([&] { fr.load(f_rr, h); });  // O_edge_feats (+ the edge row re-read)
-    } else {
-      fr.load(f_rr, h);  // O_edge: re-read
-      w = st.next();      // O_edge_feats
-    }
-    if constexpr (DI_X32_PREFETCH) x32_keep(pfo);
+    fr.load(f_row, h);  // O_edge: re-read
+    w = st.next();      // O_edge_feats
     X32<4> e1;
     init_vec32_lds(e1, st.v(), h);
     mma32<4, 8>(e1, pop, w, lane);
@@ -1946,6 +1153,7 @@ void k_edge_x32(EdgeArgs a) {
     if (valid) store_row32(fn, reinterpret_cast<u16*>(a.fn_out) + (int64_t)e * HID, h);
   }
 }
+
 
 // ================================================================ node aggregation (CSR segment sum)
 // h_attn[v] = sum_{e in in(v)} alpha[e, head] * V[src e]  /  (sum_e alpha[e, head] + 1e-6)
@@ -2354,17 +1562,17 @@ extern "C" int64_t di_blob_bytes(int kind, di_dtype dtype, int vec) {
 extern "C" int di_blob_layout(int kind, di_dtype dtype) {
   if (!dtype_ok(dtype) || kind < 0 || kind > 6) return -1;
   if (dtype != DI_BF16) return 16;
-  if (kind == 2 || kind == 3) return DI_EDGE_X32 ? 32 : 16;
-  if (kind == 1) return DI_INIT_X32 ? 32 : 16;
+  if (kind == 1 || kind == 2 || kind == 3) return 32;  // k_init_x32 / k_init_res_x32 / k_edge_x32
   return 16;
 }
 
 extern "C" int di_node_embed(const di_graph* g, di_dtype dt, int32_t in_dim, const float* node_f, const void* wmat,
-                             const float* wvec, void* h_out, void* qkv_out, void* stream) {
+                             const float* wvec, void* h_out, void* qkv_out, void* queue, int32_t signal_job,
+                             void* stream) {
   if (!g || !node_f || !wmat || !wvec || !h_out || !qkv_out || g->num_nodes <= 0 || in_dim <= 0 || in_dim > HID ||
       !dtype_ok(dt))
     return DI_EINVAL;
-  EmbedArgs a{g->num_nodes, in_dim, node_f, wmat, wvec, h_out, qkv_out};
+  EmbedArgs a{g->num_nodes, in_dim, node_f, wmat, wvec, h_out, qkv_out, (uint32_t*)queue, signal_job};
   hipStream_t s = (hipStream_t)stream;
   if (dt == DI_BF16)
     hipLaunchKernelGGL(k_node_embed<BF16T>, grid_of<EmbedGeo>(a.Nt), block_of<EmbedGeo>(), 0, s, a);
@@ -2383,14 +1591,11 @@ extern "C" int di_init_edge(const di_graph* g, di_dtype dt, const float* edge_f,
   InitArgs a{g->num_edges, edge_f, g->src, g->dst, g->node_pos, wmat, wvec, pos_src_tab, pos_dst_tab,
              f_out, fn_out};
   hipStream_t s = (hipStream_t)stream;
-  const dim3 gb = grid_of<InitGeo<BF16T>>(a.Et), bb = block_of<InitGeo<BF16T>>();
   const dim3 gf = grid_of<InitGeo<F32T>>(a.Et), bf = block_of<InitGeo<F32T>>();
   const EmbedArgs ne{};
   const dim3 gx((unsigned)((a.Et + InitX32Geo::ROWS - 1) / InitX32Geo::ROWS)), bx(InitX32Geo::THREADS);
-  if (dt == DI_BF16 && DI_INIT_X32 && gc) hipLaunchKernelGGL((k_init_x32<true>), gx, bx, 0, s, a, ne, 0);
-  else if (dt == DI_BF16 && DI_INIT_X32) hipLaunchKernelGGL((k_init_x32<false>), gx, bx, 0, s, a, ne, 0);
-  else if (dt == DI_BF16 && gc) hipLaunchKernelGGL((k_init_edge<BF16T, true>), gb, bb, 0, s, a, ne, 0);
-  else if (dt == DI_BF16) hipLaunchKernelGGL((k_init_edge<BF16T, false>), gb, bb, 0, s, a, ne, 0);
+  if (dt == DI_BF16 && gc) hipLaunchKernelGGL((k_init_x32<true>), gx, bx, 0, s, a, ne, 0);
+  else if (dt == DI_BF16) hipLaunchKernelGGL((k_init_x32<false>), gx, bx, 0, s, a, ne, 0);
   else if (gc) hipLaunchKernelGGL((k_init_edge<F32T, true>), gf, bf, 0, s, a, ne, 0);
   else hipLaunchKernelGGL((k_init_edge<F32T, false>), gf, bf, 0, s, a, ne, 0);
   return launch_status();
@@ -2400,7 +1605,7 @@ template <class DT>
 static void launch_embed_init(const InitArgs& a, const EmbedArgs& ea, hipStream_t s) {
   using G = InitGeo<DT>;
   const int eb = (ea.Nt + G::ROWS - 1) / G::ROWS;
-  if (DT::kBF16 && DI_INIT_X32) {
+  if constexpr (DT::kBF16) {
     const int ib = (a.Et + InitX32Geo::ROWS - 1) / InitX32Geo::ROWS;
     hipLaunchKernelGGL((k_init_x32<true>), dim3((unsigned)(eb + ib)), dim3(InitX32Geo::THREADS), 0, s, a, ea, eb);
     return;
@@ -2412,12 +1617,13 @@ static void launch_embed_init(const InitArgs& a, const EmbedArgs& ea, hipStream_
 extern "C" int di_embed_init_edge(const di_graph* g, di_dtype dt, int32_t in_dim, const float* node_f,
                                   const void* embed_wmat, const float* embed_wvec, void* h_out, void* qkv_out,
                                   const float* edge_f, const void* init_wmat, const float* init_wvec,
-                                  const float* pos_src_tab, const float* pos_dst_tab, void* f_out, void* stream) {
+                                  const float* pos_src_tab, const float* pos_dst_tab, void* f_out, void* queue,
+                                  int32_t signal_job, void* stream) {
   if (!g || !(g->flags & DI_GRAPH_GEO_REF) || !g->src || !g->dst || !g->node_pos || g->num_nodes <= 0 ||
       g->num_edges <= 0 || in_dim <= 0 || in_dim > HID || !node_f || !embed_wmat || !embed_wvec || !h_out ||
       !qkv_out || !edge_f || !init_wmat || !init_wvec || !pos_src_tab || !pos_dst_tab || !f_out || !dtype_ok(dt))
     return DI_EINVAL;
-  EmbedArgs ea{g->num_nodes, in_dim, node_f, embed_wmat, embed_wvec, h_out, qkv_out};
+  EmbedArgs ea{g->num_nodes, in_dim, node_f, embed_wmat, embed_wvec, h_out, qkv_out, (uint32_t*)queue, signal_job};
   InitArgs a{g->num_edges, edge_f, g->src, g->dst, g->node_pos, init_wmat, init_wvec, pos_src_tab, pos_dst_tab,
              f_out, nullptr};
   if (dt == DI_BF16) launch_embed_init<BF16T>(a, ea, (hipStream_t)stream);
@@ -2433,16 +1639,9 @@ extern "C" int di_init_edge_resident(const di_graph* g, const float* edge_f, con
   InitArgs a{g->num_edges, edge_f, g->src, g->dst, g->node_pos, wmat, wvec, pos_src_tab, pos_dst_tab, f_out, nullptr};
   // one block per CU holding the path's weights; never more blocks than the tiles need
   const int cus = device_cus();
-  if (DI_INIT_X32) {
-    const int ntiles = (a.Et + 31) / 32;
-    const int need = (ntiles + IRX_NW - 1) / IRX_NW;
-    hipLaunchKernelGGL(k_init_res_x32, dim3((unsigned)(need < cus ? need : cus)), dim3(64 * IRX_NW), 0,
-                       (hipStream_t)stream, a, ntiles);
-    return launch_status();
-  }
-  const int ntiles = (a.Et + ROWS_PER_WAVE - 1) / ROWS_PER_WAVE;
-  const int need = (ntiles + IR_NW - 1) / IR_NW;
-  hipLaunchKernelGGL(k_init_edge_res, dim3((unsigned)(need < cus ? need : cus)), block_of<InitResGeo>(), 0,
+  const int ntiles = (a.Et + 31) / 32;
+  const int need = (ntiles + IRX_NW - 1) / IRX_NW;
+  hipLaunchKernelGGL(k_init_res_x32, dim3((unsigned)(need < cus ? need : cus)), dim3(64 * IRX_NW), 0,
                      (hipStream_t)stream, a, ntiles);
   return launch_status();
 }
@@ -2461,20 +1660,13 @@ extern "C" int di_edge_layer(const di_graph* g, di_dtype dt, int final_layer, co
   EdgeArgs a{g->num_edges, edge_f, g->src, g->dst, g->nbr, f_in, fn_in, qkv, wmat, wvec, alpha_out,
              f_out, fn_out};
   hipStream_t s = (hipStream_t)stream;
-  if (dt == DI_BF16 && DI_EDGE_X32) {
+  if (dt == DI_BF16) {
     // 32x32x16 form: 128 edges (one 32-row tile per wave) per 4-wave block; 32x32-packed blob
     const dim3 grid((unsigned)((a.Et + EdgeX32Geo::ROWS - 1) / EdgeX32Geo::ROWS)), block(EdgeX32Geo::THREADS);
     if (final_layer && gc) hipLaunchKernelGGL((k_edge_x32<1, true>), grid, block, 0, s, a);
     else if (final_layer) hipLaunchKernelGGL((k_edge_x32<1, false>), grid, block, 0, s, a);
     else if (gc) hipLaunchKernelGGL((k_edge_x32<0, true>), grid, block, 0, s, a);
     else hipLaunchKernelGGL((k_edge_x32<0, false>), grid, block, 0, s, a);
-  } else if (dt == DI_BF16) {
-    // grouped form: 128 edges (two 16-row groups per wave) per 4-wave block
-    const dim3 grid((unsigned)((a.Et + Lean::ROWS_ALL - 1) / Lean::ROWS_ALL)), block = block_of<Lean>();
-    if (final_layer && gc) hipLaunchKernelGGL((k_edge_lean<1, true>), grid, block, 0, s, a);
-    else if (final_layer) hipLaunchKernelGGL((k_edge_lean<1, false>), grid, block, 0, s, a);
-    else if (gc) hipLaunchKernelGGL((k_edge_lean<0, true>), grid, block, 0, s, a);
-    else hipLaunchKernelGGL((k_edge_lean<0, false>), grid, block, 0, s, a);
   } else {
     const dim3 grid = grid_of<Geo<F32T>>(a.Et), block = block_of<Geo<F32T>>();
     if (final_layer && gc) hipLaunchKernelGGL((k_edge_layer<F32T, 1, true>), grid, block, 0, s, a);

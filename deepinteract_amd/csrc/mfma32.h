@@ -151,13 +151,9 @@ __device__ __forceinline__ void settle(const R32<NB>& r) {
   for (int i = 0; i < 4 * NB; ++i) asm volatile("" ::"v"(r.u[i].x), "v"(r.u[i].y));
 }
 
-// DI_DIAG_NOSILU (timing diagnostic only, wrong results): the block activation as a plain multiply
-#ifndef DI_DIAG_NOSILU
-#define DI_DIAG_NOSILU 0
-#endif
 __device__ __forceinline__ void silu2_blk(floatx16& v) {
 #pragma unroll
-  for (int k = 0; k < 16; ++k) v[k] = DI_DIAG_NOSILU ? v[k] * 0.5f : silu2<true>(v[k]);
+  for (int k = 0; k < 16; ++k) v[k] = silu2<true>(v[k]);
 }
 __device__ __forceinline__ void silu_blk(floatx16& v) {
 #pragma unroll
@@ -193,13 +189,10 @@ __device__ __forceinline__ void mma32(X32<NBO>& out, const P32<NS>& op, const u1
 // (SiLU, pack, residual) -- issued between the MFMAs of block b + 1: PIPE32_NV VALU / transcendental
 // instructions after each MFMA, then the step's LDS fragment read (sched_group_barrier). Block 3's
 // epilogue follows the loop. A 32x32x16 MFMA leaves 24 of its 32 issue cycles to the wave's vector
-// work (MI355X_MICROARCH.md, cycle constants).
-#ifndef DI_PIPE32_LEAD
-#define DI_PIPE32_LEAD 1
-#endif
-#ifndef DI_PIPE32_NV
-#define DI_PIPE32_NV 8
-#endif
+// work (MI355X_MICROARCH.md, cycle constants). Measured (round 4): 4 / 12 VALU per MFMA and the first
+// TWO MFMAs of block b + 1 ahead of epi(b) within noise of 8 and one.
+constexpr int PIPE32_NV = 8;    // VALU / TRANS instructions per MFMA
+constexpr int PIPE32_LEAD = 1;  // MFMAs of block b + 1 issued before epi(b)'s first VALU
 template <int NS, class Epi>
 __device__ __forceinline__ void lin32_pipe(X32<4>& out, const P32<NS>& op, const u16* w, const float* bias, int lane,
                                            int h, Epi&& epi) {
@@ -219,91 +212,18 @@ __device__ __forceinline__ void lin32_pipe(X32<4>& out, const P32<NS>& op, const
       if (i + D < N) fr[i % D] = afrag(w, i + D, lane);
     }
     if (ob > 0) epi(ob - 1);
-    // the first DI_PIPE32_LEAD MFMAs of block ob go out before any of epi(ob - 1)'s VALU, which reads
+    // the first PIPE32_LEAD MFMAs of block ob go out before any of epi(ob - 1)'s VALU, which reads
     // the accumulator block ob - 1's last MFMA is still writing
-    __builtin_amdgcn_sched_group_barrier(0x008, DI_PIPE32_LEAD, 0);  // MFMA
+    __builtin_amdgcn_sched_group_barrier(0x008, PIPE32_LEAD, 0);  // MFMA
 #pragma unroll
-    for (int s = DI_PIPE32_LEAD; s < NS + DI_PIPE32_LEAD; ++s) {
-      __builtin_amdgcn_sched_group_barrier(0x402, DI_PIPE32_NV, 0);  // VALU | TRANS
+    for (int s = PIPE32_LEAD; s < NS + PIPE32_LEAD; ++s) {
+      __builtin_amdgcn_sched_group_barrier(0x402, PIPE32_NV, 0);  // VALU | TRANS
       __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);             // DS read
       if (s < NS) __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
     }
     __builtin_amdgcn_sched_barrier(0);
   }
   epi(NBO - 1);
-}
-
-// lin32_pipe with the PREVIOUS linear's block-3 epilogue deferred into this one (round 4 experiment,
-// DI_X32_DEFER): pre() -- that epilogue, which produces op.f[NS - 2] and op.f[NS - 1] -- is issued
-// under block 0's first NS - 2 MFMAs (k-steps 0 .. NS - 3 need only the operand blocks already
-// packed), then block 0's last two k-steps; blocks 1-3 as lin32_pipe with epi(0 .. 2). This call's
-// own epi(3) is left to the caller (the next linear's pre(), or a flush). The MFMAs run in the same
-// k order as lin32_pipe, so the results are bit-identical.
-#ifndef DI_PIPE32_DEPTH_D
-#define DI_PIPE32_DEPTH_D MMA_DEPTH
-#endif
-#ifndef DI_PIPE32_NVP
-#define DI_PIPE32_NVP 12
-#endif
-template <int NS, class Pre, class Epi>
-__device__ __forceinline__ void lin32_pipe_d(X32<4>& out, const P32<NS>& op, const u16* w, const float* bias, int lane,
-                                             int h, Pre&& pre, Epi&& epi) {
-  constexpr int NBO = 4, N = NBO * NS, D = DI_PIPE32_DEPTH_D < N ? DI_PIPE32_DEPTH_D : N;
-  static_assert(NS >= 4, "block 0 needs k-steps that do not wait for pre()");
-  // accumulator blocks initialised one block ahead of their MFMAs (not all four up front): fewer
-  // registers live while pre()'s pending block is
-  const auto init_blk = [&](int b) {
-    if (bias) {
-      const __attribute__((address_space(3))) floatx4* p = (const __attribute__((address_space(3))) floatx4*)bias;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) set_quad(out.v[b], q, p[8 * b + 2 * q + h]);
-    } else {
-      out.v[b] = floatx16{};
-    }
-  };
-  init_blk(0);
-  init_blk(1);
-  bf16x8 fr[D];
-#pragma unroll
-  for (int i = 0; i < D; ++i) fr[i] = afrag(w, i, lane);
-  __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-  for (int s = 0; s < NS - 2; ++s) {
-    out.v[0] = mfma32(fr[s % D], op.f[s], out.v[0]);
-    if (s + D < N) fr[s % D] = afrag(w, s + D, lane);
-  }
-  pre();
-#pragma unroll
-  for (int s = 0; s < NS - 2; ++s) {
-    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);              // MFMA
-    __builtin_amdgcn_sched_group_barrier(0x402, DI_PIPE32_NVP, 0);  // VALU | TRANS
-    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);              // DS read
-  }
-  __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-  for (int s = NS - 2; s < NS; ++s) {
-    out.v[0] = mfma32(fr[s % D], op.f[s], out.v[0]);
-    if (s + D < N) fr[s % D] = afrag(w, s + D, lane);
-  }
-#pragma unroll
-  for (int ob = 1; ob < NBO; ++ob) {
-#pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      const int i = ob * NS + s;
-      out.v[ob] = mfma32(fr[i % D], op.f[s], out.v[ob]);
-      if (i + D < N) fr[i % D] = afrag(w, i + D, lane);
-    }
-    if (ob + 1 < NBO) init_blk(ob + 1);
-    epi(ob - 1);
-    __builtin_amdgcn_sched_group_barrier(0x008, DI_PIPE32_LEAD, 0);  // MFMA
-#pragma unroll
-    for (int s = DI_PIPE32_LEAD; s < NS + DI_PIPE32_LEAD; ++s) {
-      __builtin_amdgcn_sched_group_barrier(0x402, DI_PIPE32_NV, 0);  // VALU | TRANS
-      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);             // DS read
-      if (s < NS) __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
-    }
-    __builtin_amdgcn_sched_barrier(0);
-  }
 }
 
 }  // namespace di

@@ -30,6 +30,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include "common.h"
+#include "pair_queue.h"
 #include "../../include/deepinteract_amd.h"
 
 namespace di {
@@ -37,30 +38,8 @@ namespace di {
 constexpr int PAIR_THREADS = 256;   // k_pair_vec / k_pair_flat
 constexpr int PAIR_CHUNK = 65536;   // elements per k_pair_vec / k_pair_flat work item
 constexpr int PAIR_UNROLL = 4;
-#ifndef DI_PAIR_INFLIGHT
-#define DI_PAIR_INFLIGHT 3
-#endif
-constexpr int PAIR_INFLIGHT = DI_PAIR_INFLIGHT;  // stores in flight per wave when beside GeoT
-// beside GeoT: the store waves' s_setprio (round 4 experiment; 0 = the default priority)
-#ifndef DI_PAIR_PRIO
-#define DI_PAIR_PRIO 0
-#endif
-// beside GeoT: the partial 128-B lines at row boundaries as plain stores, the rest non-temporal
-// (round 4 experiment; 0 = every store non-temporal, the round-3 form)
-// chain-1 planes as contiguous whole-line runs (round 4 experiment; 0 = row streaming) and the
-// cache policy of those stores beside GeoT
-#ifndef DI_PAIR_C1RUN
-#define DI_PAIR_C1RUN 0
-#endif
-#ifndef DI_PAIR_C1BOUND
-#define DI_PAIR_C1BOUND 1
-#endif
-#ifndef DI_PAIR_C1CPOL
-#define DI_PAIR_C1CPOL DI_PAIR_CPOL
-#endif
-#ifndef DI_PAIR_EDGE_PLAIN
-#define DI_PAIR_EDGE_PLAIN 0
-#endif
+// stores in flight per wave beside GeoT (rounds 2-4: 2 / 4 / 5 slower or equal)
+constexpr int PAIR_INFLIGHT = 3;
 constexpr int PAIR_SEG = 128;       // 16-B chunks per row segment of k_pair_rows (2 per lane)
 constexpr int PAIR_MAX_PLANE_ROWS = 1 << 20;  // k_pair_vec / k_pair_flat row index from an fp32 quotient
 
@@ -83,14 +62,10 @@ template <bool BESIDE>
 __device__ __forceinline__ void pair_bound() {
   if constexpr (BESIDE) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PAIR_INFLIGHT) : "memory");
 }
-// CPol bits of the 16-B buffer stores: non-temporal beside GeoT, plain alone. DI_PAIR_CPOL (round 4
-// experiment) replaces the beside value: 16 = sc1, 17 = sc0 sc1, 18 = sc1 nt (sc1 stores drop the
-// line from the XCD's L2 instead of keeping it, MI355X_MICROARCH.md, store flavours)
-#ifndef DI_PAIR_CPOL
-#define DI_PAIR_CPOL 2
-#endif
+// CPol bits of the 16-B buffer stores: non-temporal (nt = 2) beside GeoT, plain alone. Measured beside
+// GeoT (rounds 2-4): plain, sc0, sc1, sc0 sc1 and sc1 nt all slower than nt
 template <bool BESIDE>
-constexpr int pair_cpol() { return BESIDE ? DI_PAIR_CPOL : 0; }
+constexpr int pair_cpol() { return BESIDE ? 2 : 0; }
 
 // (row, column) of flat plane position q: the fp32 quotient is within one of q / l2 for
 // q / l2 < 2^20 (PAIR_MAX_PLANE_ROWS) and corrected with two selects; the remainder is exact
@@ -200,23 +175,72 @@ __device__ __forceinline__ uint32_t pair_bcast_bits<float>(const float* p) {
 }
 
 // ---- 16-B aligned planes: row streaming ------------------------------------------------------
-// A work item is (complex, channel, 64 x waves rows); a wave owns a contiguous run of 64 rows. Per
-// 128-chunk segment of the row it loads what its rows need ONCE (two 16-B row-vector pieces per
-// lane, or one chain-1 value per row, one per lane, broadcast with readlane), then issues only
-// stores: buffer_store_dwordx4 with a per-lane constant voffset and the row offset in an SGPR.
+// One wave streams rows [r0, r1) (<= 64; none when r0 >= r1) of channel plane c of complex d. Per
+// 128-chunk segment of the row it loads what its rows need ONCE -- two 16-B pieces of the chain-2 row
+// vector hT[c - H, :] per lane, or one chain-1 value hT[c, h1_row + i] per row, one per lane (a
+// coalesced 128-B load), broadcast with readlane -- then issues only stores: buffer_store_dwordx4 with
+// a per-lane constant voffset and the row offset in an SGPR. hT is the transposed node-feature matrix
+// [H, nrows] of di_node_layer's hT_out, bit-identical to h (the same bf16 rounding of the same value).
+// hook(): called exactly once, unconditionally, after the first segment's loads have landed and before
+// the first store (the queue kernel issues its next-ticket atomic there: behind the item's loads, ahead
+// of all its stores). Returns the number of store instructions issued after hook().
+template <typename T, bool BESIDE, class F>
+__device__ __forceinline__ int pair_rows_item(const di_pair_desc& d, int c, int r0, int r1, int hidden,
+                                              const T* __restrict__ hT, int nrows, T* __restrict__ out, int lane,
+                                              F&& hook) {
+  using V = typename Vec16<T>::V;
+  constexpr int VEC = Vec16<T>::N;
+  const int nch = d.l2 / VEC;  // 16-B chunks per row
+  const uint32_t pitch = (uint32_t)d.l2 * sizeof(T);
+  T* o = out + d.out_off + (int64_t)c * ((int64_t)d.l1 * d.l2);
+  const __amdgpu_buffer_rsrc_t r = buf_rsrc(o);
+  const bool second = c >= hidden;
+  const bool any = r0 < r1;  // uniform
+  uint32_t hv = 0;           // chain 1: lane l holds the value of row r0 + l
+  if (!second && r0 + lane < r1) hv = pair_bcast_bits<T>(hT + (int64_t)c * nrows + d.h1_row + r0 + lane);
+  const T* src = hT + (int64_t)(c - hidden) * nrows + d.h2_row;
+  V v0 = {}, v1 = {};
+  if (second && any) {  // segment 0's chain-2 pieces
+    if (lane < nch) v0 = *reinterpret_cast<const V*>(src + lane * VEC);
+    if (64 + lane < nch) v1 = *reinterpret_cast<const V*>(src + (64 + lane) * VEC);
+  }
+  asm volatile("" ::"v"(hv), "v"(v0), "v"(v1));  // the loads land here, before hook()
+  hook();
+  int after = 0;
+  for (int seg = 0; seg < nch; seg += PAIR_SEG) {
+    const int k0 = seg + lane, k1 = seg + 64 + lane;  // this lane's chunks of the segment
+    const bool two = seg + 64 < nch;                  // uniform: the segment has a second piece
+    if (second && any && seg > 0) {
+      if (k0 < nch) v0 = *reinterpret_cast<const V*>(src + k0 * VEC);
+      if (k1 < nch) v1 = *reinterpret_cast<const V*>(src + k1 * VEC);
+    }
+    for (int i = r0; i < r1; ++i) {
+      const int soff = (int)(i * pitch);
+      if (!second) {
+        const uint32_t b = (uint32_t)__builtin_amdgcn_readlane((int)hv, i - r0);
+        v0 = __builtin_bit_cast(V, (uintx4){b, b, b, b});
+        v1 = v0;
+      }
+      if (k0 < nch)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uintx4, v0), r, k0 * 16, soff, pair_cpol<BESIDE>());
+      if (two && k1 < nch)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uintx4, v1), r, k1 * 16, soff, pair_cpol<BESIDE>());
+      pair_bound<BESIDE>();
+      after += two ? 2 : 1;
+    }
+  }
+  return after;
+}
+
+// A work item is (complex, channel, 64 x waves rows); a wave owns a contiguous run of 64 rows.
 // <= 32 VGPRs: one wave per SIMD co-resides with the edge kernels (2 x 240 VGPRs).
 template <typename T, bool BESIDE>
 __global__ __launch_bounds__(1024) __attribute__((amdgpu_num_vgpr(32)))
-void k_pair_rows(const di_pair_desc* __restrict__ descs, int hidden, const T* __restrict__ h,
-                 const T* __restrict__ hT, int nrows, int rblocks, int items, T* __restrict__ out) {
-  using V = typename Vec16<T>::V;
-  constexpr int VEC = Vec16<T>::N;
+void k_pair_rows(const di_pair_desc* __restrict__ descs, int hidden, const T* __restrict__ hT, int nrows, int rblocks,
+                 int items, T* __restrict__ out) {
   const int rows_per_item = (int)blockDim.x;  // 64 per wave
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  // beside GeoT: the store wave's few instructions (one store per 1 KiB) win the SIMD's issue
-  // arbitration against the co-resident, VALU-dense GeoT waves (round 4 experiment)
-  if constexpr (BESIDE && DI_PAIR_PRIO > 0) __builtin_amdgcn_s_setprio(DI_PAIR_PRIO);
   for (int item = blockIdx.x; item < items; item += gridDim.x) {
     const int rb = item % rblocks;
     const int rest = item / rblocks;
@@ -225,82 +249,186 @@ void k_pair_rows(const di_pair_desc* __restrict__ descs, int hidden, const T* __
     const int r0 = rb * rows_per_item + 64 * wave;  // this wave's rows [r0, r1)
     const int r1 = r0 + 64 < d.l1 ? r0 + 64 : d.l1;
     if (r0 >= r1) continue;  // uniform per wave
-    const int nch = d.l2 / VEC;  // 16-B chunks per row
-    const uint32_t pitch = (uint32_t)d.l2 * sizeof(T);
-    T* o = out + d.out_off + (int64_t)c * ((int64_t)d.l1 * d.l2);
-    const __amdgpu_buffer_rsrc_t r = buf_rsrc(o);
-    const bool second = c >= hidden;
-    uint32_t hv = 0;  // chain 1: lane l holds the value of row r0 + l
-    if (!second && r0 + lane < r1) hv = pair_bcast_bits<T>(h + (d.h1_row + r0 + lane) * hidden + c);
-    if constexpr (DI_PAIR_C1RUN) {
-      // chain 1 (round 4 experiment): the wave's rows as ONE contiguous run of 1-KiB stores, so every
-      // 128-B line inside the run is written whole by one instruction (no row-boundary partial
-      // lines); a store spans at most two rows (pitch >= 1 KiB), whose values come by readlane
-      if (!second && pitch >= 1024u) {  // uniform
-        const uint32_t nr = (uint32_t)(r1 - r0), run = nr * pitch;
-        const int base = (int)((uint32_t)r0 * pitch);
-        uint32_t lo = 0, bnd = pitch;  // first row of the store, run offset where row lo + 1 starts
-        for (uint32_t off = 0; off < run; off += 1024u) {
-          if (bnd <= off) {
-            ++lo;
-            bnd += pitch;
-          }
-          const uint32_t va = (uint32_t)__builtin_amdgcn_readlane((int)hv, (int)lo);
-          const uint32_t vb = lo + 1 < nr ? (uint32_t)__builtin_amdgcn_readlane((int)hv, (int)lo + 1) : va;
-          const uint32_t my = off + 16u * (uint32_t)lane;
-          const uint32_t v = my < bnd ? va : vb;
-          if (my < run)
-            __builtin_amdgcn_raw_buffer_store_b128((uintx4){v, v, v, v}, r, 16 * lane, base + (int)off,
-                                                   BESIDE ? DI_PAIR_C1CPOL : 0);
-          // the bound after every DI_PAIR_C1BOUND-th store (row streaming: after each row's two)
-          if (((off >> 10) + 1) % DI_PAIR_C1BOUND == 0) pair_bound<BESIDE>();
-        }
-        continue;
-      }
+    pair_rows_item<T, BESIDE>(d, c, r0, r1, hidden, hT, nrows, out, lane, [] {});
+  }
+}
+
+// ---- the pair-tensor queue: the overlapped schedule's pair stream ---------------------------------
+// Jobs (one micro-batch's pair tensors each, di_pair_job) are produced in order by the GeoT stream:
+// di_pair_signal(job) after the job's final node layer raises the queue's READY word to job + 1 (the
+// node layer's kernel end has written its hT back; the signal is a relaxed agent-scope atomic max).
+// Items of job k = (complex, channel, 64-row block), ticket order = memory order of the planes.
+//   k_pair_stream (the pair stream, beside GeoT): one persistent launch over jobs [begin, end); each
+//     wave waits for READY > k (relaxed sc1 poll + s_sleep), acquires (buffer_inv sc1), then takes
+//     tickets of job k until they run out. The next ticket's atomic is issued right after the first
+//     row of the current item and read after its last row -- every row ends with s_waitcnt vmcnt(3),
+//     so an atomic issued >= 4 stores earlier has returned and no wave ever waits for a ticket behind
+//     its own store queue (the round-3 per-item ticket, waited at once, cost 45 % beside GeoT). A wave
+//     that waits longer than `patience` for READY gives up (counted in the queue's GAVE_UP word):
+//     progress never depends on this kernel running concurrently with the producer.
+//   k_pair_help (the producer's stream): takes tickets of jobs [first, last] -- all produced, by stream
+//     order -- with plain unbounded stores on the whole chip, then one wave waits until every item of
+//     those jobs is DONE (items taken by the stream kernel included) and the launch ends. The producer
+//     calls it before reusing an hT ring slot (its jobs' reads are over) and once at the end (drain):
+//     every job is then complete whatever the stream kernel did. When the GeoT stream runs ahead, the
+//     help launches convert its idle time into pair-tensor stores at the full-chip rate.
+// Queue words: csrc/pair_queue.h. The producer signals job j with the standalone di_pair_signal launch,
+// or (no launch of its own) at the start of its next launch: the node embedding / embedding + InitEdge
+// of job j + 1 or a help launch (pq_signal_at_start) -- the kernel boundary has released hT.
+// wave-uniform copies (readfirstlane): the compiler's divergence analysis treats every value downstream
+// of an atomic as divergent and would wrap each buffer store in a waterfall loop over its resource
+__device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
+__device__ __forceinline__ int64_t uni(int64_t x) {
+  const uint64_t u = (uint64_t)x;
+  return (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(u >> 32)) << 32) |
+                   (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)u));
+}
+template <typename P>
+__device__ __forceinline__ P* uni(P* p) {
+  return reinterpret_cast<P*>(uni((int64_t)reinterpret_cast<uintptr_t>(p)));
+}
+__device__ __forceinline__ di_pair_job uni(const di_pair_job& j) {
+  di_pair_job u;
+  u.hT = uni(j.hT);
+  u.descs = uni(j.descs);
+  u.out = uni(j.out);
+  u.num_rows = uni(j.num_rows);
+  u.num_complexes = uni(j.num_complexes);
+  u.max_l1 = uni(j.max_l1);
+  u.items = uni(j.items);
+  return u;
+}
+
+__device__ __forceinline__ uint32_t pq_load(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// lane 0 takes the next ticket (returning atomic, waited here); uniform result
+__device__ __forceinline__ uint32_t pq_take(uint32_t* tick, int lane) {
+  uint32_t t = 0;
+  if (lane == 0) t = __hip_atomic_fetch_add(tick, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return (uint32_t)__builtin_amdgcn_readlane((int)t, 0);
+}
+// the same atomic issued with exec = lane 0 inside one asm statement and NOT waited for: the compiler
+// sees a VALU-defined register and inserts no s_waitcnt; the caller reads it (pq_read) only once the
+// wave's own in-order vmcnt has passed it. One statement (no branch) so no phi copy of the register
+// can be placed between issue and return.
+__device__ __forceinline__ uint32_t pq_take_async(uint32_t* tick) {
+  uint32_t t;
+  uint64_t save;
+  asm volatile(
+      "s_mov_b64 %1, exec\n\t"
+      "s_mov_b64 exec, 1\n\t"
+      "global_atomic_add %0, %2, %3, off sc0\n\t"
+      "s_mov_b64 exec, %1"
+      : "=&v"(t), "=&s"(save)
+      : "v"(tick), "v"(1u)
+      : "memory");
+  return t;
+}
+__device__ __forceinline__ uint32_t pq_read(uint32_t t, bool waited) {
+  if (!waited) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  asm volatile("" : "+v"(t));  // not read before the wait above
+  return (uint32_t)__builtin_amdgcn_readlane((int)t, 0);
+}
+// item t of job J -> (complex descriptor, channel, rows [r0, r1)); false: an empty item (r0 >= r1:
+// a row block past a smaller complex's chain 1, or a ticket past the descriptors)
+__device__ __forceinline__ bool pq_item(const di_pair_job& J, int hidden, uint32_t t, di_pair_desc& d, int& c, int& r0,
+                                        int& r1) {
+  const int rblocks = (J.max_l1 + 63) >> 6;
+  const int rb = (int)(t % (uint32_t)rblocks);
+  const int rest = (int)(t / (uint32_t)rblocks);
+  c = rest % (2 * hidden);
+  const int cx = rest / (2 * hidden);
+  const bool in = cx < J.num_complexes;
+  const di_pair_desc dd = J.descs[in ? cx : 0];
+  d.h1_row = uni(dd.h1_row);
+  d.h2_row = uni(dd.h2_row);
+  d.out_off = uni(dd.out_off);
+  d.l1 = uni(dd.l1);
+  d.l2 = uni(dd.l2);
+  c = uni(c);
+  r0 = uni(rb * 64);
+  r1 = uni(!in ? r0 : (r0 + 64 < d.l1 ? r0 + 64 : d.l1));
+  return r0 < r1;
+}
+// wait until *p >= need, at most `patience` ticks of the 100-MHz realtime clock
+__device__ __forceinline__ bool pq_wait(const uint32_t* p, uint32_t need, uint64_t patience) {
+  if (pq_load(p) >= need) return true;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  while (pq_load(p) < need) {
+    __builtin_amdgcn_s_sleep(8);
+    if (__builtin_amdgcn_s_memrealtime() - t0 > patience) return false;
+  }
+  return true;
+}
+
+template <typename T>
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_num_vgpr(32)))
+void k_pair_stream(const di_pair_job* __restrict__ jobs, int hidden, uint32_t* __restrict__ q, int job_begin,
+                   int job_end, uint64_t patience) {
+  const int lane = threadIdx.x & 63;
+  for (int k = job_begin; k < job_end; ++k) {
+    if (!pq_wait(q + PQ_READY, (uint32_t)k + 1, patience)) {
+      if (lane == 0) __hip_atomic_fetch_add(q + PQ_GAVE_UP, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return;  // the producer's help launches complete what is left
     }
-    const T* src = hT + (int64_t)(c - hidden) * nrows + d.h2_row;
-    for (int seg = 0; seg < nch; seg += PAIR_SEG) {
-      const int k0 = seg + lane, k1 = seg + 64 + lane;  // this lane's chunks of the segment
-      const bool two = seg + 64 < nch;                  // uniform: the segment has a second piece
-      V v0, v1;
-      if (second) {
-        if (k0 < nch) v0 = *reinterpret_cast<const V*>(src + k0 * VEC);
-        if (k1 < nch) v1 = *reinterpret_cast<const V*>(src + k1 * VEC);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // hT of job k as the producer wrote it
+    const di_pair_job J = uni(jobs[k]);
+    uint32_t* tick = pq_ticket(q, k);
+    uint64_t bytes = 0;
+    uint32_t t = pq_take(tick, lane);
+    while (t < (uint32_t)J.items) {
+      di_pair_desc d;
+      int c = 0, r0 = 0, r1 = 0;
+      pq_item(J, hidden, t, d, c, r0, r1);
+      uint32_t tn = 0;
+      const int after = pair_rows_item<T, true>(d, c, r0, r1, hidden, reinterpret_cast<const T*>(J.hT), J.num_rows,
+                                                reinterpret_cast<T*>(J.out), lane, [&] { tn = pq_take_async(tick); });
+      bytes += r1 > r0 ? (uint64_t)(r1 - r0) * d.l2 * sizeof(T) : 0;
+      // >= PAIR_INFLIGHT + 1 stores after the atomic and a vmcnt(PAIR_INFLIGHT) after the last one
+      t = pq_read(tn, after > PAIR_INFLIGHT);
+      if (lane == 0) __hip_atomic_fetch_add(pq_done(q, k), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (lane == 0 && bytes)
+      __hip_atomic_fetch_add(reinterpret_cast<uint64_t*>(q + PQ_SBYTES), bytes, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_num_vgpr(32)))
+void k_pair_help(const di_pair_job* __restrict__ jobs, int hidden, uint32_t* __restrict__ q, int first, int last,
+                 int signal_job, uint64_t patience) {
+  pq_signal_at_start(q, signal_job);
+  const int lane = threadIdx.x & 63;
+  uint64_t bytes = 0;
+  for (int k = first; k <= last; ++k) {
+    const di_pair_job J = uni(jobs[k]);
+    uint32_t* tick = pq_ticket(q, k);
+    for (uint32_t t = pq_take(tick, lane); t < (uint32_t)J.items; t = pq_take(tick, lane)) {
+      di_pair_desc d;
+      int c = 0, r0 = 0, r1 = 0;
+      if (pq_item(J, hidden, t, d, c, r0, r1)) {
+        pair_rows_item<T, false>(d, c, r0, r1, hidden, reinterpret_cast<const T*>(J.hT), J.num_rows,
+                                 reinterpret_cast<T*>(J.out), lane, [] {});
+        bytes += (uint64_t)(r1 - r0) * d.l2 * sizeof(T);
       }
-      for (int i = r0; i < r1; ++i) {
-        const int soff = (int)(i * pitch);
-        if (!second) {
-          const uint32_t b = (uint32_t)__builtin_amdgcn_readlane((int)hv, i - r0);
-          v0 = __builtin_bit_cast(V, (uintx4){b, b, b, b});
-          v1 = v0;
-        }
-        if constexpr (BESIDE && DI_PAIR_EDGE_PLAIN) {
-          // the row's first / last 128-B line is shared with the neighbouring row when the row does
-          // not start / end on a line: those chunks go out as plain stores (the two halves of the line
-          // merge in L2), every other chunk non-temporal -- nt stores write both halves through
-          const uint32_t rb = (uint32_t)(uintptr_t)o + (uint32_t)soff;  // the row's address (line phase only)
-          const uint32_t head = (128u - (rb & 127u)) & 127u;                    // bytes before the first line boundary
-          const uint32_t tail = (rb + pitch) & 127u;                            // bytes after the last one
-          const bool e0 = (uint32_t)(k0 * 16) < head || (uint32_t)(k0 * 16) >= pitch - tail;
-          const bool e1 = (uint32_t)(k1 * 16) < head || (uint32_t)(k1 * 16) >= pitch - tail;
-          if (k0 < nch && !e0)
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uintx4, v0), r, k0 * 16, soff, 2);
-          if (k0 < nch && e0)
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uintx4, v0), r, k0 * 16, soff, 0);
-          if (two && k1 < nch && !e1)
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uintx4, v1), r, k1 * 16, soff, 2);
-          if (two && k1 < nch && e1)
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uintx4, v1), r, k1 * 16, soff, 0);
-        } else {
-          if (k0 < nch)
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uintx4, v0), r, k0 * 16, soff, pair_cpol<BESIDE>());
-          if (two && k1 < nch)
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uintx4, v1), r, k1 * 16, soff, pair_cpol<BESIDE>());
-        }
-        pair_bound<BESIDE>();
-      }
+      if (lane == 0) __hip_atomic_fetch_add(pq_done(q, k), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
+  if (lane == 0 && bytes)
+    __hip_atomic_fetch_add(reinterpret_cast<uint64_t*>(q + PQ_HBYTES), bytes, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // one wave holds the launch open until every item of [first, last] is done (taken by either kernel)
+  if (blockIdx.x != 0 || threadIdx.x >= 64) return;
+  for (int k = first; k <= last; ++k) {
+    if (!pq_wait(pq_done(q, k), (uint32_t)jobs[k].items, patience)) {
+      if (lane == 0) __hip_atomic_fetch_or(q + PQ_ERROR, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
+  }
+}
+
+__global__ void k_pair_signal(uint32_t* __restrict__ q, uint32_t ready) {
+  if (threadIdx.x == 0) __hip_atomic_fetch_max(q + PQ_READY, ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ---- 128-B aligned planes: whole-line streaming -------------------------------------------------
@@ -452,11 +580,11 @@ extern "C" int di_pair_tensor(di_dtype dt, const di_pair_desc* descs, int32_t nu
     const int items = planes * rblocks;
     const dim3 g = grid_of(items), b(rows);
     if (dt == DI_BF16) {
-      if (beside) hipLaunchKernelGGL((k_pair_rows<u16, true>), g, b, 0, s, descs, hidden, (const u16*)h, (const u16*)hT, num_rows, rblocks, items, (u16*)out);
-      else hipLaunchKernelGGL((k_pair_rows<u16, false>), g, b, 0, s, descs, hidden, (const u16*)h, (const u16*)hT, num_rows, rblocks, items, (u16*)out);
+      if (beside) hipLaunchKernelGGL((k_pair_rows<u16, true>), g, b, 0, s, descs, hidden, (const u16*)hT, num_rows, rblocks, items, (u16*)out);
+      else hipLaunchKernelGGL((k_pair_rows<u16, false>), g, b, 0, s, descs, hidden, (const u16*)hT, num_rows, rblocks, items, (u16*)out);
     } else {
-      if (beside) hipLaunchKernelGGL((k_pair_rows<float, true>), g, b, 0, s, descs, hidden, (const float*)h, (const float*)hT, num_rows, rblocks, items, (float*)out);
-      else hipLaunchKernelGGL((k_pair_rows<float, false>), g, b, 0, s, descs, hidden, (const float*)h, (const float*)hT, num_rows, rblocks, items, (float*)out);
+      if (beside) hipLaunchKernelGGL((k_pair_rows<float, true>), g, b, 0, s, descs, hidden, (const float*)hT, num_rows, rblocks, items, (float*)out);
+      else hipLaunchKernelGGL((k_pair_rows<float, false>), g, b, 0, s, descs, hidden, (const float*)hT, num_rows, rblocks, items, (float*)out);
     }
   } else {
     const int chunks = (int)(((int64_t)max_l1 * max_l2 + PAIR_CHUNK - 1) / PAIR_CHUNK);
@@ -470,6 +598,68 @@ extern "C" int di_pair_tensor(di_dtype dt, const di_pair_desc* descs, int32_t nu
       else hipLaunchKernelGGL(k_pair_flat<float>, g, b, 0, s, descs, hidden, (const float*)h, (const float*)hT, num_rows, chunks, items, (float*)out);
     }
   }
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? DI_OK : (int)e;
+}
+
+// ---- the pair-tensor queue (C ABI) ------------------------------------------------------------
+static inline int64_t pq_bytes(int64_t jobs) { return 4 * (PQ_HEAD_WORDS + PQ_JOB_WORDS * jobs); }
+
+extern "C" int64_t di_pair_queue_bytes(int32_t num_jobs) { return num_jobs > 0 ? pq_bytes(num_jobs) : -1; }
+
+extern "C" int32_t di_pair_job_items(int32_t num_complexes, int32_t max_l1, int32_t hidden) {
+  if (num_complexes <= 0 || max_l1 <= 0 || hidden <= 0) return DI_EINVAL;
+  const int64_t n = (int64_t)num_complexes * 2 * hidden * ((max_l1 + 63) / 64);
+  return n > INT32_MAX ? DI_ERANGE : (int32_t)n;
+}
+
+// ticks of the 100-MHz-class realtime clock (s_memrealtime) in `ms` milliseconds on this device
+static uint64_t pq_ticks(double ms) {
+  int dev = 0, khz = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess ||
+      khz <= 0)
+    khz = 100000;
+  return (uint64_t)(ms * khz);
+}
+
+extern "C" int di_pair_signal(void* queue, int32_t job, void* stream) {
+  if (!queue || job < 0) return DI_EINVAL;
+  hipLaunchKernelGGL(k_pair_signal, dim3(1), dim3(64), 0, (hipStream_t)stream, (uint32_t*)queue, (uint32_t)job + 1);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? DI_OK : (int)e;
+}
+
+extern "C" int di_pair_stream(di_dtype dt, const di_pair_job* jobs, int32_t job_begin, int32_t job_end, int32_t hidden,
+                              void* queue, const di_pair_launch* launch, float patience_ms, void* stream) {
+  if (!jobs || !queue || job_begin < 0 || job_end <= job_begin || hidden <= 0 || (dt != DI_BF16 && dt != DI_F32) ||
+      !(patience_ms > 0.f))
+    return DI_EINVAL;
+  const int blocks = launch && launch->blocks > 0 ? launch->blocks : (device_cus() + 1) / 2;
+  const int waves = launch && launch->waves_per_block > 0 ? launch->waves_per_block : 4;
+  if (waves > 16) return DI_EINVAL;
+  const dim3 g((unsigned)blocks), b((unsigned)(64 * waves));
+  hipStream_t s = (hipStream_t)stream;
+  const uint64_t pt = pq_ticks(patience_ms);
+  if (dt == DI_BF16) hipLaunchKernelGGL(k_pair_stream<u16>, g, b, 0, s, jobs, hidden, (uint32_t*)queue, job_begin, job_end, pt);
+  else hipLaunchKernelGGL(k_pair_stream<float>, g, b, 0, s, jobs, hidden, (uint32_t*)queue, job_begin, job_end, pt);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? DI_OK : (int)e;
+}
+
+extern "C" int di_pair_help(di_dtype dt, const di_pair_job* jobs, int32_t first_job, int32_t last_job, int32_t hidden,
+                            void* queue, const di_pair_launch* launch, int32_t signal_job, void* stream) {
+  if (!jobs || !queue || first_job < 0 || last_job < first_job || hidden <= 0 || (dt != DI_BF16 && dt != DI_F32))
+    return DI_EINVAL;
+  const int blocks = launch && launch->blocks > 0 ? launch->blocks : device_cus();
+  const int waves = launch && launch->waves_per_block > 0 ? launch->waves_per_block : 8;
+  if (waves > 16) return DI_EINVAL;
+  const dim3 g((unsigned)blocks), b((unsigned)(64 * waves));
+  hipStream_t s = (hipStream_t)stream;
+  const uint64_t pt = pq_ticks(10000.0);  // a completion wait this long is an error (ERROR bit 0), never a hang
+  if (dt == DI_BF16)
+    hipLaunchKernelGGL(k_pair_help<u16>, g, b, 0, s, jobs, hidden, (uint32_t*)queue, first_job, last_job, signal_job, pt);
+  else
+    hipLaunchKernelGGL(k_pair_help<float>, g, b, 0, s, jobs, hidden, (uint32_t*)queue, first_job, last_job, signal_job, pt);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? DI_OK : (int)e;
 }

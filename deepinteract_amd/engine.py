@@ -92,16 +92,10 @@ class GeoTEngine:
         # di_node_layer): the segment reduction (16 lanes per destination) at full occupancy instead
         # of inside the MFMA kernel's one-block-per-CU grid
         self.split_node = True
-        # optional side stream for the node embedding (concurrent with InitEdge)
-        self.embed_stream = None
         # reference-featurised batches: node embedding as the first blocks of the InitEdge launch
         # (di_embed_init_edge, bf16 or fp32) instead of a separate launch (default, round 4: serial
         # 101 us for both vs 19 + 108 us with the resident InitEdge after the embedding)
         self.fuse_embed_init = True
-        # optional stream for the node layers (bench --node-cus: CU-masked to the CUs the pair-tensor
-        # stream does not use); None: the launch stream
-        self.node_stream = None
-        self._ev_edge, self._ev_node = torch.cuda.Event(), torch.cuda.Event()
 
     def _check_blob_sizes(self):
         p, dt = self.packed, _DI_DT[self.dtype]
@@ -156,21 +150,28 @@ class GeoTEngine:
         }
         return views
 
-    def forward(self, gb: GraphBatch, clone: bool = True, events=None, slot: int = 0, after_init=None):
+    def forward(self, gb: GraphBatch, clone: bool = True, events=None, slot: int = 0, hT_out=None, signal=None):
         """-> (node feats [Nt,128], edge feats [Et,128]) in the engine dtype.
 
         events: optional dict kernel-name -> list; (start, end) torch.cuda.Event pairs are recorded
         around every launch on the launch stream (for per-kernel timing in bench.py).
-        after_init: optional torch.cuda.Event recorded right after the InitEdge launch (lets a
-        concurrent HBM-bound consumer start once the memory-heavy prologue has passed)."""
+        hT_out: optional [128, Nt] buffer for the transposed final node features (the pair tensor's
+        input; default: the slot's own). Either way it is self.last_hT afterwards.
+        signal: optional (pair-queue state tensor, job): this forward's first launch marks `job` ready
+        at its start -- a previous forward's hT, complete by stream order (include/deepinteract_amd.h,
+        pair-tensor queue: the signal_job argument)."""
         lib, p, dt = self.lib, self.packed, _DI_DT[self.dtype]
         check_on(self.device, "GeoTEngine.forward", gb.src, gb.dst, gb.nbr, gb.node_f, gb.edge_f,
-                 gb.node_pos, gb.in_ptr)
+                 gb.node_pos, gb.in_ptr, hT_out)
         if max(gb.nodes_per_graph) > p.pos_src.shape[0]:
             # InitEdge gathers positional rows node_pos < max_num_graph_nodes (nn.Embedding, :153, :210)
             raise IndexError(f"chain of {max(gb.nodes_per_graph)} residues exceeds this model's "
                              f"max_num_graph_nodes={p.pos_src.shape[0]}")
         ws = self.workspace(gb.num_nodes, gb.num_edges, slot)
+        if hT_out is not None and (hT_out.shape != (self.cfg.num_gnn_hidden_channels, gb.num_nodes)
+                                   or hT_out.dtype != _TORCH_DT[self.dtype] or not hT_out.is_contiguous()):
+            raise ValueError("hT_out must be a contiguous [128, num_nodes] tensor of the engine dtype")
+        hT = ws["hT"] if hT_out is None else hT_out
         g = ctypes.byref(gb.c_graph)
         st = _stream()
         h, qkv, f, fn, alpha = ws["h"], ws["qkv"], ws["f"], ws["fn"], ws["alpha"]
@@ -179,51 +180,29 @@ class GeoTEngine:
         # written nor read
         if gb.geo_ref:
             fn = [None, None]
+        sq, sjob = (_ptr(signal[0]), int(signal[1])) if signal is not None else (_ptr(None), -1)
         tick = _Ticker(events)
-        fused = self.fuse_embed_init and gb.geo_ref
-        if fused:
+        if self.fuse_embed_init and gb.geo_ref:
             tick("init_edge")
             _lib.check(lib.di_embed_init_edge(g, dt, gb.node_f.shape[1], _ptr(gb.node_f), _ptr(p.embed[0]), _ptr(p.embed[1]),
                                               _ptr(h[0]), _ptr(qkv[0]), _ptr(gb.edge_f), _ptr(p.init[0]),
-                                              _ptr(p.init[1]), _ptr(p.pos_src), _ptr(p.pos_dst), _ptr(f[0]), st),
-                       "di_embed_init_edge")
-            ev1 = None
-        elif self.embed_stream is not None:
-            # node embedding (+ layer-0 Q/K/V) on a side stream, concurrent with InitEdge (which does
-            # not read it); the edge layer waits for both
-            cur = torch.cuda.current_stream()
-            ev0 = torch.cuda.Event()
-            ev0.record(cur)
-            with torch.cuda.stream(self.embed_stream):
-                self.embed_stream.wait_event(ev0)
-                _lib.check(lib.di_node_embed(g, dt, gb.node_f.shape[1], _ptr(gb.node_f), _ptr(p.embed[0]),
-                                             _ptr(p.embed[1]), _ptr(h[0]), _ptr(qkv[0]), _stream()), "di_node_embed")
-                ev1 = torch.cuda.Event()
-                ev1.record(self.embed_stream)
+                                              _ptr(p.init[1]), _ptr(p.pos_src), _ptr(p.pos_dst), _ptr(f[0]), sq, sjob,
+                                              st), "di_embed_init_edge")
         else:
             tick("node_embed")
             _lib.check(lib.di_node_embed(g, dt, gb.node_f.shape[1], _ptr(gb.node_f), _ptr(p.embed[0]),
-                                         _ptr(p.embed[1]), _ptr(h[0]), _ptr(qkv[0]), st), "di_node_embed")
-            ev1 = None
-        if fused:
-            pass
-        elif self.dtype == "bf16" and gb.geo_ref and self.embed_stream is None:
+                                         _ptr(p.embed[1]), _ptr(h[0]), _ptr(qkv[0]), sq, sjob, st), "di_node_embed")
             tick("init_edge")
-            # the path's InitEdge weights resident in LDS (one block per CU): faster alone; beside the
-            # side-stream node embedding (an LDS-staged kernel that cannot share its CU) the staged
-            # kernel is used instead
-            _lib.check(lib.di_init_edge_resident(g, _ptr(gb.edge_f), _ptr(p.init[0]), _ptr(p.init[1]),
-                                                 _ptr(p.pos_src), _ptr(p.pos_dst), _ptr(f[0]), st),
-                       "di_init_edge_resident")
-        else:
-            tick("init_edge")
-            _lib.check(lib.di_init_edge(g, dt, _ptr(gb.edge_f), _ptr(p.init[0]), _ptr(p.init[1]),
-                                        _ptr(p.pos_src), _ptr(p.pos_dst), _ptr(f[0]), _ptr(fn[0]), st),
-                       "di_init_edge")
-        if after_init is not None:
-            after_init.record(torch.cuda.current_stream())
-        if ev1 is not None:
-            torch.cuda.current_stream().wait_event(ev1)
+            if self.dtype == "bf16" and gb.geo_ref:
+                # the path's InitEdge weights resident in LDS (one block per CU): faster alone than the
+                # staged kernel
+                _lib.check(lib.di_init_edge_resident(g, _ptr(gb.edge_f), _ptr(p.init[0]), _ptr(p.init[1]),
+                                                     _ptr(p.pos_src), _ptr(p.pos_dst), _ptr(f[0]), st),
+                           "di_init_edge_resident")
+            else:
+                _lib.check(lib.di_init_edge(g, dt, _ptr(gb.edge_f), _ptr(p.init[0]), _ptr(p.init[1]),
+                                            _ptr(p.pos_src), _ptr(p.pos_dst), _ptr(f[0]), _ptr(fn[0]), st),
+                           "di_init_edge")
         L = p.num_layers
         cur = 0
         for li in range(L):
@@ -236,35 +215,26 @@ class GeoTEngine:
                                          _ptr(None if final else f[nxt]), _ptr(None if final else fn[nxt]),
                                          st), "di_edge_layer")
             nm, nv = p.node[li]
-            ns = st
-            if self.node_stream is not None:
-                # node layer on its own (e.g. CU-masked) stream, ordered between the edge layers
-                self._ev_edge.record(torch.cuda.current_stream())
-                self.node_stream.wait_event(self._ev_edge)
-                ns = ctypes.c_void_p(self.node_stream.cuda_stream)
             if self.split_node:
                 # CSR segment reduction of the attention messages, then O_node / FFN / next Q,K,V
                 tick("node_aggr")
-                _lib.check(lib.di_node_aggregate(g, dt, _ptr(alpha), _ptr(qkv[cur]), _ptr(ws["attn"]), ns),
+                _lib.check(lib.di_node_aggregate(g, dt, _ptr(alpha), _ptr(qkv[cur]), _ptr(ws["attn"]), st),
                            "di_node_aggregate")
                 tick("node_layer_final" if final else "node_layer")
                 _lib.check(lib.di_node_update(g, dt, int(final), _ptr(ws["attn"]), _ptr(h[cur]), _ptr(nm), _ptr(nv),
                                               _ptr(h[nxt]), _ptr(None if final else qkv[nxt]),
-                                              _ptr(ws["hT"] if final else None), ns), "di_node_update")
+                                              _ptr(hT if final else None), st), "di_node_update")
             else:
                 tick("node_layer_final" if final else "node_layer")
                 _lib.check(lib.di_node_layer(g, dt, int(final), _ptr(alpha), _ptr(h[cur]), _ptr(qkv[cur]),
                                              _ptr(nm), _ptr(nv), _ptr(h[nxt]), _ptr(None if final else qkv[nxt]),
-                                             _ptr(ws["hT"] if final else None), ns), "di_node_layer")
-            if self.node_stream is not None:
-                self._ev_node.record(self.node_stream)
-                torch.cuda.current_stream().wait_event(self._ev_node)
+                                             _ptr(hT if final else None), st), "di_node_layer")
             if not final:
                 f_out = nxt
             cur = nxt
         tick(None)
         node_out = h[cur]
-        self.last_hT = ws["hT"]  # [128, Nt] transposed final node features (pair-tensor input)
+        self.last_hT = hT  # [128, Nt] transposed final node features (pair-tensor input)
         edge_out = f[f_out] if L > 1 else f[0]
         if clone:
             return node_out.clone(), edge_out.clone()

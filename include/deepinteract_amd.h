@@ -16,6 +16,8 @@
  *   di_node_layer   send_and_recv(u_mul_e/copy_e, sum) gSpMM         deepinteract_modules.py:93-96,116
  *                   + O_node / node FFN                               deepinteract_modules.py:696-723, 923-943
  *   di_pair_tensor  construct_interact_tensor (pad=False)            deepinteract_utils.py:158-172
+ *   di_pair_stream / di_pair_help / di_pair_signal: the same, per micro-batch, as a device queue beside
+ *                   the GeoT stream (lit_model_predict.py:236 calls it once per complex)
  *   di_head_prologue  ELU(inorm_1(conv2d_1(T))) of the head, T never materialised
  *                                                                    deepinteract_modules.py:1181-1184, 1228-1232
  *   di_inorm_elu    ELU(InstanceNorm2d(x)) of the head's ResNet blocks deepinteract_modules.py:1016-1030,1075-1095
@@ -45,7 +47,7 @@
 extern "C" {
 #endif
 
-#define DI_ABI_VERSION 5
+#define DI_ABI_VERSION 6
 
 /* activation / weight storage type of the GeoT kernels (accumulation is always fp32). A plain
  * int32 (not a C enum type): a foreign caller may pass any value, and every entry point refuses
@@ -102,18 +104,25 @@ int di_abi_version(void);
  * 2 edge_layer(non-final), 3 edge_layer(final), 4 node_layer(non-final), 5 node_layer(final).
  * `vec` selects the fp32 vector blob (biases) instead of the matrix blob. */
 int64_t di_blob_bytes(int kind, di_dtype dtype, int vec);
-/* MFMA fragment order of a kind's matrix blob in this build (ABI 5): 16 = blocks of 16 output rows
- * x 32 input features (v_mfma_f32_16x16x32_bf16 / 16x16x4_f32 A fragments), 32 = blocks of 32
- * output rows x 16 input features (v_mfma_f32_32x32x16_bf16: the bf16 InitEdge and edge-layer
- * blobs, kinds 1, 2 and 3); -1 for an unknown kind or dtype. Both orders hold the same number of 512-element blocks at
- * the same block offsets (deepinteract_amd/packing.py: pack_matrix / pack_matrix32). */
+/* MFMA fragment order of a kind's matrix blob (ABI 5): 16 = blocks of 16 output rows x 32 input
+ * features (v_mfma_f32_16x16x32_bf16 / 16x16x4_f32 A fragments), 32 = blocks of 32 output rows x 16
+ * input features (v_mfma_f32_32x32x16_bf16: the bf16 InitEdge and edge-layer blobs, kinds 1, 2 and 3;
+ * the kind-1 32 order also carries the DI_GRAPH_GEO_REF orientation constant as a bf16 hi/lo pair in
+ * columns 28/29 of the collapsed message map); -1 for an unknown kind or dtype. Both orders hold the
+ * same number of 512-element blocks at the same block offsets (deepinteract_amd/packing.py:
+ * pack_matrix / pack_matrix32, init_blob / edge_blob with layout = di_blob_layout(kind, dtype)). */
 int di_blob_layout(int kind, di_dtype dtype);
 
 /* in_dim: width of node_f rows (113 for LitGINI's raw node features; 128 with an identity
- * embedding when DGLGeometricTransformer is used standalone on already-embedded features) */
+ * embedding when DGLGeometricTransformer is used standalone on already-embedded features).
+ * queue / signal_job (ABI 6; NULL / -1: none): a pair-queue signal carried by this launch -- at its
+ * start it marks job signal_job ready, i.e. what di_pair_signal(queue, signal_job) issued just before
+ * it on `stream` would do, without that launch (the producer of signal_job's hT must precede this
+ * launch on `stream`). Same pair on di_embed_init_edge and di_pair_help. */
 int di_node_embed(const di_graph* g, di_dtype dt, int32_t in_dim, const float* node_f /*[Nt,in_dim]*/,
                   const void* wmat, const float* wvec,
-                  void* h_out /*[Nt,128]*/, void* qkv_out /*[Nt,384]*/, void* stream);
+                  void* h_out /*[Nt,128]*/, void* qkv_out /*[Nt,384]*/, void* queue, int32_t signal_job,
+                  void* stream);
 
 int di_init_edge(const di_graph* g, di_dtype dt, const float* edge_f /*[Et,28]*/,
                  const void* wmat, const float* wvec,
@@ -134,7 +143,8 @@ int di_init_edge_resident(const di_graph* g, const float* edge_f /*[Et,28]*/, co
 int di_embed_init_edge(const di_graph* g, di_dtype dt, int32_t in_dim, const float* node_f /*[Nt,in_dim]*/,
                        const void* embed_wmat, const float* embed_wvec, void* h_out /*[Nt,128]*/,
                        void* qkv_out /*[Nt,384]*/, const float* edge_f, const void* init_wmat, const float* init_wvec,
-                       const float* pos_src_tab, const float* pos_dst_tab, void* f_out /*[Et,128]*/, void* stream);
+                       const float* pos_src_tab, const float* pos_dst_tab, void* f_out /*[Et,128]*/, void* queue,
+                       int32_t signal_job, void* stream);
 
 int di_edge_layer(const di_graph* g, di_dtype dt, int final_layer, const float* edge_f,
                   const void* f_in, const void* fn_in, const void* qkv,
@@ -189,6 +199,50 @@ int di_pair_tensor(di_dtype dt, const di_pair_desc* descs /*device [B]*/, int32_
  * DI_EINVAL or DI_ERANGE. elem_bytes: 2 (bf16) or 4 (fp32). */
 int di_pair_tensor_check(int32_t num_complexes, int32_t max_l1, int32_t max_l2, int32_t hidden, int32_t elem_bytes,
                          const di_pair_launch* launch);
+
+/* ---- pair-tensor queue (ABI 6): the overlapped schedule's pair stream -----------------------------
+ * A job is one micro-batch's pair tensors (construct_interact_tensor of each complex,
+ * deepinteract_utils.py:158-172), produced by the GeoT stream in job order. The producer stream signals
+ * each job after its final node layer (hT written): with di_pair_signal, or carried by its next launch
+ * (the signal_job argument of di_node_embed / di_embed_init_edge / di_pair_help); it calls
+ * di_pair_help before it reuses a job's hT buffer and once at the end of a run (drain). di_pair_stream is one persistent launch
+ * on its own stream over a range of jobs, beside the producer: its waves wait for each job's signal and
+ * take the job's items (complex, channel, 64-row block) from the queue's per-job ticket counter, with
+ * the bounded non-temporal stores of di_pair_launch.beside. di_pair_help takes the remaining items of
+ * its jobs with plain stores on the whole chip and returns (on the device) once every item of them is
+ * done, whoever took it. Completion never depends on di_pair_stream running concurrently: a stream
+ * wave that waits longer than patience_ms for a signal gives up and the help launches do the rest. The
+ * bytes written are those of di_pair_tensor(aligned = 1) for the same descriptors.
+ * Preconditions (the kernels cannot check device-resident jobs): every job's descs are 16-B aligned
+ * planes (L2 and out_off multiples of 16 bytes of the dtype, h2_row too), hT 16-B aligned, items =
+ * di_pair_job_items(num_complexes, max_l1, hidden), and max_l1 >= every descs[i].l1. */
+typedef struct {
+  const void* hT;             /* [hidden, num_rows] transposed final node features (di_node_layer hT_out) */
+  const di_pair_desc* descs;  /* [num_complexes] (device) */
+  void* out;                  /* base of the job's pair tensors (descs[i].out_off elements from here) */
+  int32_t num_rows;           /* columns of hT: node rows of the micro-batch */
+  int32_t num_complexes;
+  int32_t max_l1;             /* largest chain-1 length of the job */
+  int32_t items;              /* di_pair_job_items(num_complexes, max_l1, hidden) */
+} di_pair_job;
+/* device bytes of a queue for jobs 0 .. num_jobs-1 (zero it before first use; -1 for num_jobs <= 0).
+ * Words (uint32): [0] jobs signalled, [32] error bits (1: a help launch's completion wait timed out),
+ * [33] stream waves that gave up waiting, [40..41] / [42..43] bytes written by stream / help launches
+ * (uint64), then 256 B per job (ticket, arrive, done; csrc/pair_queue.h). */
+int64_t di_pair_queue_bytes(int32_t num_jobs);
+/* items of a job: num_complexes * 2 * hidden * ceil(max_l1 / 64); DI_EINVAL / DI_ERANGE */
+int32_t di_pair_job_items(int32_t num_complexes, int32_t max_l1, int32_t hidden);
+/* the job's hT is complete (stream order of `stream`): raises the queue's signalled count to job + 1 */
+int di_pair_signal(void* queue, int32_t job, void* stream);
+/* persistent pair stream over jobs [job_begin, job_end) (jobs: device array indexed by job number);
+ * launch: blocks (0: half the CUs), waves_per_block (0: 4); always the beside store policy */
+int di_pair_stream(di_dtype dt, const di_pair_job* jobs, int32_t job_begin, int32_t job_end, int32_t hidden,
+                   void* queue, const di_pair_launch* launch, float patience_ms, void* stream);
+/* complete jobs [first_job, last_job] (all produced before this call in `stream` order); launch:
+ * blocks (0: one per CU), waves_per_block (0: 8); signal_job >= 0: also marks that job ready at the
+ * launch's start (as di_node_embed's signal) */
+int di_pair_help(di_dtype dt, const di_pair_job* jobs, int32_t first_job, int32_t last_job, int32_t hidden,
+                 void* queue, const di_pair_launch* launch, int32_t signal_job, void* stream);
 
 /* Fused head prologue: x = ELU(InstanceNorm2d(conv2d_1(T))) of the contact
  * head (ResNet2DInputWithOptAttention.forward, deepinteract_modules.py:1181-1184, 1228-1232) for a

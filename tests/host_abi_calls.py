@@ -69,15 +69,15 @@ def main(path):
     G = _lib.DiGraph
     for g in (G(8, 16, 16, 16, 16, 16, 16, 0), G(0, 0, 16, 16, 16, 16, 16, 0), G(-1, -20, 16, 16, 16, 16, 16, 1)):
         gp = ctypes.byref(g)
-        expect(lib.di_node_embed(gp, 1, 0, p, p, p, p, p, None), EINVAL, "embed in_dim")
-        expect(lib.di_node_embed(gp, 1, 129, p, p, p, p, p, None), EINVAL, "embed in_dim > 128")
-        expect(lib.di_node_embed(gp, 9, 113, p, p, p, p, p, None), EINVAL, "embed dtype")
-        expect(lib.di_node_embed(gp, 1, 113, None, p, p, p, p, None), EINVAL, "embed NULL")
+        expect(lib.di_node_embed(gp, 1, 0, p, p, p, p, p, None, -1, None), EINVAL, "embed in_dim")
+        expect(lib.di_node_embed(gp, 1, 129, p, p, p, p, p, None, -1, None), EINVAL, "embed in_dim > 128")
+        expect(lib.di_node_embed(gp, 9, 113, p, p, p, p, p, None, -1, None), EINVAL, "embed dtype")
+        expect(lib.di_node_embed(gp, 1, 113, None, p, p, p, p, None, -1, None), EINVAL, "embed NULL")
         expect(lib.di_init_edge(gp, 1, p, p, p, p, p, p, None, None), EINVAL, "init Fn")
         expect(lib.di_init_edge(gp, 9, p, p, p, p, p, p, p, None), EINVAL, "init dtype")
         expect(lib.di_init_edge_resident(gp, p, p, p, p, p, None, None), EINVAL, "init resident f_out")
-        expect(lib.di_embed_init_edge(gp, 1, 129, p, p, p, p, p, p, p, p, p, p, p, None), EINVAL, "embed+init in_dim")
-        expect(lib.di_embed_init_edge(gp, 6, 113, p, p, p, p, p, p, p, p, p, p, p, None), EINVAL, "embed+init dtype")
+        expect(lib.di_embed_init_edge(gp, 1, 129, p, p, p, p, p, p, p, p, p, p, p, None, -1, None), EINVAL, "embed+init in_dim")
+        expect(lib.di_embed_init_edge(gp, 6, 113, p, p, p, p, p, p, p, p, p, p, p, None, -1, None), EINVAL, "embed+init dtype")
         expect(lib.di_edge_layer(gp, 1, 0, p, p, None, p, p, p, p, p, p, None), EINVAL, "edge Fn in")
         expect(lib.di_edge_layer(gp, 1, 0, p, p, p, p, p, p, p, p, None, None), EINVAL, "edge Fn out")
         expect(lib.di_edge_layer(gp, 1, 0, p, p, p, p, p, p, p, None, p, None), EINVAL, "edge f_out")

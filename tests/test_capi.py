@@ -25,7 +25,7 @@ def test_library_builds_and_exports_all_declared_symbols():
 
 def test_abi_version_and_blob_sizes():
     lib = _lib.load()
-    assert lib.di_abi_version() == _lib.ABI_VERSION == 5
+    assert lib.di_abi_version() == _lib.ABI_VERSION == 6
     for kind, (nblk, nvec) in packing.BLOB_SIZES.items():
         assert lib.di_blob_bytes(kind, _lib.DI_F32, 0) == nblk * 512 * 4
         assert lib.di_blob_bytes(kind, _lib.DI_BF16, 0) == nblk * 512 * 2
@@ -40,7 +40,7 @@ def test_abi_version_and_blob_sizes():
 
 def test_invalid_arguments_rejected_without_gpu():
     lib = _lib.load()
-    assert lib.di_node_embed(None, 0, 113, None, None, None, None, None, None) == -1
+    assert lib.di_node_embed(None, 0, 113, None, None, None, None, None, None, -1, None) == -1
     assert lib.di_pair_tensor(0, None, 0, 0, 0, 128, 1, None, None, 0, None, None, None) == -1
     assert lib.di_knn_topk(1, None, None, 20, 10, None, None, None) == -1
     assert lib.di_head_prologue(0, None, 1, 8, 8, 128, 128, 1, None, None, None, None, None, 1e-6,
@@ -85,8 +85,8 @@ def test_geo_ref_fn_contract_without_gpu():
     assert lib.di_init_edge(ctypes.byref(g), _lib.DI_BF16, p, p, p, p, p, p, None, None) == -1
     # the resident InitEdge is the DI_GRAPH_GEO_REF path only
     assert lib.di_init_edge_resident(ctypes.byref(g), p, p, p, p, p, p, None) == -1
-    assert lib.di_embed_init_edge(ctypes.byref(g), _lib.DI_BF16, 113, p, p, p, p, p, p, p, p, p, p, p, None) == -1
-    assert lib.di_embed_init_edge(ctypes.byref(g), _lib.DI_F32, 113, p, p, p, p, p, p, p, p, p, p, p, None) == -1
+    assert lib.di_embed_init_edge(ctypes.byref(g), _lib.DI_BF16, 113, p, p, p, p, p, p, p, p, p, p, p, None, -1, None) == -1
+    assert lib.di_embed_init_edge(ctypes.byref(g), _lib.DI_F32, 113, p, p, p, p, p, p, p, p, p, p, p, None, -1, None) == -1
     assert lib.di_edge_layer(ctypes.byref(g), _lib.DI_BF16, 0, p, p, None, p, p, p, p, p, p, None) == -1
     assert lib.di_edge_layer(ctypes.byref(g), _lib.DI_BF16, 0, p, p, p, p, p, p, p, p, None, None) == -1
     assert _lib.DI_GRAPH_GEO_REF == 1
@@ -103,6 +103,31 @@ def test_ctypes_struct_layouts():
     assert ctypes.sizeof(_lib.DiGraph) == 8 + 5 * 8 + 8  # + int32 flags, padded to 8
     assert ctypes.sizeof(_lib.DiPairDesc) == 32
     assert ctypes.sizeof(_lib.DiGeoArgs) == 16 + 8 * 9
+    assert ctypes.sizeof(_lib.DiPairJob) == 3 * 8 + 4 * 4
+
+
+def test_pair_queue_host_contract():
+    """The pair queue's sizes and argument validation (host only, no launch): 256 B of header plus
+    256 B per job; items = complexes x 2H x ceil(L1 / 64); refusals before any launch."""
+    lib = _lib.load()
+    assert lib.di_pair_queue_bytes(1) == 256 + 256
+    assert lib.di_pair_queue_bytes(128) == 256 * 129
+    assert lib.di_pair_queue_bytes(0) == -1
+    assert lib.di_pair_job_items(8, 1000, 128) == 8 * 256 * 16
+    assert lib.di_pair_job_items(2, 4000, 128) == 2 * 256 * 63
+    assert lib.di_pair_job_items(0, 1000, 128) == -1
+    assert lib.di_pair_job_items(1 << 20, 4096, 128) == -2
+    p = ctypes.c_void_p(16)
+    assert lib.di_pair_signal(None, 0, None) == -1
+    assert lib.di_pair_signal(p, -1, None) == -1
+    assert lib.di_pair_stream(_lib.DI_BF16, p, 3, 3, 128, p, None, 20.0, None) == -1   # empty range
+    assert lib.di_pair_stream(_lib.DI_BF16, p, 0, 4, 128, p, None, 0.0, None) == -1    # no patience
+    assert lib.di_pair_stream(5, p, 0, 4, 128, p, None, 20.0, None) == -1             # dtype
+    bad = _lib.DiPairLaunch(0, 0, 17, 1)
+    assert lib.di_pair_stream(_lib.DI_BF16, p, 0, 4, 128, p, ctypes.byref(bad), 20.0, None) == -1
+    assert lib.di_pair_help(_lib.DI_BF16, p, 4, 3, 128, p, None, -1, None) == -1
+    assert lib.di_pair_help(_lib.DI_F32, None, 0, 3, 128, p, None, -1, None) == -1
+    assert lib.di_pair_help(_lib.DI_F32, p, 0, 3, 128, p, ctypes.byref(bad), -1, None) == -1
 
 
 def _declared_struct_fields(name):
@@ -121,7 +146,8 @@ def _declared_struct_fields(name):
 
 
 def test_ctypes_struct_fields_match_header():
-    for cls, name in ((_lib.DiGraph, "di_graph"), (_lib.DiPairDesc, "di_pair_desc"), (_lib.DiGeoArgs, "di_geo_args")):
+    for cls, name in ((_lib.DiGraph, "di_graph"), (_lib.DiPairDesc, "di_pair_desc"), (_lib.DiGeoArgs, "di_geo_args"),
+                      (_lib.DiPairJob, "di_pair_job")):
         assert [f for f, _ in cls._fields_] == _declared_struct_fields(name), name
 
 
@@ -130,7 +156,7 @@ def _declared_arg_counts():
     src = open(os.path.join(ROOT, "include", "deepinteract_amd.h")).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     out = {}
-    for m in re.finditer(r"\b(?:int|int64_t)\s+(di_[a-z0-9_]+)\s*\(([^)]*)\)\s*;", src):
+    for m in re.finditer(r"\b(?:int|int32_t|int64_t)\s+(di_[a-z0-9_]+)\s*\(([^)]*)\)\s*;", src):
         args = m.group(2).strip()
         out[m.group(1)] = 0 if args in ("", "void") else len(args.split(","))
     return out

@@ -1,16 +1,16 @@
-"""C3 parity on the benchmark's own path (BASELINE configs[2]; bench.py step()): synthetic 2x1000
-heterodimers built on the device (kNN, features, torch-seeded neighbour ids), micro-batches of 8
-complexes concatenated as the bench does, bf16 GeoT in two workspace slots on stream A, the
-pair-tensor kernel reading hT on stream B (the bench's row-streaming kernel with its bounded store
-queue, and the per-vector kernel), cross-stream events between them, three micro-batches so slot 0
-is reused after its pair tensor has drained.
+"""C3 parity on the benchmark's own path (BASELINE configs[2]; bench.py's overlapped schedule,
+deepinteract_amd.pipeline.OverlappedSchedule): synthetic 2x1000 heterodimers built on the device (kNN,
+features, torch-seeded neighbour ids), micro-batches of 8 complexes concatenated as the bench does,
+bf16 GeoT on one stream writing an hT ring, the pair tensors on the persistent device-queue pair
+stream beside it (di_pair_stream, bounded nt stores), di_pair_help launches on the GeoT stream before
+ring slots are reused, and the drain.
 
 Checked against the oracle (fp32 CPU restatement of the reference, pinned to the reference's own
 modules by test_oracle_golden.py) on the same device-built graphs:
 * GeoT node / edge outputs of sampled complexes: bf16 bound BF16_GEOT_TOL (max-abs error / max-abs
   reference), the stated looser bound of north_star for bf16;
-* the pair tensor: bit-exact copies of the GPU's own node features (full 512 MB tensors), and
-  sampled entries vs the oracle's pair tensor within the same bf16 bound.
+* the pair tensor of EVERY complex of EVERY micro-batch: bit-exact copies of the GPU's own node
+  features (full 512 MB tensors), and sampled entries vs the oracle's pair tensor within the bf16 bound.
 """
 import numpy as np
 import pytest
@@ -35,23 +35,18 @@ def _oracle_graph(gb, g):
             "edge_f": gb.edge_f[e0:e1].cpu()}
 
 
-@pytest.mark.parametrize("pair_kernel,side", [("auto", True), ("vector", False)])
-def test_c3_bench_path_bf16_two_slots_two_streams(pair_kernel, side):
-    """side: bench.py's overlapped defaults — the node embedding as the first blocks of the InitEdge
-    launch (di_embed_init_edge) and the fused node layer."""
+@pytest.fixture(scope="module")
+def c3():
     from deepinteract_amd import synth
     from deepinteract_amd.builder import build_graph_batch
-    from deepinteract_amd.engine import GeoTEngine, PairTensorOp
+    from deepinteract_amd.engine import GeoTEngine
     from deepinteract_amd.graph import select_graphs
     from deepinteract_amd.weights import seeded_state_dict
-    from oracle import geot_oracle as O
 
     sd = seeded_state_dict(0, with_head=False)
     eng = GeoTEngine(sd, "bf16")
-    if side:
-        eng.embed_stream = torch.cuda.Stream()
-        eng.fuse_embed_init = True  # bench.py's overlapped default: the embedding inside the InitEdge launch
-        eng.split_node = False
+    eng.fuse_embed_init = True  # bench.py's overlapped defaults: the embedding inside the InitEdge launch,
+    eng.split_node = False      # the fused node layer
     n_cx = M * N_MB
     chains = [c for j in range(n_cx) for c in synth.synthetic_complex(700 + j, N_RES, N_RES)]
     pool = build_graph_batch(chains, k=K, nbr_seeds=list(range(1, 2 * n_cx + 1)))
@@ -59,61 +54,88 @@ def test_c3_bench_path_bf16_two_slots_two_streams(pair_kernel, side):
     gb0 = mbs[0]
     h1r = [gb0.node_off[2 * j] for j in range(M)]
     h2r = [gb0.node_off[2 * j + 1] for j in range(M)]
-    l1 = l2 = [N_RES] * M
-    # bench.py's schedule beside GeoT: row-streaming pair stores with a bounded store queue, 4-wave
-    # blocks on half the CUs
-    cus = torch.cuda.get_device_properties(0).multi_processor_count
-    pair = PairTensorOp(kernel=pair_kernel, blocks=cus // 2 if side else 0, waves_per_block=4 if side else 0,
-                        beside=side)
-    s_geot = torch.cuda.current_stream()
-    s_pair = torch.cuda.Stream()
-    done, keep = [None, None], []
-    for m, gb in enumerate(mbs):
-        slot = m & 1
-        with torch.cuda.stream(s_geot):
-            if done[slot] is not None:
-                s_geot.wait_event(done[slot])
-            h, e = eng.forward(gb, clone=False, slot=slot)
-            hT = eng.last_hT
-            ready = torch.cuda.Event()
-            ready.record(s_geot)
-        with torch.cuda.stream(s_pair):
-            s_pair.wait_event(ready)
-            out, views = pair(h, h1r, h2r, l1, l2, hT=hT)
-            hc, ec = h.clone(), e.clone()   # snapshot of this slot before it is reused
-            ev = torch.cuda.Event()
-            ev.record(s_pair)
-            done[slot] = ev
-        keep.append((hc, ec, views))
+    # each micro-batch's GeoT outputs, computed alone (the kernels are deterministic: the schedule's
+    # node features are bit-identical)
+    outs = []
+    for gb in mbs:
+        h, e = eng.forward(gb)
+        outs.append((h, e))
     torch.cuda.synchronize()
+    return {"sd": sd, "eng": eng, "mbs": mbs, "h1r": h1r, "h2r": h2r, "outs": outs}
+
+
+def _run_schedule(c3, steps, ring, help_every, patience_ms=20.0):
+    from deepinteract_amd.pipeline import OverlappedSchedule
+    eng, mbs = c3["eng"], c3["mbs"]
+    numel = M * 2 * 128 * N_RES * N_RES
+    n_jobs = steps * len(mbs)
+    sinks = [torch.full((numel,), float("nan"), dtype=torch.bfloat16, device="cuda") for _ in range(n_jobs)]
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    sch = OverlappedSchedule(eng, mbs, c3["h1r"], c3["h2r"], [N_RES] * M, [N_RES] * M, sinks,
+                             torch.cuda.current_stream(), torch.cuda.Stream(), ring=ring, help_every=help_every,
+                             stream_blocks=cus // 2, stream_waves=4, patience_ms=patience_ms)
+    for _ in range(steps):
+        sch.step()
+    sch.finish()
+    torch.cuda.synchronize()
+    return sch, sch.check()
+
+
+def _check_pair_exact(c3, sch, n_jobs):
+    """Every pair tensor of every job == the outer concat of the GPU's own node features."""
+    for j in range(n_jobs):
+        h = c3["outs"][j % len(c3["mbs"])][0]
+        for cx, t in enumerate(sch.views(j)):
+            a, b = h[c3["h1r"][cx]:c3["h1r"][cx] + N_RES], h[c3["h2r"][cx]:c3["h2r"][cx] + N_RES]
+            assert t.shape == (1, 256, N_RES, N_RES) and t.dtype == torch.bfloat16
+            assert torch.equal(t[0, :128], a.t().unsqueeze(2).expand(128, N_RES, N_RES)), (j, cx)
+            assert torch.equal(t[0, 128:], b.t().unsqueeze(1).expand(128, N_RES, N_RES)), (j, cx)
+
+
+def test_c3_bench_path_bf16_pair_queue(c3):
+    """Two steps of the bench's schedule (6 jobs) with a 4-slot hT ring and a help launch every 2
+    jobs, so ring slots are reused behind help launches; every pair tensor bit-exact, GeoT of sampled
+    complexes and sampled pair entries vs the oracle."""
+    from oracle import geot_oracle as O
+    sch, cnt = _run_schedule(c3, steps=2, ring=4, help_every=2)
+    n_jobs = 2 * N_MB
+    assert cnt["signalled"] == n_jobs and cnt["error"] == 0, cnt
+    assert cnt["stream_bytes"] + cnt["help_bytes"] == n_jobs * M * 256 * N_RES * N_RES * 2, cnt
+    print("pair queue counters:", cnt, "help launches:", sch.help_launches)
+    _check_pair_exact(c3, sch, n_jobs)
 
     errs = {}
     for m, j in ((0, 0), (0, 5), (2, 3)):
-        hc, ec, views = keep[m]
-        gb = mbs[m]
+        hc, ec = c3["outs"][m]
+        gb = c3["mbs"][m]
         ref = []
         for g in (2 * j, 2 * j + 1):
             with torch.no_grad():
-                n_ref, e_ref = O.geot_forward(sd, _oracle_graph(gb, g))
+                n_ref, e_ref = O.geot_forward(c3["sd"], _oracle_graph(gb, g))
             n0, n1 = gb.node_off[g], gb.node_off[g + 1]
             e0, e1 = gb.edge_off[g], gb.edge_off[g + 1]
             errs[f"mb{m}_c{j}_g{g % 2}_node"] = rel_max(hc[n0:n1].float().cpu().numpy(), n_ref.numpy())
             errs[f"mb{m}_c{j}_g{g % 2}_edge"] = rel_max(ec[e0:e1].float().cpu().numpy(), e_ref.numpy())
             ref.append(n_ref)
-        # pair tensor: bit-exact copy of the GPU's node features (the whole tensor) ...
-        a, b = hc[h1r[j]:h1r[j] + N_RES], hc[h2r[j]:h2r[j] + N_RES]
-        t = views[j]
-        assert t.shape == (1, 256, N_RES, N_RES) and t.dtype == torch.bfloat16
-        assert torch.equal(t[0, :128], a.t().unsqueeze(2).expand(128, N_RES, N_RES))
-        assert torch.equal(t[0, 128:], b.t().unsqueeze(1).expand(128, N_RES, N_RES))
-        # ... and sampled entries against the oracle's pair tensor
+        # sampled entries of the pair tensor the SECOND step wrote for this micro-batch vs the oracle's
+        t = sch.views(N_MB + m)[j]
         rng = np.random.default_rng(m * 100 + j)
         idx = np.stack([rng.integers(0, 256, 4096), rng.integers(0, N_RES, 4096), rng.integers(0, N_RES, 4096)], 1)
         pt = O.pair_tensor(ref[0], ref[1])[0].numpy()
         got = t[0][torch.as_tensor(idx[:, 0]), torch.as_tensor(idx[:, 1]), torch.as_tensor(idx[:, 2])]
         errs[f"mb{m}_c{j}_pair"] = rel_max(got.float().cpu().numpy(), pt[idx[:, 0], idx[:, 1], idx[:, 2]])
-    print(f"C3 bf16 errors, pair kernel {pair_kernel} (max-abs / max-abs ref):", {k: f"{v:.3e}" for k, v in errs.items()})
+    print("C3 bf16 errors, pair queue (max-abs / max-abs ref):", {k: f"{v:.3e}" for k, v in errs.items()})
     assert max(errs.values()) < BF16_GEOT_TOL, errs
+
+
+def test_c3_pair_queue_without_concurrent_stream(c3):
+    """Completion never depends on the pair stream: with no patience its waves give up at once and
+    the help launches on the GeoT stream write every pair tensor, still bit-exact."""
+    sch, cnt = _run_schedule(c3, steps=1, ring=4, help_every=2, patience_ms=1e-6)
+    assert cnt["error"] == 0 and cnt["signalled"] == N_MB, cnt
+    assert cnt["help_bytes"] > 0 and cnt["stream_bytes"] + cnt["help_bytes"] == N_MB * M * 256 * N_RES * N_RES * 2, cnt
+    print("pair queue counters (no patience):", cnt)
+    _check_pair_exact(c3, sch, N_MB)
 
 
 def test_c3_fp32_matches_oracle():

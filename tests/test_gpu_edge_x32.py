@@ -1,5 +1,5 @@
-"""The bf16 edge-layer kernel (k_edge_lean: two 16-row groups per wave sharing every LDS weight
-fragment) against the golden vectors of the reference (tiny/c1/c2), and against the fp32 path
+"""The bf16 edge-layer kernel (k_edge_x32: each wave's 32 edges as one v_mfma_f32_32x32x16_bf16 tile
+chain, weights streamed through LDS) against the golden vectors of the reference (tiny/c1/c2), and against the fp32 path
 (k_edge_layer, exact-f32 MFMA; pinned to the oracle at C3 by test_gpu_c3.py) over EVERY node and
 edge of a full C3 micro-batch (8 concatenated 2x1000 complexes).
 
@@ -24,7 +24,7 @@ def engines():
 
 
 @pytest.mark.parametrize("case", ["tiny", "c1", "c2"])
-def test_lean_matches_reference(engines, case):
+def test_edge_x32_matches_reference(engines, case):
     from deepinteract_amd.graph import GraphBatch
     z = load_case(case)
     gb = GraphBatch.from_arrays([chain_item(z, "g1"), chain_item(z, "g2")], "cuda")
@@ -33,12 +33,12 @@ def test_lean_matches_reference(engines, case):
     n1, e1 = gb.nodes_per_graph[0], gb.edges_per_graph[0]
     errs = [rel_max(h[:n1], z["g1_node_out"]), rel_max(h[n1:], z["g2_node_out"]),
             rel_max(e[:e1][z["g1_edge_rows"]], z["g1_edge_out"]), rel_max(e[e1:][z["g2_edge_rows"]], z["g2_edge_out"])]
-    print(f"{case} lean bf16 GeoT node/edge errors:", ", ".join(f"{x:.3e}" for x in errs))
+    print(f"{case} x32 bf16 GeoT node/edge errors:", ", ".join(f"{x:.3e}" for x in errs))
     assert max(errs) < BF16_TOL
 
 
 @pytest.mark.parametrize("geo_ref", [True, False])
-def test_lean_vs_fp32_c3_microbatch(engines, geo_ref):
+def test_edge_x32_vs_fp32_c3_microbatch(engines, geo_ref):
     """geo_ref False: the general path (neighbour gathers live, Fn rows written and read) on the
     same reference-featurised batch."""
     from deepinteract_amd import synth
@@ -51,5 +51,5 @@ def test_lean_vs_fp32_c3_microbatch(engines, geo_ref):
     assert torch.isfinite(h1.float()).all() and torch.isfinite(e1.float()).all()
     dn = rel_max(h1.float().cpu().numpy(), h0.cpu().numpy())
     de = rel_max(e1.float().cpu().numpy(), e0.cpu().numpy())
-    print(f"C3 micro-batch lean bf16 vs fp32 (geo_ref={geo_ref}): node {dn:.3e} edge {de:.3e}")
+    print(f"C3 micro-batch x32 bf16 vs fp32 (geo_ref={geo_ref}): node {dn:.3e} edge {de:.3e}")
     assert dn < BF16_TOL and de < BF16_TOL

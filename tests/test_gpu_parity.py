@@ -370,10 +370,11 @@ def test_embed_init_edge_one_launch_matches_separate(engines, dtype):
         if fused:
             _lib.check(lib.di_embed_init_edge(g, di, d, _ptr(gb.node_f), _ptr(p.embed[0]), _ptr(p.embed[1]), _ptr(h),
                                               _ptr(qkv), _ptr(gb.edge_f), _ptr(p.init[0]), _ptr(p.init[1]),
-                                              _ptr(p.pos_src), _ptr(p.pos_dst), _ptr(f), None), "di_embed_init_edge")
+                                              _ptr(p.pos_src), _ptr(p.pos_dst), _ptr(f), None, -1, None),
+                       "di_embed_init_edge")
         else:
             _lib.check(lib.di_node_embed(g, di, d, _ptr(gb.node_f), _ptr(p.embed[0]), _ptr(p.embed[1]),
-                                         _ptr(h), _ptr(qkv), None), "di_node_embed")
+                                         _ptr(h), _ptr(qkv), None, -1, None), "di_node_embed")
             _lib.check(lib.di_init_edge(g, di, _ptr(gb.edge_f), _ptr(p.init[0]), _ptr(p.init[1]),
                                         _ptr(p.pos_src), _ptr(p.pos_dst), _ptr(f), None, None), "di_init_edge")
         outs.append((h, qkv, f))
@@ -381,3 +382,63 @@ def test_embed_init_edge_one_launch_matches_separate(engines, dtype):
     for a, b in zip(*outs):
         assert not torch.isnan(a.float()).any()
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_pair_queue_ragged_jobs(dtype):
+    """The pair queue (di_pair_signal / di_pair_stream / di_pair_help) over ragged jobs straight
+    through the C ABI: complexes of different sizes in one job (empty 64-row blocks past a smaller
+    chain 1, rows spanning several 128-chunk segments), jobs of different shapes, signals issued
+    from the producer stream while the pair stream waits on the device, a help launch over the first
+    jobs and the drain; every pair tensor bit-exact with its inputs."""
+    import ctypes
+
+    from deepinteract_amd import _lib
+    from deepinteract_amd.pipeline import PairQueue
+    lib = _lib.load()
+    esz = torch.tensor([], dtype=dtype).element_size()
+    vec = 16 // esz
+    torch.manual_seed(3)
+    job_sizes = [[(12, 8), (300, 1000)], [(65, 2064), (129, 24)], [(1, 8)], [(200, 200), (64, 64), (7, 1000)]]
+    jobs, keep = [], []
+    for sizes in job_sizes:
+        rows = sum(-(-a // vec) * vec + b for a, b in sizes)
+        h = torch.randn(rows, 128, device="cuda").to(dtype)
+        hT = h.t().contiguous()
+        h1r, h2r, r, off, descs = [], [], 0, 0, (_lib.DiPairDesc * len(sizes))()
+        for i, (a, b) in enumerate(sizes):
+            descs[i] = _lib.DiPairDesc(r, r + -(-a // vec) * vec, off, a, b)
+            h1r.append(r)
+            h2r.append(r + -(-a // vec) * vec)
+            r += -(-a // vec) * vec + b
+            off += 256 * a * b
+        d = torch.frombuffer(bytearray(bytes(descs)), dtype=torch.uint8).cuda()
+        out = torch.full((off,), float("nan"), dtype=dtype, device="cuda")
+        items = lib.di_pair_job_items(len(sizes), max(a for a, _ in sizes), 128)
+        jobs.append(_lib.DiPairJob(hT.data_ptr(), d.data_ptr(), out.data_ptr(), rows, len(sizes),
+                                   max(a for a, _ in sizes), items))
+        keep.append((h, hT, d, out, sizes, h1r, h2r))
+    q = PairQueue(torch.device("cuda"), len(jobs))
+    q.set_jobs(jobs)
+    di = _lib.DI_BF16 if dtype == torch.bfloat16 else _lib.DI_F32
+    main, side = torch.cuda.current_stream(), torch.cuda.Stream()
+    st = lambda s: ctypes.c_void_p(s.cuda_stream)  # noqa: E731
+    qp, jp = ctypes.c_void_p(q.state.data_ptr()), ctypes.c_void_p(q.jobs.data_ptr())
+    _lib.check(lib.di_pair_stream(di, jp, 0, len(jobs), 128, qp, None, 200.0, st(side)), "di_pair_stream")
+    for j in range(len(jobs)):
+        torch.cuda._sleep(200000)  # the producer's work before each signal (~0.1 ms)
+        _lib.check(lib.di_pair_signal(qp, j, st(main)), "di_pair_signal")
+        if j == 1:
+            _lib.check(lib.di_pair_help(di, jp, 0, 1, 128, qp, None, -1, st(main)), "di_pair_help")
+    _lib.check(lib.di_pair_help(di, jp, 2, len(jobs) - 1, 128, qp, None, -1, st(main)), "di_pair_help (drain)")
+    torch.cuda.synchronize()
+    cnt = q.counters()
+    total = sum(256 * a * b * esz for _, _, _, _, sizes, _, _ in keep for a, b in sizes)
+    assert cnt["error"] == 0 and cnt["signalled"] == len(jobs) and cnt["stream_bytes"] + cnt["help_bytes"] == total, cnt
+    for h, _, _, out, sizes, h1r, h2r in keep:
+        off = 0
+        for (a, b), r1, r2 in zip(sizes, h1r, h2r):
+            t = out[off:off + 256 * a * b].view(256, a, b)
+            assert torch.equal(t[:128], h[r1:r1 + a].t().unsqueeze(2).expand(128, a, b))
+            assert torch.equal(t[128:], h[r2:r2 + b].t().unsqueeze(1).expand(128, a, b))
+            off += 256 * a * b

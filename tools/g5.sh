@@ -1,0 +1,11 @@
+# round 5: piggyback signal; parity of the touched paths, same-box A/B vs the round-4 tree, trace
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+O=$GRAFT_REPO_ROOT/gpurun_out
+B="--no-cpu --no-sub --no-prologue --complexes 512 --steps 3 --warmup 1"
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_c3.py tests/test_gpu_parity.py tests/test_gpu_node_aggr.py tests/test_gpu_api.py > $O/g5_pytest.log 2>&1 || exit 1
+for r in 1 2; do
+  timeout -k 10 150 python bench.py $B > $O/g5_new$r.json 2>/dev/null || exit 1
+  (cd r4tree && timeout -k 10 150 python bench.py $B > $O/g5_r4_$r.json 2>/dev/null) || exit 1
+done
+cd /tmp && timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d $O/g5_trace -o run -- python3 $GRAFT_REPO_ROOT/bench.py --no-cpu --no-sub --no-prologue --complexes 256 --steps 2 --warmup 1 > $O/g5_trace.json 2>/dev/null
