@@ -49,7 +49,7 @@ EXEC_EDGE_MAC = {True: {"init_edge": 65_536, "edge_layer": 348_160, "edge_layer_
 EXEC_NODE_EMBED_MAC = 128 * 128 + 3 * 128 * 128
 
 
-EDGE_KERNEL = {"bf16": "k_edge_x32 (v_mfma_f32_32x32x16_bf16)", "f32": "k_edge_layer (v_mfma_f32_16x16x4_f32)"}
+EDGE_KERNEL = {"bf16": "k_edge_x32_ring (v_mfma_f32_32x32x16_bf16, 8-wave weight ring)", "f32": "k_edge_layer (v_mfma_f32_16x16x4_f32)"}
 
 
 def node_mac(kind):
@@ -636,7 +636,7 @@ def main():
     mfma_frac = flops_c * value / ws / (MFMA_PEAK_TFLOPS[args.dtype] * 1e12)
     xmfma_frac = xflops_c * value / ws / (MFMA_PEAK_TFLOPS[args.dtype] * 1e12)
     if args.overlap:
-        streams = (f"GeoT || pair tensor: GeoT on one HIP stream (di_pair_signal after each micro-batch), the "
+        streams = (f"GeoT || pair tensor: GeoT on one HIP stream (each micro-batch signalled by the next GeoT launch), the "
                    f"pair tensors on ONE persistent di_pair_stream launch per step on a second stream "
                    f"({args.pair_blocks or 'CUs/2'} blocks x {args.pair_waves or 4} waves, bounded nt stores, "
                    f"device-queue tickets), di_pair_help on the GeoT stream every {args.help_every} micro-batches "

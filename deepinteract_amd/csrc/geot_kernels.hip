@@ -601,7 +601,7 @@ constexpr int EL_NSTAGE_CONF = 18, EL_NSTAGE_FINAL = 19, EL_NSTAGE = 25;
 constexpr int EL_CAP = 36;
 
 // k_edge_layer: 16 rows per wave, 4-wave blocks, two blocks per CU: the fp32 edge layers (the
-// reference's precision; the bf16 layers are k_edge_x32 below) and the conformation module
+// reference's precision; the bf16 layers are k_edge_x32_ring below) and the conformation module
 // alone (di_conformation, both dtypes).
 template <class DT>
 using EdgePipe = WPipe<typename DT::T, Geo<DT>::NW, Geo<DT>::DBUF, EL_CAP, 128>;
@@ -854,49 +854,15 @@ void k_edge_layer(EdgeArgs a) {
   }
 }
 
-// ================================================================ weight stages of the bf16 edge layers
-// Double-buffered 36-block stage slots (plus the stage's bias vector) for a 4-wave block: the LDS-DMA
-// of stage i+1 runs under stage i's MFMAs.
-using X32Pipe = WPipe<u16, 4, true, EL_CAP, 128>;
-
-// stage sequencer of one tile: next() publishes stage i and issues the DMA of stage i + 1.
-// GC (DI_GRAPH_GEO_REF batches): the sequence starts at orig_msg_linear (stages 0-1, the neighbour
-// messages, are exactly zero), which then carries the orig_msg_linear bias, and (intermediate
-// layers) ends before the next layer's nbr_linear (its gathered rows are never needed).
-template <int NS, bool GC = false>
-struct X32Stages {
-  X32Pipe& pipe;
-  const u16* W;
-  const float* V;
-  int i;
-  __device__ void issue(int s) {
-    const int si = GC ? s + 2 : s;
-    const int vo = (GC && s == 0) ? ELV_OM : EL_VEC[si];
-    pipe.issue(W + EL_ORDER[si] * BLK, EL_SIZE[si], vo >= 0 ? V + vo : nullptr, 128);
-  }
-  __device__ const u16* next() {
-    const u16* w = pipe.next();
-    if (i + 1 < NS) issue(i + 1);
-    ++i;
-    return w;
-  }
-  __device__ const float* v() const { return pipe.v(); }
-};
-
 // ================================================================ fused edge layer on 32x32x16 MFMA (bf16)
 // The stage sequence and arithmetic of k_edge_layer<BF16T, MODE, GC>, with each wave's 32 rows as ONE
 // 32x32 tile (csrc/mfma32.h): a 128x128 linear is 32 v_mfma_f32_32x32x16_bf16 per wave. Weight stages
-// LDS-DMA double-buffered (X32Pipe, one 36-block slot per stage), 4-wave blocks of 128 edges, two
-// blocks per CU at <= 240 VGPRs; the weight blobs are packed in the 32x32 fragment order
-// (packing.pack_matrix32, di_blob_layout() == 32).
-struct EdgeX32Geo {
-  static constexpr int NW = 4, THREADS = 64 * NW, ROWS_PER_WAVE = 32, ROWS = ROWS_PER_WAVE * NW;
-};
-static_assert(EdgeX32Geo::NW == 4, "X32Pipe splits every stage's DMA pieces over 4 waves");
+// weight stages on an 8-wave LDS ring (k_edge_x32_ring below); the weight blobs are packed in the 32x32
+// fragment order (packing.pack_matrix32, di_blob_layout() == 32).
 
 // x through one ResBlock: two silu2(W . + b) layers packed as the next operand, then x += ln2 * silu2(W . + b)
-template <int NS, bool GC>
-__device__ __forceinline__ void x32_res_block(X32<4>& x, X32Stages<NS, GC>& st, int lane, int h) {
+template <class ST>
+__device__ __forceinline__ void x32_res_block(X32<4>& x, ST& st, int lane, int h) {
   P32<8> op;
   make_op32(op, x);
 #pragma unroll 1
@@ -934,22 +900,13 @@ __device__ __forceinline__ void x32_f_residual(X32<4>& x, const u16* w, const fl
   pin(x);
 }
 
-template <int MODE, bool GC>
-__global__ __attribute__((amdgpu_flat_work_group_size(1, EdgeX32Geo::THREADS), amdgpu_waves_per_eu(2, 2),
-                          amdgpu_num_vgpr(120)))
-void k_edge_x32(EdgeArgs a) {
+// One 32-row tile per wave through the whole edge layer: the stage sequence `st` (the 8-wave ring's
+// RingStages) hands out each weight stage in order (next(): its weights, v(): its bias).
+template <int MODE, bool GC, class ST>
+__device__ __forceinline__ void edge_x32_tile(const EdgeArgs& a, ST& st, int e, bool valid, int lane, int h) {
   constexpr bool FINAL = MODE == 1;
-  constexpr int NS = (FINAL ? EL_NSTAGE_FINAL : EL_NSTAGE) - (GC ? (FINAL ? 2 : 3) : 0);
-  __shared__ __attribute__((aligned(16))) char lds[2 * X32Pipe::SLOT_BYTES];
-  const int lane = lane_id(), h = lane >> 5;
-  const int r = blockIdx.x * EdgeX32Geo::ROWS + (threadIdx.x >> 6) * EdgeX32Geo::ROWS_PER_WAVE + (lane & 31);
-  const bool valid = r < a.Et;
-  const int e = valid ? r : a.Et - 1;
   const u16* f_row = reinterpret_cast<const u16*>(a.f_in) + (int64_t)e * HID;
   const u16* qkv = reinterpret_cast<const u16*>(a.qkv);
-  X32Pipe pipe(lds);
-  X32Stages<NS, GC> st{pipe, reinterpret_cast<const u16*>(a.wmat), a.wvec, 0};
-  st.issue(0);
 
   // the edge's geometric features [28] (fp32 row) as a 32-feature operand, features 28..31 = 0
   P32<2> gop;
@@ -970,7 +927,7 @@ void k_edge_x32(EdgeArgs a) {
     // DI_GRAPH_GEO_REF: the neighbour messages are multiplied by dir_linear_1(dir_linear_0(0)) = 0
     // (:408), so x = orig_msg_linear(F) + b exactly; no gathered rows, no stages 0-1
     fr.load(f_row, h);
-    w = st.next();  // orig_msg_linear (+ its bias)
+    w = st.next([&] { settle(fr); });  // orig_msg_linear (+ its bias)
     init_vec32_lds(x, st.v(), h);
   } else {
     // ---- neighbour-edge messages (conformation_module_message_func :384-418)
@@ -1047,7 +1004,7 @@ void k_edge_x32(EdgeArgs a) {
       pin(x);
     }
     fr.load(f_row, h);
-    w = st.next();  // stage 2: orig_msg_linear(res) + nbr
+    w = st.next([&] { settle(fr); });  // stage 2: orig_msg_linear(res) + nbr
   }
   {
     P32<8> fop;
@@ -1060,7 +1017,7 @@ void k_edge_x32(EdgeArgs a) {
   // F rows are loaded BEFORE the stage's barrier and DMA issue: vmcnt retires in order, so a load
   // issued after the stage's LDS-DMA pieces would make its use wait for the whole weight stage
   fr.load(f_row, h);
-  w = st.next();  // res_connect_linear: x = F + silu(rc(x))
+  w = st.next([&] { settle(fr); });  // res_connect_linear: x = F + silu(rc(x))
   x32_f_residual(x, w, st.v(), fr, lane, h);
   x32_res_block(x, st, lane, h);
   x32_res_block(x, st, lane, h);
@@ -1074,14 +1031,17 @@ void k_edge_x32(EdgeArgs a) {
     pin(x);
   }
   fr.load(f_row, h);
-  w = st.next();  // final_linear: x = F + silu(final(x)) = conformation output
+  w = st.next([&] { settle(fr); });  // final_linear: x = F + silu(final(x)) = conformation output
   x32_f_residual(x, w, st.v(), fr, lane, h);
 
   // ---- attention scores (propagate_attention :76-91): head hd = features 32 hd .. 32 hd + 31 = block hd
   R32<4> kr, qr;  // K[src], Q[dst], issued before the stage barrier
   kr.load(qkv + (int64_t)a.src[e] * 3 * HID + HID, h);
   qr.load(qkv + (int64_t)a.dst[e] * 3 * HID, h);
-  w = st.next();  // edge_feats_projection(BN1e(conf))
+  w = st.next([&] {
+    settle(kr);
+    settle(qr);
+  });  // edge_feats_projection(BN1e(conf))
   X32<4> p;
   {
     P32<8> xop;
@@ -1114,8 +1074,8 @@ void k_edge_x32(EdgeArgs a) {
     P32<8> pop;
     make_op32(pop, p);
     pin(pop);
-    fr.load(f_row, h);  // O_edge: re-read
-    w = st.next();      // O_edge_feats
+    fr.load(f_row, h);                 // O_edge: re-read
+    w = st.next([&] { settle(fr); });  // O_edge_feats
     X32<4> e1;
     init_vec32_lds(e1, st.v(), h);
     mma32<4, 8>(e1, pop, w, lane);
@@ -1154,6 +1114,167 @@ void k_edge_x32(EdgeArgs a) {
   }
 }
 
+// ================================================================ the bf16 edge layers on an 8-wave weight ring
+// One persistent 8-wave block per CU (2 waves per SIMD, <= 240 VGPRs), a 4-slot ring of
+// 36-block weight stages in LDS (150 KB): every stage is DMA'd ONCE per 256 edges (8 waves x 32 rows)
+// instead of once per 128 -- half the L2 -> LDS weight stream of round 4's two 4-wave blocks per CU,
+// the traffic that competes with the pair-tensor stores beside it -- and there is no
+// block-wide barrier per stage. Per slot two LDS counters, both monotonic: FULL counts publications of
+// the slot's stages (the owner waits its vmcnt, then adds), FREE the waves done reading it. A wave entering global stage g (stages run on across the block's tiles, so the
+// next tile's first stages are in flight under the current tile's last ones):
+//   releases stage g - 1 (FREE += 1); if it owns a stage it issued earlier (stage s is loaded by wave
+//   s % 8), waits for its own loads (vmcnt(0)) and publishes it (FULL += 1); if it owns stage g + 2,
+//   issues it into the slot of stage g - 2 once all 8 waves have released that one; then waits until
+//   stage g is published. No block-wide barrier: a wave waits only for the owner of the stage it needs
+//   and, once in 8 stages, for the slowest wave two stages back.
+constexpr int RING_NW = 8, RING_SLOTS = 4, RING_AHEAD = 2;
+using RingSlot = WPipe<u16, RING_NW, true, EL_CAP, 128>;  // slot geometry only (SLOT_BYTES)
+struct EdgeRingGeo {
+  static constexpr int NW = RING_NW, THREADS = 64 * NW, ROWS_PER_WAVE = 32, ROWS = ROWS_PER_WAVE * NW;
+};
+
+// The ring's LDS counters are read and added with explicit ds_ instructions: through C++ atomics the
+// compiler cannot tell them from the weight slots the in-flight LDS-DMA writes and puts an
+// s_waitcnt vmcnt(0) in front of every poll, which would drain the prefetch at every stage.
+__device__ __forceinline__ uint32_t lds_off(const uint32_t* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint32_t*)p;
+}
+__device__ __forceinline__ uint32_t lds_ld(const uint32_t* p) {
+  uint32_t v;
+  asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(lds_off(p)) : "memory");
+  return v;
+}
+// +1 per WAVE (one lane; LDS operations of a wave execute in order, so the add follows the wave's
+// earlier reads of the slot)
+__device__ __forceinline__ void lds_add(uint32_t* p) {
+  asm volatile(
+      "s_mov_b64 s[0:1], exec\n\t"
+      "s_mov_b64 exec, 1\n\t"
+      "ds_add_u32 %0, %1\n\t"
+      "s_mov_b64 exec, s[0:1]" ::"v"(lds_off(p)), "v"(1u)
+      : "memory", "s0", "s1");
+}
+// spin until *p >= v (s_sleep between LDS polls)
+__device__ __forceinline__ void lds_wait_ge(const uint32_t* p, uint32_t v) {
+  while (lds_ld(p) < v) __builtin_amdgcn_s_sleep(1);
+}
+
+// raw buffer descriptor (as buf_rsrc: stride 0, num_records 0x7fffffff, DATA_FORMAT 32) in SGPRs
+typedef uint32_t rsrc4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ rsrc4 rsrc_of(const void* p) {
+  const uint64_t a = (uint64_t)(uintptr_t)p;
+  return (rsrc4){(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)a),
+                 (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(a >> 32)) & 0xffffu, 0x7fffffffu,
+                 (uint32_t)BUF_RSRC_W3};
+}
+// one 1-KiB LDS-DMA piece: 16 B per lane from rsrc + voff + soff to LDS byte address lds + 16 * lane
+__device__ __forceinline__ void dma_piece(rsrc4 r, uint32_t lds, int voff, int soff) {
+  asm volatile(
+      "s_mov_b32 m0, %0\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %1, %2, %3 offen lds" ::"s"(__builtin_amdgcn_readfirstlane((int)lds)),
+      "v"(voff), "s"(r), "s"(__builtin_amdgcn_readfirstlane(soff))
+      : "memory", "m0");
+}
+
+template <int NS, bool GC>
+struct RingStages {
+  char* base;          // RING_SLOTS x RingSlot::SLOT_BYTES
+  uint32_t* full;      // [RING_SLOTS]: stage uses published (1 per use)
+  uint32_t* freec;     // [RING_SLOTS]: wave releases (RING_NW per use)
+  const u16* W;
+  const float* V;
+  int wave;
+  int total;           // global stages of this block (tiles x NS)
+  int g = 0;           // next stage to consume
+  int issued = 0;      // stages [0, issued) are issued (by their owners)
+  int pending = -1;    // a stage this wave issued and has not published yet
+  int cur = 0;         // slot of the stage being consumed
+  __device__ u16* slot_w(int sl) const { return reinterpret_cast<u16*>(base + sl * RingSlot::SLOT_BYTES); }
+  __device__ float* slot_v(int sl) const {
+    return reinterpret_cast<float*>(base + sl * RingSlot::SLOT_BYTES + EL_CAP * BLK * 2);
+  }
+  // global stage gs is loaded and published by ONE wave, gs % RING_NW (its owner): all its 1-KiB
+  // LDS-DMA pieces and the bias vector. Issued by inline asm: the compiler's waitcnt pass cannot tell a
+  // ring slot (runtime index) from the one being read and would wait for every piece before the next
+  // ds_read -- completion is what FULL tracks (the owner's vmcnt(0), then its publish).
+  __device__ void issue_one(int gs) {
+    const int s = gs % NS;
+    const int si = GC ? s + 2 : s;
+    const int vo = (GC && s == 0) ? ELV_OM : EL_VEC[si];
+    const int sl = gs % RING_SLOTS;
+    const uint32_t dst = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)slot_w(sl);
+    const int nkib = EL_SIZE[si];  // 512 bf16 elements = 1 KiB per block
+    const int loff = (threadIdx.x & 63) * 16;
+    const rsrc4 r = rsrc_of(W + EL_ORDER[si] * BLK);
+    for (int i = 0; i < nkib; ++i) dma_piece(r, dst + i * 1024, loff, i * 1024);
+    if (vo >= 0 && (threadIdx.x & 63) < 32) dma_piece(rsrc_of(V + vo), dst + EL_CAP * BLK * 2, loff, 0);
+    pending = gs;
+  }
+  // stages issued ahead of the one consumed, owners' slots permitting
+  __device__ void issue_ahead() {
+    for (; issued <= g + RING_AHEAD && issued < total; ++issued) {
+      if (issued % RING_NW != wave) continue;
+      const int prev = issued - RING_SLOTS;  // the stage that used this slot last
+      if (prev >= 0) lds_wait_ge(freec + issued % RING_SLOTS, (uint32_t)(RING_NW * (prev / RING_SLOTS + 1)));
+      issue_one(issued);
+    }
+  }
+  __device__ void fill() {
+    for (; issued < RING_AHEAD && issued < total; ++issued)
+      if (issued % RING_NW == wave) issue_one(issued);
+  }
+  // settle(): an empty asm reading the rows the caller loaded just before this call (F rows, K / Q):
+  // the compiler then waits for them HERE, after the vmcnt(0) that has landed them anyway -- not after
+  // the asm-issued DMA below, which it cannot see and would otherwise wait for at their first use
+  template <class F>
+  __device__ const u16* next(F&& settle) {
+    asm volatile("" ::: "memory");
+    if (g > 0) lds_add(freec + (g - 1) % RING_SLOTS);  // done reading stage g - 1 (its reads are in order before)
+    lds_dma_wait();  // this wave's loads (rows, and the pieces of a stage it owns) have landed
+    settle();
+    if (pending >= 0) {
+      lds_add(full + pending % RING_SLOTS);
+      pending = -1;
+    }
+    issue_ahead();
+    lds_wait_ge(full + g % RING_SLOTS, (uint32_t)(g / RING_SLOTS + 1));
+    asm volatile("" ::: "memory");
+    cur = g % RING_SLOTS;
+    ++g;
+    return slot_w(cur);
+  }
+  __device__ const u16* next() {
+    return next([] {});
+  }
+  __device__ const float* v() const { return slot_v(cur); }
+};
+
+template <int MODE, bool GC>
+__global__ __attribute__((amdgpu_flat_work_group_size(1, EdgeRingGeo::THREADS), amdgpu_waves_per_eu(2, 2),
+                          amdgpu_num_vgpr(120)))
+void k_edge_x32_ring(EdgeArgs a, int ntiles) {
+  constexpr bool FINAL = MODE == 1;
+  constexpr int NS = (FINAL ? EL_NSTAGE_FINAL : EL_NSTAGE) - (GC ? (FINAL ? 2 : 3) : 0);
+  __shared__ __attribute__((aligned(16))) char lds[RING_SLOTS * RingSlot::SLOT_BYTES];
+  __shared__ uint32_t counters[2 * RING_SLOTS];
+  const int lane = lane_id(), h = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int my_tiles = ((int)blockIdx.x < ntiles) ? (ntiles - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
+  if (threadIdx.x < 2 * RING_SLOTS) counters[threadIdx.x] = 0;
+  __syncthreads();
+  RingStages<NS, GC> st{lds, counters, counters + RING_SLOTS, reinterpret_cast<const u16*>(a.wmat), a.wvec, wave,
+                        my_tiles * NS};
+  st.fill();
+#pragma unroll 1
+  for (int i = 0; i < my_tiles; ++i) {
+    const int tile = (int)blockIdx.x + i * (int)gridDim.x;
+    const int r = tile * EdgeRingGeo::ROWS + wave * EdgeRingGeo::ROWS_PER_WAVE + (lane & 31);
+    const bool valid = r < a.Et;
+    const int e = valid ? r : a.Et - 1;
+    edge_x32_tile<MODE, GC>(a, st, e, valid, lane, h);
+  }
+}
 
 // ================================================================ node aggregation (CSR segment sum)
 // h_attn[v] = sum_{e in in(v)} alpha[e, head] * V[src e]  /  (sum_e alpha[e, head] + 1e-6)
@@ -1562,7 +1683,7 @@ extern "C" int64_t di_blob_bytes(int kind, di_dtype dtype, int vec) {
 extern "C" int di_blob_layout(int kind, di_dtype dtype) {
   if (!dtype_ok(dtype) || kind < 0 || kind > 6) return -1;
   if (dtype != DI_BF16) return 16;
-  if (kind == 1 || kind == 2 || kind == 3) return 32;  // k_init_x32 / k_init_res_x32 / k_edge_x32
+  if (kind == 1 || kind == 2 || kind == 3) return 32;  // k_init_x32 / k_init_res_x32 / k_edge_x32_ring
   return 16;
 }
 
@@ -1661,12 +1782,14 @@ extern "C" int di_edge_layer(const di_graph* g, di_dtype dt, int final_layer, co
              f_out, fn_out};
   hipStream_t s = (hipStream_t)stream;
   if (dt == DI_BF16) {
-    // 32x32x16 form: 128 edges (one 32-row tile per wave) per 4-wave block; 32x32-packed blob
-    const dim3 grid((unsigned)((a.Et + EdgeX32Geo::ROWS - 1) / EdgeX32Geo::ROWS)), block(EdgeX32Geo::THREADS);
-    if (final_layer && gc) hipLaunchKernelGGL((k_edge_x32<1, true>), grid, block, 0, s, a);
-    else if (final_layer) hipLaunchKernelGGL((k_edge_x32<1, false>), grid, block, 0, s, a);
-    else if (gc) hipLaunchKernelGGL((k_edge_x32<0, true>), grid, block, 0, s, a);
-    else hipLaunchKernelGGL((k_edge_x32<0, false>), grid, block, 0, s, a);
+    // persistent 8-wave blocks on the weight ring, one per CU (k_edge_x32_ring)
+    const int ntiles = (a.Et + EdgeRingGeo::ROWS - 1) / EdgeRingGeo::ROWS;
+    const int cus = device_cus();
+    const dim3 grid((unsigned)(ntiles < cus ? ntiles : cus)), block(EdgeRingGeo::THREADS);
+    if (final_layer && gc) hipLaunchKernelGGL((k_edge_x32_ring<1, true>), grid, block, 0, s, a, ntiles);
+    else if (final_layer) hipLaunchKernelGGL((k_edge_x32_ring<1, false>), grid, block, 0, s, a, ntiles);
+    else if (gc) hipLaunchKernelGGL((k_edge_x32_ring<0, true>), grid, block, 0, s, a, ntiles);
+    else hipLaunchKernelGGL((k_edge_x32_ring<0, false>), grid, block, 0, s, a, ntiles);
   } else {
     const dim3 grid = grid_of<Geo<F32T>>(a.Et), block = block_of<Geo<F32T>>();
     if (final_layer && gc) hipLaunchKernelGGL((k_edge_layer<F32T, 1, true>), grid, block, 0, s, a);

@@ -95,16 +95,22 @@ def gpu_forward(model, k: int = 20, seed: int = 0):
     """The per-micro-batch forward of ``predict_sharded`` on the HIP path: on-device graph build
     (deepinteract_amd.builder) -> LitGINI.predict_batch -> contact probabilities. Complex i's
     chains draw their neighbour-edge ids as torch.manual_seed(seed + 2i + s) would (s = 0, 1), so
-    the maps do not depend on how the complexes are sharded or micro-batched."""
+    the maps do not depend on how the complexes are sharded or micro-batched. out (optional): one
+    [L1, L2] tensor per complex -- the chunked gather's send slices -- that receive the maps (the
+    softmax output written straight into the collective's buffer, in its wire dtype)."""
     from .builder import build_graph_batch
 
-    def fn(complexes, ids):
+    def fn(complexes, ids, out=None):
         chains = [c for pair in complexes for c in pair]
         dev = model.engine.device
         gb = build_graph_batch(chains, k=k, device=dev, node_count_limit=model.cfg.node_count_limit,
                                nbr_seeds=[seed + 2 * i + s for i in ids for s in (0, 1)])
         with torch.no_grad():
             _, probs = model.predict_batch(gb, [(2 * j, 2 * j + 1) for j in range(len(complexes))])
+            if out is not None:
+                for dst, p in zip(out, probs):
+                    dst.copy_(p)
+                return out
         return probs
 
     return fn
@@ -129,38 +135,53 @@ def gather_rounds(sizes: Sequence[tuple], plan, micro_batch: int):
 
 class ChunkedGather:
     """Round-by-round asynchronous all-gather of contact maps (chunked and overlapped
-    with compute). ``put(c, maps)`` packs this rank's maps of round c into the round's send buffer
-    and issues ``all_gather_into_tensor(..., async_op=True)`` -- on RCCL it runs on the process
-    group's own stream after the work already queued on the current stream, so the next
-    micro-batch's kernels, issued right after, overlap it; ``finish()`` waits for every round and
-    returns the maps of all complexes in global order (views of the rounds' receive buffers)."""
+    with compute). Every round's send and receive buffers are allocated up front (sizes are known
+    from the plan), and ``slots(c)`` hands out this rank's [L1, L2] slices of round c's send buffer
+    for the forward to write its maps into (gpu_forward's ``out``): the compute stream runs no pack,
+    pad or cast kernels. ``put(c)`` issues ``all_gather_into_tensor(..., async_op=True)`` -- on
+    RCCL it runs on the process group's own stream, which waits for the work already queued on the
+    current stream (one event), so the next micro-batch's kernels, issued right after, overlap it;
+    ``finish()`` waits for every round and returns the maps of all complexes in global order (views
+    of the rounds' receive buffers)."""
 
     def __init__(self, sizes, plan, micro_batch, dtype, device, group=None):
         self.sizes, self.dtype, self.device, self.group = sizes, dtype, device, group
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
         self.rounds = gather_rounds(sizes, plan, micro_batch)
+        # padding of a round's send buffer is never read by a receiver; zeroed once for determinism
+        self.send = [torch.zeros(width, dtype=dtype, device=device) for _, width in self.rounds]
+        self.recv = [torch.empty(self.world * width, dtype=dtype, device=device) for _, width in self.rounds]
         self.pending = []
 
-    def put(self, c, maps):
-        members, width = self.rounds[c]
-        mine = members[self.rank]
-        if len(maps) != len(mine):
-            raise ValueError(f"rank {self.rank}: {len(maps)} maps for round {c}'s {len(mine)} complexes")
-        send = torch.zeros(width, dtype=self.dtype, device=self.device)
-        if maps:
-            flat = torch.cat([m.reshape(-1).to(device=self.device, dtype=self.dtype) for m in maps])
-            send[:flat.numel()] = flat
-        recv = torch.empty(self.world * width, dtype=self.dtype, device=self.device)
-        work = dist.all_gather_into_tensor(recv, send, group=self.group, async_op=True)
-        self.pending.append((c, recv, send, work))
+    def slots(self, c):
+        """This rank's maps of round c as [L1, L2] views of the round's send buffer (member order)."""
+        views, off = [], 0
+        for i in self.rounds[c][0][self.rank]:
+            l1, l2 = self.sizes[i]
+            views.append(self.send[c][off:off + l1 * l2].view(l1, l2))
+            off += l1 * l2
+        return views
+
+    def put(self, c, maps=None):
+        """Issue round c's collective. maps (optional): this rank's maps of the round, copied into the
+        send slices (for a forward that did not write them there itself)."""
+        mine = self.rounds[c][0][self.rank]
+        if maps is not None:
+            if len(maps) != len(mine):
+                raise ValueError(f"rank {self.rank}: {len(maps)} maps for round {c}'s {len(mine)} complexes")
+            for dst, m in zip(self.slots(c), maps):
+                if dst.data_ptr() != m.data_ptr():
+                    dst.copy_(m)
+        work = dist.all_gather_into_tensor(self.recv[c], self.send[c], group=self.group, async_op=True)
+        self.pending.append((c, self.recv[c], self.send[c], work))
 
     def finish(self):
         # rounds in which this rank has no micro-batch still take part (every rank issues every round)
         done = {c for c, *_ in self.pending}
         for c in range(len(self.rounds)):
             if c not in done:
-                self.put(c, [])
+                self.put(c)
         out = [None] * len(self.sizes)
         for c, recv, _send, work in sorted(self.pending, key=lambda t: t[0]):
             work.wait()
@@ -182,7 +203,8 @@ def predict_sharded(complexes: Sequence, forward: Callable, micro_batch: int = 8
 
     complexes: per complex a (chain1, chain2) pair of builder inputs (dicts with backbone
     [N,4,3], amide_norm [N,3], dips [N,106]); forward(batch, ids) -> list of [L1, L2] maps for
-    the complexes ``batch`` (global indices ``ids``).
+    the complexes ``batch`` (global indices ``ids``); a forward that takes ``out=`` (gpu_forward)
+    writes them straight into the chunked gather's send slices.
     gather: "chunked" (default) -- one asynchronous all-gather per micro-batch round, overlapped
     with the next round's compute (ChunkedGather); "once" -- ONE all-gather after the last
     micro-batch (all_gather_maps); "none" -- no collective, this rank's maps only (timing the
@@ -200,9 +222,14 @@ def predict_sharded(complexes: Sequence, forward: Callable, micro_batch: int = 8
     chunks = ChunkedGather(sizes, plan, micro_batch, dtype, device, group) if gather == "chunked" else None
     mine = local_order(sizes, plan[rank])
     maps = {}
+    import inspect
+    takes_out = "out" in inspect.signature(forward).parameters
     for c, s in enumerate(range(0, len(mine), micro_batch)):
         ids = mine[s:s + micro_batch]
-        got = list(forward([complexes[i] for i in ids], ids))
+        if chunks is not None and takes_out:
+            got = list(forward([complexes[i] for i in ids], ids, out=chunks.slots(c)))
+        else:
+            got = list(forward([complexes[i] for i in ids], ids))
         for i, m in zip(ids, got):
             if tuple(m.shape) != sizes[i]:
                 raise ValueError(f"complex {i}: map {tuple(m.shape)} != {sizes[i]}")

@@ -130,13 +130,25 @@ def _cpu_forward(batch, ids):
     return out
 
 
-def _worker_predict(rank, world, port, gather, dtype, q):
+def _cpu_forward_out(batch, ids, out=None):
+    """_cpu_forward writing into the caller's buffers when given (gpu_forward's contract: the chunked
+    gather's send slices)."""
+    maps = _cpu_forward(batch, ids)
+    if out is None:
+        return maps
+    for dst, m in zip(out, maps):
+        dst.copy_(m)
+    return out
+
+
+def _worker_predict(rank, world, port, gather, dtype, fwd, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         cx = _complexes()
-        maps, plan = predict_sharded(cx, _cpu_forward, micro_batch=2, gather=gather, dtype=dtype)
+        forward = _cpu_forward_out if fwd == "out" else _cpu_forward
+        maps, plan = predict_sharded(cx, forward, micro_batch=2, gather=gather, dtype=dtype)
         ref = [m.to(dtype) for m in _cpu_forward(cx, list(range(len(cx))))]
         ok = len(maps) == len(cx) and all(m.dtype == dtype and torch.equal(m, r) for m, r in zip(maps, ref))
         q.put((rank, ok, [len(p) for p in plan]))
@@ -151,6 +163,15 @@ def test_predict_sharded_gloo(world, gather, dtype):
     gathered once at the end or round by round with asynchronous all-gathers (world 3: ranks with
     different micro-batch counts); every rank ends with every complex's map, equal to a
     single-process run."""
-    res = _spawn(_worker_predict, world, gather, dtype)
+    res = _spawn(_worker_predict, world, gather, dtype, "plain")
     assert all(ok for _, ok, _ in res), res
     assert sum(res[0][2]) == len(_complexes())
+
+
+@pytest.mark.parametrize("world,dtype", [(2, torch.float32), (3, torch.bfloat16)])
+def test_predict_sharded_chunked_forward_writes_send_slices(world, dtype):
+    """The chunked gather with a forward that takes ``out=``: the maps are written straight into the
+    rounds' preallocated send buffers (no pack / pad / cast on the compute stream) and gathered
+    bit-identical to a single-process run."""
+    res = _spawn(_worker_predict, world, "chunked", dtype, "out")
+    assert all(ok for _, ok, _ in res), res

@@ -18,7 +18,7 @@ import numpy as np
 import pytest
 import torch
 
-from gpu_common import chain_arrays, chain_item, load_case, rel_elem, rel_max
+from gpu_common import chain_arrays, chain_item, close_elem, load_case, logit_floor, rel_elem, rel_max
 
 pytestmark = pytest.mark.gpu
 F32_TOL = 1e-4
@@ -88,6 +88,11 @@ def test_shared_step_and_predict_step(model_f32, case):
         logits_list, g1_nf, g1_ef, g2_nf, g2_ef = model_f32.shared_step(g1, g2, return_representations=True)
     assert len(logits_list) == 1 and tuple(logits_list[0].shape) == tuple(z["logits"].shape)
     assert rel_max(_np(logits_list[0]), z["logits"]) < F32_TOL
+    # every logit, elementwise: 1e-4 relative + 1e-5 of max|logit| absolute (gpu_common.close_elem)
+    le = rel_elem(_np(logits_list[0]), z["logits"], logit_floor(z["logits"]))
+    lc = close_elem(_np(logits_list[0]), z["logits"])
+    print(f"{case} shared_step logits elementwise relative {le:.3e} (floored), allclose ratio {lc:.3f}")
+    assert lc <= 1.0
     for nf, ef, tag in ((g1_nf, g1_ef, "g1"), (g2_nf, g2_ef, "g2")):
         assert isinstance(nf, np.ndarray) and isinstance(ef, np.ndarray)
         assert rel_max(nf, z[f"{tag}_node_out"]) < F32_TOL

@@ -1,5 +1,5 @@
-"""The bf16 edge-layer kernel (k_edge_x32: each wave's 32 edges as one v_mfma_f32_32x32x16_bf16 tile
-chain, weights streamed through LDS) against the golden vectors of the reference (tiny/c1/c2), and against the fp32 path
+"""The bf16 edge-layer kernel (k_edge_x32_ring: each wave's 32 edges as one v_mfma_f32_32x32x16_bf16
+tile chain, weight stages on a 4-slot LDS ring shared by the 8 waves of a persistent block) against the golden vectors of the reference (tiny/c1/c2), and against the fp32 path
 (k_edge_layer, exact-f32 MFMA; pinned to the oracle at C3 by test_gpu_c3.py) over EVERY node and
 edge of a full C3 micro-batch (8 concatenated 2x1000 complexes).
 

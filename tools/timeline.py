@@ -21,7 +21,7 @@ KINDS = [("k_pair_stream", "pstream"), ("k_pair_help", "help"), ("k_pair_signal"
          ("k_init_edge", "init"), ("k_node_layer<di::BF16T, false", "node0"), ("k_node_layer<di::BF16T, true", "node1"),
          ("k_node_layer<di::F32T, false", "node0"), ("k_node_layer<di::F32T, true", "node1"),
          ("k_node_aggr", "aggr"), ("k_node_update_ring<false", "node0"), ("k_node_update_ring<true", "node1"),
-         ("k_node_embed", "embed"), ("k_edge_x32<0", "edge0"), ("k_edge_x32<1", "edge1"), ("k_init_x32", "init"),
+         ("k_node_embed", "embed"), ("k_edge_x32_ring<0", "edge0"), ("k_edge_x32_ring<1", "edge1"), ("k_init_x32", "init"),
          ("k_init_res_x32", "init")]
 PAIR_STREAM = ("pstream", "pair")
 
