@@ -452,6 +452,7 @@ def sub_record(what, dtype, geo_ref, complexes, pool_gb, P, M, n_res, k, args, d
     from deepinteract_amd.graph import select_graphs
     eng = GeoTEngine(sd, dtype, cfg, device=dev)
     eng.split_node = args.node_kernel == "split"
+    eng.fold_attn = args.node_kernel == "fold"
     eng.fuse_embed_init = args.init_kernel == "fused"
     mbs = [select_graphs(pool_gb, [2 * ((m * M + j) % P) + s for j in range(M) for s in (0, 1)]).with_geo_ref(geo_ref)
            for m in range(complexes // M)]
@@ -518,8 +519,9 @@ def main():
     ap.add_argument("--layers", type=int, default=None, help="GeoT layers (default 2; c5: 4)")
     ap.add_argument("--node-limit", type=int, default=None,
                     help="max_num_graph_nodes of the synthetic model (default 2304; c5: 4096)")
-    ap.add_argument("--node-kernel", default=None, choices=["split", "fused"],
-                    help="node layer as di_node_aggregate + di_node_update (split) or one di_node_layer (fused). "
+    ap.add_argument("--node-kernel", default=None, choices=["split", "fused", "fold"],
+                    help="node layer as di_node_aggregate + di_node_update (split), one di_node_layer (fused), or "
+                         "the aggregation folded into the bf16 edge layer + di_node_update_folded (fold). "
                          "Default: fused when overlapped, split otherwise")
     ap.add_argument("--init-kernel", default="fused", choices=["fused", "split"],
                     help="fused: the node embedding as the first blocks of the InitEdge launch (reference-"
@@ -571,6 +573,7 @@ def main():
     sd = seeded_state_dict(0, cfg, with_head=False)
     eng = GeoTEngine(sd, args.dtype, cfg, device=dev)
     eng.split_node = args.node_kernel == "split"
+    eng.fold_attn = args.node_kernel == "fold"
     eng.fuse_embed_init = args.init_kernel == "fused"
 
     # ---- inputs: a pool of distinct complexes built on the device (kNN + features + ids) ----

@@ -39,7 +39,7 @@ class DiPairLaunch(ctypes.Structure):
 
 
 DI_PAIR_AUTO, DI_PAIR_ROWS, DI_PAIR_VECTOR, DI_PAIR_LINES = 0, 1, 2, 3
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 
 class DiPairJob(ctypes.Structure):
@@ -68,6 +68,10 @@ _SIGS = {
     "di_node_layer": ([ctypes.POINTER(DiGraph), _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P], ctypes.c_int),
     "di_node_aggregate": ([ctypes.POINTER(DiGraph), _I, _P, _P, _P, _P], ctypes.c_int),
     "di_node_update": ([ctypes.POINTER(DiGraph), _I, _I, _P, _P, _P, _P, _P, _P, _P, _P], ctypes.c_int),
+    "di_attn_parts_bytes": ([_I], ctypes.c_int64),
+    "di_edge_layer_attn": ([ctypes.POINTER(DiGraph), _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
+                           ctypes.c_int),
+    "di_node_update_folded": ([ctypes.POINTER(DiGraph), _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P], ctypes.c_int),
     "di_pair_tensor": ([_I, _P, _I, _I, _I, _I, _I, _P, _P, _I, ctypes.POINTER(DiPairLaunch), _P, _P], ctypes.c_int),
     "di_pair_tensor_check": ([_I, _I, _I, _I, _I, ctypes.POINTER(DiPairLaunch)], ctypes.c_int),
     "di_pair_queue_bytes": ([_I], ctypes.c_int64),

@@ -63,6 +63,10 @@ struct EdgeArgs {
   float* alpha_out;
   void* f_out;
   void* fn_out;
+  // di_edge_layer_attn (bf16): the attention aggregation folded into the epilogue (edge_attn_fold)
+  float* attn_out = nullptr;
+  float* attn_parts = nullptr;
+  const int* in_ptr = nullptr;
 };
 
 struct NodeArgs {
@@ -78,6 +82,9 @@ struct NodeArgs {
   const float* wvec;
   void* h_out;
   void* qkv_out;
+  // with attn: di_edge_layer_attn's partial sums of the destinations split over edge tiles
+  // (attn_row; in_ptr is then the CSR row pointer)
+  const float* attn_parts = nullptr;
 };
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
@@ -903,7 +910,7 @@ __device__ __forceinline__ void x32_f_residual(X32<4>& x, const u16* w, const fl
 // One 32-row tile per wave through the whole edge layer: the stage sequence `st` (the 8-wave ring's
 // RingStages) hands out each weight stage in order (next(): its weights, v(): its bias).
 template <int MODE, bool GC, class ST>
-__device__ __forceinline__ void edge_x32_tile(const EdgeArgs& a, ST& st, int e, bool valid, int lane, int h) {
+__device__ __forceinline__ floatx4 edge_x32_tile(const EdgeArgs& a, ST& st, int e, bool valid, int lane, int h) {
   constexpr bool FINAL = MODE == 1;
   const u16* f_row = reinterpret_cast<const u16*>(a.f_in) + (int64_t)e * HID;
   const u16* qkv = reinterpret_cast<const u16*>(a.qkv);
@@ -1068,7 +1075,7 @@ __device__ __forceinline__ void edge_x32_tile(const EdgeArgs& a, ST& st, int e, 
     sum += __shfl_xor(sum, 32);  // the head's other 16 features: the same row in the other lane half
     al[b] = expf_<true>(fminf(fmaxf(sum, -5.f), 5.f));
   }
-  if (valid && h == 0) st4(a.alpha_out + (int64_t)e * 4, al);
+  if (valid && h == 0 && a.alpha_out != nullptr) st4(a.alpha_out + (int64_t)e * 4, al);
   if constexpr (!FINAL) {
     // ---- edge output: e = in + O_e(e_out); e = e + FFN(BN2e(e)) (:697-724)
     P32<8> pop;
@@ -1102,7 +1109,7 @@ __device__ __forceinline__ void edge_x32_tile(const EdgeArgs& a, ST& st, int e, 
       pin(e1);
     }
     if (valid) store_row32(e1, reinterpret_cast<u16*>(a.f_out) + (int64_t)e * HID, h);
-    if constexpr (GC) return;  // the next layer gathers no silu(nbr_linear(F)) rows
+    if constexpr (GC) return al;  // the next layer gathers no silu(nbr_linear(F)) rows
     make_op32(eop, e1);
     w = st.next();  // next layer's silu(nbr_linear(.))
     X32<4> fn;
@@ -1112,6 +1119,7 @@ __device__ __forceinline__ void edge_x32_tile(const EdgeArgs& a, ST& st, int e, 
     for (int b = 0; b < 4; ++b) silu_blk(fn.v[b]);
     if (valid) store_row32(fn, reinterpret_cast<u16*>(a.fn_out) + (int64_t)e * HID, h);
   }
+  return al;
 }
 
 // ================================================================ the bf16 edge layers on an 8-wave weight ring
@@ -1250,6 +1258,84 @@ struct RingStages {
   __device__ const float* v() const { return slot_v(cur); }
 };
 
+// ---- the node layer's attention aggregation folded into the edge layer (di_edge_layer_attn)
+// h_attn[v] = sum_{e in in(v)} alpha[e, head] * V[src e] / (sum_e alpha[e, head] + 1e-6)
+// (send_and_recv(u_mul_e('V_h','score'), sum), (copy_e('score'), sum), wV / (z + 1e-6):
+// deepinteract_modules.py:93-96, 116). Edges are destination-major, so a destination's in-edges are
+// consecutive rows: a wave's 32 rows hold whole destinations plus at most one continuing from the
+// previous 32-row tile and one continuing into the next. Each lane forms alpha * V[src] for its row
+// (the 64 features of its lane half, in the accumulator quads) and alpha itself; a segmented
+// inclusive scan over the 32 rows -- DPP row shifts by 1, 2, 4, 8 inside each 16-lane row, then the
+// first row's last lane broadcast into the second -- leaves every destination's sums in the lane of
+// its last row here. That lane writes attn[v] = wV / (z + 1e-6) when all of v's in-edges are in this
+// tile, else the partial sums to attn_parts[tile][slot] (slot 1: v continues into the next tile;
+// slot 0: v continues from the previous one); attn_row (the node update) adds a split
+// destination's partials. Summation order: a tree over each tile's rows, then tile by tile.
+constexpr int FOLD_ROWS = 32;   // edges per tile of attn_parts (one wave's rows)
+constexpr int FOLD_PART = 132;  // floats per partial: 128 wV, then z of the 4 heads
+static_assert(EdgeRingGeo::ROWS_PER_WAVE == FOLD_ROWS, "a fold tile is one wave's rows");
+
+// one scan step: lanes whose DPP source row has the same destination add its sums
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ void fold_step(X32<4>& s, floatx4& z, int d) {
+  const bool same = __builtin_amdgcn_update_dpp(-2, d, CTRL, ROW_MASK, 0xf, false) == d;
+  auto mv = [](float x) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL, ROW_MASK, 0xf,
+                                                                  false));
+  };
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const float t = mv(s.v[b][k]);
+      s.v[b][k] += same ? t : 0.f;
+    }
+    const float t = mv(z[b]);
+    z[b] += same ? t : 0.f;
+  }
+}
+
+__device__ __forceinline__ void edge_attn_fold(const EdgeArgs& a, int e, bool valid, int lane, int h, floatx4 al) {
+  const int d = valid ? a.dst[e] : -1;  // rows past the end: their own (empty) segment
+  if (!valid) al = (floatx4){0.f, 0.f, 0.f, 0.f};
+  R32<4> vr;
+  vr.load(reinterpret_cast<const u16*>(a.qkv) + (int64_t)a.src[e] * 3 * HID + 2 * HID, h);
+  X32<4> s;
+#pragma unroll
+  for (int b = 0; b < 4; ++b)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) set_quad(s.v[b], q, al[b] * unpack4(vr.u[4 * b + q]));
+  floatx4 z = al;
+  fold_step<0x111, 0xf>(s, z, d);  // row_shr:1
+  fold_step<0x112, 0xf>(s, z, d);  // row_shr:2
+  fold_step<0x114, 0xf>(s, z, d);  // row_shr:4
+  fold_step<0x118, 0xf>(s, z, d);  // row_shr:8
+  fold_step<0x142, 0xa>(s, z, d);  // row_bcast:15 into rows 1 and 3 (each lane half's second 16 rows)
+  const int dnext = __shfl_down(d, 1, 32);
+  if (!valid || ((lane & 31) != 31 && dnext == d)) return;
+  const int e0 = a.in_ptr[d], e1 = a.in_ptr[d + 1];
+  const int t = e / FOLD_ROWS, t0 = e0 / FOLD_ROWS, t1 = (e1 - 1) / FOLD_ROWS;
+  if (t0 == t1) {
+    float* row = a.attn_out + (int64_t)d * HID;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const float den = z[b] + 1e-6f;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const floatx4 x = quad(s.v[b], q);
+        st4(row + 32 * b + 8 * q + 4 * h, (floatx4){x[0] / den, x[1] / den, x[2] / den, x[3] / den});
+      }
+    }
+  } else {
+    float* p = a.attn_parts + ((int64_t)t * 2 + (t == t0 ? 1 : 0)) * FOLD_PART;
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) st4(p + 32 * b + 8 * q + 4 * h, quad(s.v[b], q));
+    if (h == 0) st4(p + HID, z);
+  }
+}
+
 template <int MODE, bool GC>
 __global__ __attribute__((amdgpu_flat_work_group_size(1, EdgeRingGeo::THREADS), amdgpu_waves_per_eu(2, 2),
                           amdgpu_num_vgpr(120)))
@@ -1272,7 +1358,8 @@ void k_edge_x32_ring(EdgeArgs a, int ntiles) {
     const int r = tile * EdgeRingGeo::ROWS + wave * EdgeRingGeo::ROWS_PER_WAVE + (lane & 31);
     const bool valid = r < a.Et;
     const int e = valid ? r : a.Et - 1;
-    edge_x32_tile<MODE, GC>(a, st, e, valid, lane, h);
+    const floatx4 al = edge_x32_tile<MODE, GC>(a, st, e, valid, lane, h);
+    if (a.attn_out != nullptr) edge_attn_fold(a, e, valid, lane, h, al);
   }
 }
 
@@ -1365,6 +1452,40 @@ __global__ __launch_bounds__(16 * AGG_NODES) void k_node_aggr(AggrArgs a) {
   float* out = a.attn + (int64_t)v * HID + FPL * j;
   *reinterpret_cast<float4*>(out) = o0;
   *reinterpret_cast<float4*>(out + 4) = o1;
+}
+
+// The attention row of node v from precomputed aggregates: di_node_aggregate's rows, or
+// di_edge_layer_attn's (attn_parts != null): complete rows for destinations whose in-edges lie in
+// one fold tile, partial sums for the others (edge_attn_fold), zero for a node without in-edges
+// (wV / (z + 1e-6) = 0 there).
+__device__ __forceinline__ void attn_row(Act<8>& wv, const NodeArgs& a, int v, int g) {
+  if (a.attn_parts == nullptr) {
+    load_row(wv, a.attn + (int64_t)v * HID, g);
+    return;
+  }
+  const int e0 = a.in_ptr[v], e1 = a.in_ptr[v + 1];
+  const int t0 = e0 / FOLD_ROWS, t1 = (e1 - 1) / FOLD_ROWS;
+  if (e1 <= e0) {
+    zero(wv);
+  } else if (t0 == t1) {
+    load_row(wv, a.attn + (int64_t)v * HID, g);
+  } else {
+    const float* p = a.attn_parts + ((int64_t)t0 * 2 + 1) * FOLD_PART;
+    load_row(wv, p, g);
+    floatx4 z = ld4(p + HID);
+#pragma unroll 1
+    for (int t = t0 + 1; t <= t1; ++t) {
+      p = a.attn_parts + (int64_t)t * 2 * FOLD_PART;
+      add_row(wv, p, g);
+      z += ld4(p + HID);
+    }
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      const float d = z[b >> 1] + 1e-6f;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) wv.v[b][q] = wv.v[b][q] / d;
+    }
+  }
 }
 
 // The CSR segment sum of one node held in the MFMA layout (wv[b][q] = feature 16b + 4g + q of node
@@ -1469,7 +1590,7 @@ __global__ __launch_bounds__(NodeRingGeo::THREADS, 1) void k_node_update_ring(No
   RawRow<u16> hin;
   hin.load(reinterpret_cast<const u16*>(a.h_in) + (int64_t)v * HID, g);
   Act<8> wv;
-  load_row(wv, a.attn + (int64_t)v * HID, g);
+  attn_row(wv, a, v, g);
   settle(hin);
 #pragma unroll
   for (int b = 0; b < 8; ++b) asm volatile("" ::"v"(wv.v[b]));
@@ -1586,7 +1707,7 @@ __global__ __launch_bounds__(NodeGeo::THREADS, 2) void k_node_layer(NodeArgs a) 
 
   // send_and_recv(u_mul_e('V_h','score'), sum) and (copy_e('score'), sum); h = wV / (z + 1e-6)
   Act<8> wv;
-  if (a.attn != nullptr) load_row(wv, a.attn + (int64_t)v * HID, g);  // k_node_aggr: same products, order, division
+  if (a.attn != nullptr) attn_row(wv, a, v, g);  // k_node_aggr (same products, order, division) or the fold
   else node_gather<DT>(wv, a, v, g);
   // n = in1 + O_node(h)
   const T* w = pipe.next();
@@ -1767,19 +1888,20 @@ extern "C" int di_init_edge_resident(const di_graph* g, const float* edge_f, con
   return launch_status();
 }
 
-extern "C" int di_edge_layer(const di_graph* g, di_dtype dt, int final_layer, const float* edge_f,
-                             const void* f_in, const void* fn_in, const void* qkv, const void* wmat,
-                             const float* wvec, float* alpha_out, void* f_out, void* fn_out,
-                             void* stream) {
+static int edge_layer(const di_graph* g, di_dtype dt, int final_layer, const float* edge_f, const void* f_in,
+                      const void* fn_in, const void* qkv, const void* wmat, const float* wvec, float* alpha_out,
+                      void* f_out, void* fn_out, float* attn_out, float* attn_parts, void* stream) {
   // DI_GRAPH_GEO_REF: the neighbour-message branch is skipped (exactly zero), fn_in is not read and
   // fn_out not written (every edge-layer kernel; di_conformation computes the branch)
   const bool gc = g && (g->flags & DI_GRAPH_GEO_REF);
-  if (!g || !edge_f || !f_in || (!fn_in && !gc) || !qkv || !wmat || !wvec || !alpha_out || g->num_edges <= 0 ||
-      !dtype_ok(dt))
+  const bool fold = attn_out != nullptr;
+  if (!g || !edge_f || !f_in || (!fn_in && !gc) || !qkv || !wmat || !wvec || (!alpha_out && !fold) ||
+      g->num_edges <= 0 || !dtype_ok(dt))
     return DI_EINVAL;
+  if (fold && (dt != DI_BF16 || !attn_parts || !g->in_ptr || !g->src || !g->dst)) return DI_EINVAL;
   if (!final_layer && (!f_out || (!fn_out && !gc))) return DI_EINVAL;
   EdgeArgs a{g->num_edges, edge_f, g->src, g->dst, g->nbr, f_in, fn_in, qkv, wmat, wvec, alpha_out,
-             f_out, fn_out};
+             f_out, fn_out, attn_out, attn_parts, g->in_ptr};
   hipStream_t s = (hipStream_t)stream;
   if (dt == DI_BF16) {
     // persistent 8-wave blocks on the weight ring, one per CU (k_edge_x32_ring)
@@ -1798,6 +1920,28 @@ extern "C" int di_edge_layer(const di_graph* g, di_dtype dt, int final_layer, co
     else hipLaunchKernelGGL((k_edge_layer<F32T, 0>), grid, block, 0, s, a);
   }
   return launch_status();
+}
+
+extern "C" int di_edge_layer(const di_graph* g, di_dtype dt, int final_layer, const float* edge_f,
+                             const void* f_in, const void* fn_in, const void* qkv, const void* wmat,
+                             const float* wvec, float* alpha_out, void* f_out, void* fn_out,
+                             void* stream) {
+  return edge_layer(g, dt, final_layer, edge_f, f_in, fn_in, qkv, wmat, wvec, alpha_out, f_out, fn_out, nullptr,
+                    nullptr, stream);
+}
+
+extern "C" int64_t di_attn_parts_bytes(int32_t num_edges) {
+  if (num_edges <= 0) return DI_EINVAL;
+  return (int64_t)((num_edges + FOLD_ROWS - 1) / FOLD_ROWS) * 2 * FOLD_PART * (int64_t)sizeof(float);
+}
+
+extern "C" int di_edge_layer_attn(const di_graph* g, di_dtype dt, int final_layer, const float* edge_f,
+                                  const void* f_in, const void* fn_in, const void* qkv, const void* wmat,
+                                  const float* wvec, float* alpha_out, void* f_out, void* fn_out, float* attn_out,
+                                  float* attn_parts, void* stream) {
+  if (!attn_out) return DI_EINVAL;
+  return edge_layer(g, dt, final_layer, edge_f, f_in, fn_in, qkv, wmat, wvec, alpha_out, f_out, fn_out, attn_out,
+                    attn_parts, stream);
 }
 
 extern "C" int di_conformation(const di_graph* g, di_dtype dt, const float* edge_f, const void* f_in,
@@ -1846,12 +1990,14 @@ extern "C" int di_node_aggregate(const di_graph* g, di_dtype dt, const float* al
   return launch_status();
 }
 
-extern "C" int di_node_update(const di_graph* g, di_dtype dt, int final_layer, const float* attn, const void* h_in,
-                              const void* wmat, const float* wvec, void* h_out, void* qkv_out, void* hT_out,
-                              void* stream) {
+static int node_update(const di_graph* g, di_dtype dt, int final_layer, const float* attn, const float* attn_parts,
+                       const void* h_in, const void* wmat, const float* wvec, void* h_out, void* qkv_out, void* hT_out,
+                       void* stream) {
   if (!g || !attn || !h_in || !wmat || !wvec || !h_out || g->num_nodes <= 0 || !dtype_ok(dt)) return DI_EINVAL;
   if (!final_layer && !qkv_out) return DI_EINVAL;
-  NodeArgs a{g->num_nodes, attn, hT_out, nullptr, nullptr, nullptr, h_in, nullptr, wmat, wvec, h_out, qkv_out};
+  if (attn_parts && !g->in_ptr) return DI_EINVAL;
+  NodeArgs a{g->num_nodes, attn, hT_out, nullptr, attn_parts ? g->in_ptr : nullptr, nullptr, h_in, nullptr, wmat,
+             wvec, h_out, qkv_out, attn_parts};
   hipStream_t s = (hipStream_t)stream;
   if (dt == DI_BF16) {
     const dim3 grid = grid_of<NodeRingGeo>(a.Nt), block = block_of<NodeRingGeo>();
@@ -1863,4 +2009,17 @@ extern "C" int di_node_update(const di_graph* g, di_dtype dt, int final_layer, c
     else hipLaunchKernelGGL((k_node_layer<F32T, false>), grid, block, 0, s, a);
   }
   return launch_status();
+}
+
+extern "C" int di_node_update(const di_graph* g, di_dtype dt, int final_layer, const float* attn, const void* h_in,
+                              const void* wmat, const float* wvec, void* h_out, void* qkv_out, void* hT_out,
+                              void* stream) {
+  return node_update(g, dt, final_layer, attn, nullptr, h_in, wmat, wvec, h_out, qkv_out, hT_out, stream);
+}
+
+extern "C" int di_node_update_folded(const di_graph* g, di_dtype dt, int final_layer, const float* attn,
+                                     const float* attn_parts, const void* h_in, const void* wmat, const float* wvec,
+                                     void* h_out, void* qkv_out, void* hT_out, void* stream) {
+  if (!attn_parts) return DI_EINVAL;
+  return node_update(g, dt, final_layer, attn, attn_parts, h_in, wmat, wvec, h_out, qkv_out, hT_out, stream);
 }

@@ -92,6 +92,9 @@ class GeoTEngine:
         # di_node_layer): the segment reduction (16 lanes per destination) at full occupancy instead
         # of inside the MFMA kernel's one-block-per-CU grid
         self.split_node = True
+        # bf16: the attention aggregation folded into the edge layer's epilogue (di_edge_layer_attn +
+        # di_node_update_folded; takes precedence over split_node for bf16)
+        self.fold_attn = False
         # reference-featurised batches: node embedding as the first blocks of the InitEdge launch
         # (di_embed_init_edge, bf16 or fp32) instead of a separate launch (default, round 4: serial
         # 101 us for both vs 19 + 108 us with the resident InitEdge after the embedding)
@@ -138,6 +141,7 @@ class GeoTEngine:
                 "fn": [torch.empty(ce, H, dtype=dt, device=dev) for _ in range(2)],
                 "alpha": torch.empty(ce, 4, dtype=torch.float32, device=dev),
                 "attn": torch.empty(cn, H, dtype=torch.float32, device=dev),
+                "parts": torch.empty(max(self.lib.di_attn_parts_bytes(ce), 4) // 4, dtype=torch.float32, device=dev),
                 "hT": torch.empty(H * cn, dtype=dt, device=dev),
             })
         b, H = cap[1], self.cfg.num_gnn_hidden_channels
@@ -145,7 +149,7 @@ class GeoTEngine:
         views = self._ws_views[key] = {
             "h": [t[:num_nodes] for t in b["h"]], "qkv": [t[:num_nodes] for t in b["qkv"]],
             "f": [t[:num_edges] for t in b["f"]], "fn": [t[:num_edges] for t in b["fn"]],
-            "alpha": b["alpha"][:num_edges], "attn": b["attn"][:num_nodes],
+            "alpha": b["alpha"][:num_edges], "attn": b["attn"][:num_nodes], "parts": b["parts"],
             "hT": b["hT"][:H * num_nodes].view(H, num_nodes),
         }
         return views
@@ -205,16 +209,32 @@ class GeoTEngine:
                            "di_init_edge")
         L = p.num_layers
         cur = 0
+        fold = self.fold_attn and self.dtype == "bf16"
         for li in range(L):
             final = li == L - 1
             nxt = 1 - cur
             em, ev = p.edge[li]
+            nm, nv = p.node[li]
             tick("edge_layer_final" if final else "edge_layer")
+            if fold:
+                # edge layer + the attention segment sums of its rows; node update adds split rows
+                _lib.check(lib.di_edge_layer_attn(g, dt, int(final), _ptr(gb.edge_f), _ptr(f[cur]), _ptr(fn[cur]),
+                                                  _ptr(qkv[cur]), _ptr(em), _ptr(ev), _ptr(None),
+                                                  _ptr(None if final else f[nxt]), _ptr(None if final else fn[nxt]),
+                                                  _ptr(ws["attn"]), _ptr(ws["parts"]), st), "di_edge_layer_attn")
+                tick("node_layer_final" if final else "node_layer")
+                _lib.check(lib.di_node_update_folded(g, dt, int(final), _ptr(ws["attn"]), _ptr(ws["parts"]),
+                                                     _ptr(h[cur]), _ptr(nm), _ptr(nv), _ptr(h[nxt]),
+                                                     _ptr(None if final else qkv[nxt]), _ptr(hT if final else None),
+                                                     st), "di_node_update_folded")
+                if not final:
+                    f_out = nxt
+                cur = nxt
+                continue
             _lib.check(lib.di_edge_layer(g, dt, int(final), _ptr(gb.edge_f), _ptr(f[cur]), _ptr(fn[cur]),
                                          _ptr(qkv[cur]), _ptr(em), _ptr(ev), _ptr(alpha),
                                          _ptr(None if final else f[nxt]), _ptr(None if final else fn[nxt]),
                                          st), "di_edge_layer")
-            nm, nv = p.node[li]
             if self.split_node:
                 # CSR segment reduction of the attention messages, then O_node / FFN / next Q,K,V
                 tick("node_aggr")

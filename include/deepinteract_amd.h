@@ -14,6 +14,7 @@
  *   di_edge_layer   ConformationModule (:373-455) + attention edge UDFs (:76-91, graph_utils.py:21-63)
  *                   + O_edge/edge FFN of GeometricTransformerModule  deepinteract_modules.py:669-727
  *   di_node_layer   send_and_recv(u_mul_e/copy_e, sum) gSpMM         deepinteract_modules.py:93-96,116
+ *   di_edge_layer_attn / di_node_update_folded: the same gSpMM folded into the edge layer (bf16)
  *                   + O_node / node FFN                               deepinteract_modules.py:696-723, 923-943
  *   di_pair_tensor  construct_interact_tensor (pad=False)            deepinteract_utils.py:158-172
  *   di_pair_stream / di_pair_help / di_pair_signal: the same, per micro-batch, as a device queue beside
@@ -47,7 +48,7 @@
 extern "C" {
 #endif
 
-#define DI_ABI_VERSION 6
+#define DI_ABI_VERSION 7
 
 /* activation / weight storage type of the GeoT kernels (accumulation is always fp32). A plain
  * int32 (not a C enum type): a foreign caller may pass any value, and every entry point refuses
@@ -167,6 +168,26 @@ int di_node_aggregate(const di_graph* g, di_dtype dt, const float* alpha /*[Et,4
 int di_node_update(const di_graph* g, di_dtype dt, int final_layer, const float* attn /*[Nt,128]*/,
                    const void* h_in, const void* wmat, const float* wvec, void* h_out, void* qkv_out,
                    void* hT_out, void* stream);
+/* ABI 7: the same aggregation folded into the bf16 edge layer's epilogue (no alpha round trip, no
+ * gather launch). di_edge_layer_attn = di_edge_layer (alpha_out may be NULL: not written) + the
+ * segment sums of its edges: the kernel's waves each hold 32 consecutive (destination-major) edges,
+ * "fold tile" t = edges 32t .. 32t+31; for every destination v
+ *   all in-edges in one fold tile:  attn_out[v, :] = wV / (z + 1e-6)  (fp32 [Nt,128], as di_node_aggregate)
+ *   in-edges over tiles t0 < .. < t1: attn_parts[t0][1] holds tile t0's partial sums (wV[128], z[4]),
+ *                                     attn_parts[t][0] tile t's for t0 < t <= t1
+ * attn_parts: di_attn_parts_bytes(num_edges) bytes (fp32 [ceil(Et/32)][2][132]); rows of nodes
+ * without in-edges are not written. dt must be DI_BF16 and g->in_ptr set (DI_EINVAL otherwise).
+ * Summation order: a tree over a tile's rows, then tile by tile (di_node_aggregate adds in edge
+ * order; both within the bf16 path's bound). di_node_update_folded = di_node_update on those
+ * outputs: split destinations add their partials, nodes without in-edges get 0. */
+int64_t di_attn_parts_bytes(int32_t num_edges);
+int di_edge_layer_attn(const di_graph* g, di_dtype dt, int final_layer, const float* edge_f,
+                       const void* f_in, const void* fn_in, const void* qkv, const void* wmat, const float* wvec,
+                       float* alpha_out, void* f_out, void* fn_out, float* attn_out /*[Nt,128]*/,
+                       float* attn_parts, void* stream);
+int di_node_update_folded(const di_graph* g, di_dtype dt, int final_layer, const float* attn,
+                          const float* attn_parts, const void* h_in, const void* wmat, const float* wvec,
+                          void* h_out, void* qkv_out, void* hT_out, void* stream);
 
 /* Pair-tensor kernel of a di_pair_tensor call (di_pair_launch.kernel). Scheduling choice of this
  * build, not a reference interface; every kernel writes the same bytes. */

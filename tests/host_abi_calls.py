@@ -85,16 +85,30 @@ def main(path):
         expect(lib.di_node_layer(gp, 1, 0, p, p, p, p, p, p, None, None, None), EINVAL, "node qkv_out")
         expect(lib.di_node_layer(gp, 3, 1, p, p, p, p, p, p, None, None, None), EINVAL, "node dtype")
         expect(lib.di_node_update(gp, 1, 0, p, p, p, p, p, None, None, None), EINVAL, "update qkv_out")
+        expect(lib.di_edge_layer_attn(gp, 0, 1, p, p, p, p, p, p, None, None, None, p, p, None), EINVAL,
+               "edge attn f32")
+        expect(lib.di_edge_layer_attn(gp, 1, 1, p, p, p, p, p, p, None, None, None, None, p, None), EINVAL,
+               "edge attn NULL attn")
+        expect(lib.di_edge_layer_attn(gp, 1, 1, p, p, p, p, p, p, None, None, None, p, None, None), EINVAL,
+               "edge attn NULL parts")
+        expect(lib.di_edge_layer_attn(gp, 1, 0, p, p, p, p, p, p, None, None, None, p, p, None), EINVAL,
+               "edge attn f_out")
+        expect(lib.di_node_update_folded(gp, 1, 1, p, None, p, p, p, p, None, None, None), EINVAL,
+               "update folded NULL parts")
         expect(lib.di_node_aggregate(gp, 1, None, p, p, None), EINVAL, "aggregate NULL")
         expect(lib.di_conformation(gp, 1, p, p, None, p, p, p, None), EINVAL, "conformation Fn")
         expect(lib.di_geo_attention(gp, 1, None, p, p, p, p, None), EINVAL, "attention NULL")
     # every graph entry point with a NULL graph (remaining arguments plausible)
     for fn in ("di_node_embed", "di_init_edge", "di_init_edge_resident", "di_embed_init_edge", "di_edge_layer", "di_node_layer", "di_node_aggregate",
-               "di_node_update", "di_conformation", "di_geo_attention"):
+               "di_node_update", "di_conformation", "di_geo_attention", "di_edge_layer_attn", "di_node_update_folded"):
         argtypes = _lib._SIGS[fn][0]
         args = [None] + [1 if t is _lib._I else p for t in argtypes[1:]]
         args[-1] = None  # stream
         expect(getattr(lib, fn)(*args), EINVAL, f"{fn} NULL graph")
+    # fold partial-sum buffer: ceil(Et / 32) tiles x 2 slots x 132 floats
+    expect(lib.di_attn_parts_bytes(0), EINVAL, "attn parts empty")
+    expect(lib.di_attn_parts_bytes(33), 2 * 2 * 132 * 4, "attn parts 33 edges")
+    expect(lib.di_attn_parts_bytes(32), 1 * 2 * 132 * 4, "attn parts 32 edges")
     # builder entry points: range checks in int32 / int64 arithmetic
     expect(lib.di_knn_topk(1, None, None, 20, 10, None, None, None), EINVAL, "knn NULL")
     expect(lib.di_knn_topk(1, p, p, 20, 4097, p, p, None), EINVAL, "knn max nodes")
