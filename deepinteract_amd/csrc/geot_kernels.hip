@@ -907,10 +907,88 @@ __device__ __forceinline__ void x32_f_residual(X32<4>& x, const u16* w, const fl
   pin(x);
 }
 
+// ---- the node layer's attention aggregation folded into the edge layer (di_edge_layer_attn)
+// h_attn[v] = sum_{e in in(v)} alpha[e, head] * V[src e] / (sum_e alpha[e, head] + 1e-6)
+// (send_and_recv(u_mul_e('V_h','score'), sum), (copy_e('score'), sum), wV / (z + 1e-6):
+// deepinteract_modules.py:93-96, 116). Edges are destination-major, so a destination's in-edges are
+// consecutive rows: a wave's 32 rows hold whole destinations plus at most one continuing from the
+// previous 32-row tile and one continuing into the next. Each lane forms alpha * V[src] for its row
+// (the 64 features of its lane half, in the accumulator quads) and alpha itself; a segmented
+// inclusive scan over the 32 rows -- DPP row shifts by 1, 2, 4, 8 inside each 16-lane row, then the
+// first row's last lane broadcast into the second -- leaves every destination's sums in the lane of
+// its last row here. That lane writes attn[v] = wV / (z + 1e-6) when all of v's in-edges are in this
+// tile, else the partial sums to attn_parts[tile][slot] (slot 1: v continues into the next tile;
+// slot 0: v continues from the previous one); attn_row (the node update) adds a split
+// destination's partials. Summation order: a tree over each tile's rows, then tile by tile.
+constexpr int FOLD_ROWS = 32;   // edges per tile of attn_parts (one wave's rows)
+constexpr int FOLD_PART = 132;  // floats per partial: 128 wV, then z of the 4 heads
+
+// one scan step: lanes whose DPP source row has the same destination add its sums
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ void fold_step(X32<4>& s, floatx4& z, int d) {
+  const bool same = __builtin_amdgcn_update_dpp(-2, d, CTRL, ROW_MASK, 0xf, false) == d;
+  auto mv = [](float x) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL, ROW_MASK, 0xf,
+                                                                  false));
+  };
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const float t = mv(s.v[b][k]);
+      s.v[b][k] += same ? t : 0.f;
+    }
+    const float t = mv(z[b]);
+    z[b] += same ? t : 0.f;
+  }
+}
+
+// d: the row's destination, vr: its V[src] row, ip: in_ptr[d], in_ptr[d + 1] (loaded with K / Q)
+__device__ __forceinline__ void edge_attn_fold(const EdgeArgs& a, int e, bool valid, int lane, int h, floatx4 al,
+                                               int d, const R32<4>& vr, int2 ip) {
+  if (!valid) {  // rows past the end: their own (empty) segment
+    d = -1;
+    al = (floatx4){0.f, 0.f, 0.f, 0.f};
+  }
+  X32<4> s;
+#pragma unroll
+  for (int b = 0; b < 4; ++b)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) set_quad(s.v[b], q, al[b] * unpack4(vr.u[4 * b + q]));
+  floatx4 z = al;
+  fold_step<0x111, 0xf>(s, z, d);  // row_shr:1
+  fold_step<0x112, 0xf>(s, z, d);  // row_shr:2
+  fold_step<0x114, 0xf>(s, z, d);  // row_shr:4
+  fold_step<0x118, 0xf>(s, z, d);  // row_shr:8
+  fold_step<0x142, 0xa>(s, z, d);  // row_bcast:15 into rows 1 and 3 (each lane half's second 16 rows)
+  const int dnext = __shfl_down(d, 1, 32);
+  if (!valid || ((lane & 31) != 31 && dnext == d)) return;
+  const int t = e / FOLD_ROWS, t0 = ip.x / FOLD_ROWS, t1 = (ip.y - 1) / FOLD_ROWS;
+  if (t0 == t1) {
+    float* row = a.attn_out + (int64_t)d * HID;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const float den = z[b] + 1e-6f;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const floatx4 x = quad(s.v[b], q);
+        st4(row + 32 * b + 8 * q + 4 * h, (floatx4){x[0] / den, x[1] / den, x[2] / den, x[3] / den});
+      }
+    }
+  } else {
+    float* p = a.attn_parts + ((int64_t)t * 2 + (t == t0 ? 1 : 0)) * FOLD_PART;
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) st4(p + 32 * b + 8 * q + 4 * h, quad(s.v[b], q));
+    if (h == 0) st4(p + HID, z);
+  }
+}
+
 // One 32-row tile per wave through the whole edge layer: the stage sequence `st` (the 8-wave ring's
 // RingStages) hands out each weight stage in order (next(): its weights, v(): its bias).
 template <int MODE, bool GC, class ST>
-__device__ __forceinline__ floatx4 edge_x32_tile(const EdgeArgs& a, ST& st, int e, bool valid, int lane, int h) {
+__device__ __forceinline__ void edge_x32_tile(const EdgeArgs& a, ST& st, int e, bool valid, int lane, int h) {
   constexpr bool FINAL = MODE == 1;
   const u16* f_row = reinterpret_cast<const u16*>(a.f_in) + (int64_t)e * HID;
   const u16* qkv = reinterpret_cast<const u16*>(a.qkv);
@@ -1043,11 +1121,26 @@ __device__ __forceinline__ floatx4 edge_x32_tile(const EdgeArgs& a, ST& st, int 
 
   // ---- attention scores (propagate_attention :76-91): head hd = features 32 hd .. 32 hd + 31 = block hd
   R32<4> kr, qr;  // K[src], Q[dst], issued before the stage barrier
-  kr.load(qkv + (int64_t)a.src[e] * 3 * HID + HID, h);
-  qr.load(qkv + (int64_t)a.dst[e] * 3 * HID, h);
+  const int sn = a.src[e], dn = a.dst[e];
+  kr.load(qkv + (int64_t)sn * 3 * HID + HID, h);
+  qr.load(qkv + (int64_t)dn * 3 * HID, h);
+  // the fold's V[src] row and the destination's in-edge range, in flight with K / Q (GEO_REF kernels;
+  // the general path's extra live rows leave no room: loaded at the fold)
+  const bool fold = a.attn_out != nullptr;  // uniform
+  R32<4> vr;
+  int2 ip = {0, 0};
+  auto fold_loads = [&] {
+    vr.load(qkv + (int64_t)sn * 3 * HID + 2 * HID, h);
+    ip = *reinterpret_cast<const int2*>(a.in_ptr + dn);
+  };
+  if (GC && fold) fold_loads();
   w = st.next([&] {
     settle(kr);
     settle(qr);
+    if (GC && fold) {
+      settle(vr);
+      asm volatile("" ::"v"(ip.x), "v"(ip.y));
+    }
   });  // edge_feats_projection(BN1e(conf))
   X32<4> p;
   {
@@ -1076,11 +1169,15 @@ __device__ __forceinline__ floatx4 edge_x32_tile(const EdgeArgs& a, ST& st, int 
     al[b] = expf_<true>(fminf(fmaxf(sum, -5.f), 5.f));
   }
   if (valid && h == 0 && a.alpha_out != nullptr) st4(a.alpha_out + (int64_t)e * 4, al);
-  if constexpr (!FINAL) {
+  if (!GC && fold) fold_loads();
+  if constexpr (FINAL) {
+    if (fold) edge_attn_fold(a, e, valid, lane, h, al, dn, vr, ip);
+  } else {
     // ---- edge output: e = in + O_e(e_out); e = e + FFN(BN2e(e)) (:697-724)
     P32<8> pop;
     make_op32(pop, p);
     pin(pop);
+    if (fold) edge_attn_fold(a, e, valid, lane, h, al, dn, vr, ip);  // p is packed: room for the scan
     fr.load(f_row, h);                 // O_edge: re-read
     w = st.next([&] { settle(fr); });  // O_edge_feats
     X32<4> e1;
@@ -1109,7 +1206,7 @@ __device__ __forceinline__ floatx4 edge_x32_tile(const EdgeArgs& a, ST& st, int 
       pin(e1);
     }
     if (valid) store_row32(e1, reinterpret_cast<u16*>(a.f_out) + (int64_t)e * HID, h);
-    if constexpr (GC) return al;  // the next layer gathers no silu(nbr_linear(F)) rows
+    if constexpr (GC) return;  // the next layer gathers no silu(nbr_linear(F)) rows
     make_op32(eop, e1);
     w = st.next();  // next layer's silu(nbr_linear(.))
     X32<4> fn;
@@ -1119,7 +1216,6 @@ __device__ __forceinline__ floatx4 edge_x32_tile(const EdgeArgs& a, ST& st, int 
     for (int b = 0; b < 4; ++b) silu_blk(fn.v[b]);
     if (valid) store_row32(fn, reinterpret_cast<u16*>(a.fn_out) + (int64_t)e * HID, h);
   }
-  return al;
 }
 
 // ================================================================ the bf16 edge layers on an 8-wave weight ring
@@ -1140,6 +1236,7 @@ using RingSlot = WPipe<u16, RING_NW, true, EL_CAP, 128>;  // slot geometry only 
 struct EdgeRingGeo {
   static constexpr int NW = RING_NW, THREADS = 64 * NW, ROWS_PER_WAVE = 32, ROWS = ROWS_PER_WAVE * NW;
 };
+static_assert(EdgeRingGeo::ROWS_PER_WAVE == FOLD_ROWS, "a fold tile is one wave's rows");
 
 // The ring's LDS counters are read and added with explicit ds_ instructions: through C++ atomics the
 // compiler cannot tell them from the weight slots the in-flight LDS-DMA writes and puts an
@@ -1258,84 +1355,6 @@ struct RingStages {
   __device__ const float* v() const { return slot_v(cur); }
 };
 
-// ---- the node layer's attention aggregation folded into the edge layer (di_edge_layer_attn)
-// h_attn[v] = sum_{e in in(v)} alpha[e, head] * V[src e] / (sum_e alpha[e, head] + 1e-6)
-// (send_and_recv(u_mul_e('V_h','score'), sum), (copy_e('score'), sum), wV / (z + 1e-6):
-// deepinteract_modules.py:93-96, 116). Edges are destination-major, so a destination's in-edges are
-// consecutive rows: a wave's 32 rows hold whole destinations plus at most one continuing from the
-// previous 32-row tile and one continuing into the next. Each lane forms alpha * V[src] for its row
-// (the 64 features of its lane half, in the accumulator quads) and alpha itself; a segmented
-// inclusive scan over the 32 rows -- DPP row shifts by 1, 2, 4, 8 inside each 16-lane row, then the
-// first row's last lane broadcast into the second -- leaves every destination's sums in the lane of
-// its last row here. That lane writes attn[v] = wV / (z + 1e-6) when all of v's in-edges are in this
-// tile, else the partial sums to attn_parts[tile][slot] (slot 1: v continues into the next tile;
-// slot 0: v continues from the previous one); attn_row (the node update) adds a split
-// destination's partials. Summation order: a tree over each tile's rows, then tile by tile.
-constexpr int FOLD_ROWS = 32;   // edges per tile of attn_parts (one wave's rows)
-constexpr int FOLD_PART = 132;  // floats per partial: 128 wV, then z of the 4 heads
-static_assert(EdgeRingGeo::ROWS_PER_WAVE == FOLD_ROWS, "a fold tile is one wave's rows");
-
-// one scan step: lanes whose DPP source row has the same destination add its sums
-template <int CTRL, int ROW_MASK>
-__device__ __forceinline__ void fold_step(X32<4>& s, floatx4& z, int d) {
-  const bool same = __builtin_amdgcn_update_dpp(-2, d, CTRL, ROW_MASK, 0xf, false) == d;
-  auto mv = [](float x) {
-    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL, ROW_MASK, 0xf,
-                                                                  false));
-  };
-#pragma unroll
-  for (int b = 0; b < 4; ++b) {
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      const float t = mv(s.v[b][k]);
-      s.v[b][k] += same ? t : 0.f;
-    }
-    const float t = mv(z[b]);
-    z[b] += same ? t : 0.f;
-  }
-}
-
-__device__ __forceinline__ void edge_attn_fold(const EdgeArgs& a, int e, bool valid, int lane, int h, floatx4 al) {
-  const int d = valid ? a.dst[e] : -1;  // rows past the end: their own (empty) segment
-  if (!valid) al = (floatx4){0.f, 0.f, 0.f, 0.f};
-  R32<4> vr;
-  vr.load(reinterpret_cast<const u16*>(a.qkv) + (int64_t)a.src[e] * 3 * HID + 2 * HID, h);
-  X32<4> s;
-#pragma unroll
-  for (int b = 0; b < 4; ++b)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) set_quad(s.v[b], q, al[b] * unpack4(vr.u[4 * b + q]));
-  floatx4 z = al;
-  fold_step<0x111, 0xf>(s, z, d);  // row_shr:1
-  fold_step<0x112, 0xf>(s, z, d);  // row_shr:2
-  fold_step<0x114, 0xf>(s, z, d);  // row_shr:4
-  fold_step<0x118, 0xf>(s, z, d);  // row_shr:8
-  fold_step<0x142, 0xa>(s, z, d);  // row_bcast:15 into rows 1 and 3 (each lane half's second 16 rows)
-  const int dnext = __shfl_down(d, 1, 32);
-  if (!valid || ((lane & 31) != 31 && dnext == d)) return;
-  const int e0 = a.in_ptr[d], e1 = a.in_ptr[d + 1];
-  const int t = e / FOLD_ROWS, t0 = e0 / FOLD_ROWS, t1 = (e1 - 1) / FOLD_ROWS;
-  if (t0 == t1) {
-    float* row = a.attn_out + (int64_t)d * HID;
-#pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      const float den = z[b] + 1e-6f;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const floatx4 x = quad(s.v[b], q);
-        st4(row + 32 * b + 8 * q + 4 * h, (floatx4){x[0] / den, x[1] / den, x[2] / den, x[3] / den});
-      }
-    }
-  } else {
-    float* p = a.attn_parts + ((int64_t)t * 2 + (t == t0 ? 1 : 0)) * FOLD_PART;
-#pragma unroll
-    for (int b = 0; b < 4; ++b)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) st4(p + 32 * b + 8 * q + 4 * h, quad(s.v[b], q));
-    if (h == 0) st4(p + HID, z);
-  }
-}
-
 template <int MODE, bool GC>
 __global__ __attribute__((amdgpu_flat_work_group_size(1, EdgeRingGeo::THREADS), amdgpu_waves_per_eu(2, 2),
                           amdgpu_num_vgpr(120)))
@@ -1358,8 +1377,7 @@ void k_edge_x32_ring(EdgeArgs a, int ntiles) {
     const int r = tile * EdgeRingGeo::ROWS + wave * EdgeRingGeo::ROWS_PER_WAVE + (lane & 31);
     const bool valid = r < a.Et;
     const int e = valid ? r : a.Et - 1;
-    const floatx4 al = edge_x32_tile<MODE, GC>(a, st, e, valid, lane, h);
-    if (a.attn_out != nullptr) edge_attn_fold(a, e, valid, lane, h, al);
+    edge_x32_tile<MODE, GC>(a, st, e, valid, lane, h);
   }
 }
 

@@ -3,12 +3,13 @@ di_node_update_folded; send_and_recv(u_mul_e('V_h','score'), sum), (copy_e('scor
 wV / (z + 1e-6), deepinteract_modules.py:93-96, 116).
 
 * ragged CSR (in-degrees 0 .. 100: empty destinations, destinations inside one 32-edge fold tile,
-  and destinations spanning 2 .. 5 tiles, with a partial last tile): the complete rows and the
+  and destinations spanning 2 .. 5 tiles, with a partial last tile; the reference-featurised and the
+  general edge kernel): the complete rows and the
   partial sums combined as di_node_update_folded does vs an fp64 torch reference from the same
   launch's alpha and the bf16 V rows -- <= 1e-5 relative (only the fp32 accumulation rounds); the
   launch's F rows and alpha bit-identical to di_edge_layer's; di_node_update_folded vs di_node_update
-  on di_node_aggregate's rows (same weights, only the summation order differs) within 2e-3 of the
-  max |h| (bf16 outputs: one rounding step);
+  on di_node_aggregate's rows (same weights, only the summation order differs) within 4e-3 of the
+  max |h| (bf16 outputs: one rounding step, 2^-8);
 * whole GeoT forward with the fold vs the golden vectors of the reference (tiny/c1/c2) at the bf16
   bound, and vs the fused node layer on a full C3 micro-batch (the bf16 bound: the changed summation
   order flips bf16 roundings of layer 0's outputs).
@@ -53,7 +54,8 @@ def combine(attn, parts, in_ptr):
     return out
 
 
-def test_fold_ragged_csr(eng):
+@pytest.mark.parametrize("geo_ref", [True, False])
+def test_fold_ragged_csr(eng, geo_ref):
     from deepinteract_amd import _lib
     lib, dev = eng.lib, torch.device("cuda")
     g = torch.Generator().manual_seed(11)
@@ -71,26 +73,31 @@ def test_fold_ragged_csr(eng):
     edge_f = torch.rand(E, 28, generator=g)
     f_in = (0.5 * torch.randn(E, 128, generator=g)).bfloat16()
     qkv = (0.5 * torch.randn(n, 384, generator=g)).bfloat16()
+    fn_in = (0.5 * torch.randn(E, 128, generator=g)).bfloat16()  # the general path's gathered rows
     d = {k: x.to(dev) for k, x in dict(dst=dst, src=src, nbr=nbr, node_pos=node_pos, in_ptr=in_ptr, edge_f=edge_f,
-                                       f_in=f_in, qkv=qkv).items()}
+                                       f_in=f_in, qkv=qkv, fn_in=fn_in).items()}
     cg = _lib.DiGraph(n, E, d["src"].data_ptr(), d["dst"].data_ptr(), d["nbr"].data_ptr(), d["node_pos"].data_ptr(),
-                      d["in_ptr"].data_ptr(), _lib.DI_GRAPH_GEO_REF)
+                      d["in_ptr"].data_ptr(), _lib.DI_GRAPH_GEO_REF if geo_ref else 0)
+    fn_in_p = None if geo_ref else d["fn_in"].data_ptr()
+    fn_out = [None if geo_ref else torch.empty(E, 128, dtype=torch.bfloat16, device=dev) for _ in range(2)]
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     em, ev = eng.packed.edge[0]
     alpha0 = torch.empty(E, 4, device=dev)
     f0 = torch.empty(E, 128, dtype=torch.bfloat16, device=dev)
-    assert lib.di_edge_layer(ctypes.byref(cg), _lib.DI_BF16, 0, d["edge_f"].data_ptr(), d["f_in"].data_ptr(), None,
-                             d["qkv"].data_ptr(), em.data_ptr(), ev.data_ptr(), alpha0.data_ptr(), f0.data_ptr(),
-                             None, st) == 0
+    assert lib.di_edge_layer(ctypes.byref(cg), _lib.DI_BF16, 0, d["edge_f"].data_ptr(), d["f_in"].data_ptr(),
+                             fn_in_p, d["qkv"].data_ptr(), em.data_ptr(), ev.data_ptr(), alpha0.data_ptr(),
+                             f0.data_ptr(), None if geo_ref else fn_out[0].data_ptr(), st) == 0
     alpha1 = torch.empty(E, 4, device=dev)
     f1 = torch.empty(E, 128, dtype=torch.bfloat16, device=dev)
     attn = torch.full((n, 128), float("nan"), device=dev)
     parts = torch.full((lib.di_attn_parts_bytes(E) // 4,), float("nan"), device=dev)
     assert lib.di_edge_layer_attn(ctypes.byref(cg), _lib.DI_BF16, 0, d["edge_f"].data_ptr(), d["f_in"].data_ptr(),
-                                  None, d["qkv"].data_ptr(), em.data_ptr(), ev.data_ptr(), alpha1.data_ptr(),
-                                  f1.data_ptr(), None, attn.data_ptr(), parts.data_ptr(), st) == 0
+                                  fn_in_p, d["qkv"].data_ptr(), em.data_ptr(), ev.data_ptr(), alpha1.data_ptr(),
+                                  f1.data_ptr(), None if geo_ref else fn_out[1].data_ptr(), attn.data_ptr(),
+                                  parts.data_ptr(), st) == 0
     torch.cuda.synchronize()
     assert torch.equal(alpha0, alpha1) and torch.equal(f0, f1)
+    assert geo_ref or torch.equal(fn_out[0], fn_out[1])
     # fp64 reference from the launch's own alpha and the bf16 V rows
     a = alpha1.double().cpu().repeat_interleave(32, dim=1)
     v = qkv[:, 256:].double()
@@ -100,7 +107,7 @@ def test_fold_ragged_csr(eng):
     got = combine(attn.cpu(), parts.cpu(), in_ptr)
     assert torch.isfinite(got).all()
     err = ((got - ref).abs().max() / ref.abs().max()).item()
-    print(f"fold ragged: attn rel err {err:.3e} over {n} nodes, {E} edges")
+    print(f"fold ragged (geo_ref={geo_ref}): attn rel err {err:.3e} over {n} nodes, {E} edges")
     assert err < 1e-5
     assert (got[deg == 0] == 0).all()
     # node update from the fold vs from di_node_aggregate's rows (final layer: h and hT)
@@ -125,7 +132,7 @@ def test_fold_ragged_csr(eng):
         outs.append((h_out.float().cpu(), hT.float().cpu()))
     dh = rel_max(outs[1][0].numpy(), outs[0][0].numpy())
     print(f"fold ragged: node update folded vs aggregate rows {dh:.3e}")
-    assert dh < 2e-3
+    assert dh < 4e-3  # one bf16 rounding step of the largest |h| (2^-8)
     assert torch.equal(outs[1][1], outs[1][0].t())
 
 
