@@ -387,7 +387,8 @@ def roofline_of(kern, dtype, traffic=None, mfma_only=False):
     """Roofline of the dominant kernel (largest total time; mfma_only: among the GeoT kernels).
     MFMA-bound kernels report executed FLOPs (what the MFMA pipe runs) with the reference-equivalent
     rate beside it."""
-    cands = {n: r for n, r in kern.items() if not mfma_only or "tflops" in r}
+    # kernels with a rate only (a pair-stream launch the help launches left no bytes to has none)
+    cands = {n: r for n, r in kern.items() if ("tflops" in r if mfma_only else ("tflops" in r or "gbs" in r))}
     dom = max(cands, key=lambda n: cands[n]["total_ms"])
     d = kern[dom]
     if "tflops" in d:

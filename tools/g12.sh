@@ -7,3 +7,4 @@ cd /tmp && timeout -k 10 240 rocprofv3 --kernel-trace --output-format csv -d $O/
 cd $GRAFT_REPO_ROOT && python tools/timeline.py $O/g12_trace/run_kernel_trace.csv --save $O/g12_timeline.csv > $O/g12_timeline.txt 2>&1
 rm -f $O/g12_trace/run_kernel_trace.csv
 TAG=_g12 bash tools/counters.sh
+cd $GRAFT_REPO_ROOT && timeout -k 10 400 python bench.py --dist --no-cpu --no-sub --no-prologue --complexes 64 --steps 2 --warmup 1 > $O/g12_dist.json 2> $O/g12_dist.err
