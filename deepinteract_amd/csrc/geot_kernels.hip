@@ -1687,6 +1687,202 @@ __global__ __launch_bounds__(NodeRingGeo::THREADS, 1) void k_node_update_ring(No
   }
 }
 
+// ================================================================ node layer at full occupancy (bf16)
+// The bf16 di_node_layer (the overlapped schedule's node layer, round 5). k_node_layer runs 16
+// destinations per wave and one 4-wave block per CU (a C3 micro-batch's 16 k nodes are 250 blocks):
+// one latency-bound chain per CU -- in-edge gathers, then eight dependent weight stages. Here a
+// 256-thread block owns 16 destinations and splits BOTH halves of the layer over its threads:
+//   1. the CSR segment sum, 16 lanes per destination, exactly as k_node_aggr (same products, same
+//      order, same division: bit-identical rows), into LDS;
+//   2. O_node + residual, the node FFN and the next layer's Q/K/V with the OUTPUT features split
+//      over the 4 waves (wave w: features 32w..32w+31 of O and of the FFN output, 64w..64w+63 of the
+//      FFN hidden layer, 96w..96w+95 of Q|K|V), each wave reading its A fragments straight from L2
+//      (a wave's slice of a 128x128 matrix is 8 KiB: no LDS weight stages, no stage waits), the
+//      activations between the linears exchanged through LDS as the bf16 operand the MFMAs read.
+// 4x the blocks of k_node_layer (1000 per C3 micro-batch, four per CU): the latency of one block's
+// chain is covered by the others. Per output element the arithmetic is k_node_layer<BF16T>'s (the
+// same bias + residual initial value, the same k-steps in the same order, the same bf16 operands),
+// so h / Q,K,V / hT are bit-identical to di_node_layer's fused and split forms.
+constexpr int NF_NODES = 16;  // destinations per block (16 lanes each in the aggregation)
+template <bool FINAL>
+__global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_eu(4)))
+void k_node_fast(NodeArgs a) {
+  __shared__ __attribute__((aligned(16))) float s_attn[NF_NODES * HID];  // aggregated rows (fp32)
+  __shared__ __attribute__((aligned(16))) u16 s_n[NF_NODES * HID];       // n as a bf16 operand
+  __shared__ __attribute__((aligned(16))) u16 s_t[NF_NODES * 2 * HID];   // FFN hidden (bf16)
+  const int v0 = (int)blockIdx.x * NF_NODES;
+  // ---- 1. wV / (z + 1e-6), 16 lanes per destination (k_node_aggr<BF16T>'s loop)
+  {
+    constexpr int U = AggrCfg<BF16T>::U, FPL = 8;
+    const int j = threadIdx.x & 15, nl = threadIdx.x >> 4;
+    const int v = v0 + nl;
+    float acc[FPL];
+#pragma unroll
+    for (int f = 0; f < FPL; ++f) acc[f] = 0.f;
+    float z = 0.f;
+    if (v < a.Nt) {  // uniform per 16-lane group (the shuffles stay inside the group)
+      const int head = (FPL * j) >> 5;
+      const u16* vbase = reinterpret_cast<const u16*>(a.qkv) + 2 * HID + FPL * j;
+      const int e0 = a.in_ptr[v], e1 = a.in_ptr[v + 1];
+      const int lane_base = threadIdx.x & 48;
+      int id_next = e0 + j < e1 ? a.src[e0 + j] : 0;
+#pragma unroll 1
+      for (int c = e0; c < e1; c += U) {
+        const int n = min(U, e1 - c);
+        const int id_cur = id_next;
+        int ids[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) ids[u] = __shfl(id_cur, lane_base + (u & 15), 64);
+        float al[U];
+        u16 vv[U][FPL];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          if (u < n) {
+            al[u] = a.alpha[(int64_t)(c + u) * 4 + head];
+            *reinterpret_cast<uint4*>(vv[u]) = *reinterpret_cast<const uint4*>(vbase + (int64_t)ids[u] * 3 * HID);
+          }
+        }
+        if (c + U < e1) id_next = c + U + j < e1 && j < U ? a.src[c + U + j] : 0;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          if (u < n) {
+#pragma unroll
+            for (int f = 0; f < FPL; ++f) acc[f] += al[u] * __builtin_bit_cast(float, (uint32_t)vv[u][f] << 16);
+            z += al[u];
+          }
+        }
+      }
+    }
+    const float d = z + 1e-6f;
+    float* out = s_attn + nl * HID + FPL * j;
+    st4(out, (floatx4){acc[0] / d, acc[1] / d, acc[2] / d, acc[3] / d});
+    st4(out + 4, (floatx4){acc[4] / d, acc[5] / d, acc[6] / d, acc[7] / d});
+  }
+  // ---- 2. the update, output features split over the waves
+  const int lane = lane_id(), g = lane >> 4, r = lane & 15;
+  const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+  const int v = v0 + r;
+  const bool valid = v < a.Nt;
+  const int vc = valid ? v : a.Nt - 1;
+  const u16* W = reinterpret_cast<const u16*>(a.wmat);
+  const float* V = a.wvec;
+  // A fragment (output block bo, k-step s) of the 128x128 matrix at packed block m, from L2
+  auto frag = [&](int m, int bo, int s) {
+    return *reinterpret_cast<const bf16x8*>(W + (m + bo * 4 + s) * BLK + lane * 8);
+  };
+  // the bf16 operand of 16 rows stored row-major in LDS (make_op's packing of blocks 2s, 2s+1)
+  auto lds_op = [&](const u16* rows, int stride, int f0) {
+    Op<BF16T, 4> o;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const uint2 lo = *reinterpret_cast<const uint2*>(rows + r * stride + f0 + 32 * s + 4 * g);
+      const uint2 hi = *reinterpret_cast<const uint2*>(rows + r * stride + f0 + 32 * s + 16 + 4 * g);
+      o.f[s] = __builtin_bit_cast(bf16x8, (uint4){lo.x, lo.y, hi.x, hi.y});
+    }
+    return o;
+  };
+  auto put_slice = [&](u16* rows, int stride, int f, floatx4 x) {
+    *reinterpret_cast<uint2*>(rows + r * stride + f + 4 * g) = (uint2){pack_bf16x2(x[0], x[1]), pack_bf16x2(x[2], x[3])};
+  };
+  // n = b_O + h_in + O(attn), this wave's blocks 2w, 2w+1
+  Act<2> n;
+#pragma unroll
+  for (int b = 0; b < 2; ++b)
+    n.v[b] = ld4(V + NLV_ON + 16 * (2 * w + b) + 4 * g) +
+             ld4(reinterpret_cast<const u16*>(a.h_in) + (int64_t)vc * HID + 16 * (2 * w + b) + 4 * g);
+  bf16x8 fo[2][4];
+#pragma unroll
+  for (int b = 0; b < 2; ++b)
+#pragma unroll
+    for (int s = 0; s < 4; ++s) fo[b][s] = frag(NL_ON, 2 * w + b, s);
+  __syncthreads();  // the aggregated rows
+  {
+    Act<8> wv;
+#pragma unroll
+    for (int b = 0; b < 8; ++b) wv.v[b] = *reinterpret_cast<const floatx4*>(s_attn + r * HID + 16 * b + 4 * g);
+    Op<BF16T, 4> op;
+    make_op(op, wv);
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int s = 0; s < 4; ++s) n.v[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fo[b][s], op.f[s], n.v[b], 0, 0, 0);
+  }
+#pragma unroll
+  for (int b = 0; b < 2; ++b) put_slice(s_n, HID, 16 * (2 * w + b), n.v[b]);
+  // FFN hidden: this wave's 64 features 64w.. (half hf = w / 2, output blocks 4 (w % 2) + b)
+  const int hf = w >> 1;
+  bf16x8 f1[4][4];
+#pragma unroll
+  for (int b = 0; b < 4; ++b)
+#pragma unroll
+    for (int s = 0; s < 4; ++s) f1[b][s] = frag(NL_F1 + MAT128 * hf, 4 * (w & 1) + b, s);
+  Act<4> t;
+#pragma unroll
+  for (int b = 0; b < 4; ++b) t.v[b] = ld4(V + NLV_F1 + 64 * w + 16 * b + 4 * g);
+  __syncthreads();  // n, all 128 features
+  {
+    const Op<BF16T, 4> nop = lds_op(s_n, HID, 0);
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+#pragma unroll
+      for (int s = 0; s < 4; ++s) t.v[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f1[b][s], nop.f[s], t.v[b], 0, 0, 0);
+  }
+  silu2_<4, true>(t);
+#pragma unroll
+  for (int b = 0; b < 4; ++b) put_slice(s_t, 2 * HID, 64 * w + 16 * b, t.v[b]);
+  // FFN output (blocks 2w, 2w+1): both hidden halves in order, as k_node_layer
+  bf16x8 f2[2][2][4];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int s = 0; s < 4; ++s) f2[h][b][s] = frag(NL_F2 + MAT128 * h, 2 * w + b, s);
+  __syncthreads();  // the hidden layer, all 256 features (and every wave is past its n operand)
+  Act<2> o;
+  zero(o);
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const Op<BF16T, 4> top = lds_op(s_t, 2 * HID, HID * h);
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int s = 0; s < 4; ++s) o.v[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f2[h][b][s], top.f[s], o.v[b], 0, 0, 0);
+  }
+  add_(n, o);
+  u16* hrow = reinterpret_cast<u16*>(a.h_out) + (int64_t)v * HID;
+  if (valid) {
+#pragma unroll
+    for (int b = 0; b < 2; ++b) st4(hrow + 16 * (2 * w + b) + 4 * g, n.v[b]);
+  }
+  if constexpr (FINAL) {
+    if (a.hT_out != nullptr && valid) {
+      u16* hT = reinterpret_cast<u16*>(a.hT_out);
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          hT[(int64_t)(16 * (2 * w + b) + 4 * g + q) * a.Nt + v] = (u16)(pack_bf16x2(n.v[b][q], 0.f) & 0xffffu);
+    }
+  } else {
+    // next layer's Q | K | V from the new h: this wave's 6 output blocks 6w .. 6w+5 of the 24
+#pragma unroll
+    for (int b = 0; b < 2; ++b) put_slice(s_n, HID, 16 * (2 * w + b), n.v[b]);
+    __syncthreads();  // the new h, all 128 features (s_n's previous readers finished before the last barrier)
+    const Op<BF16T, 4> hop = lds_op(s_n, HID, 0);
+    u16* qo = reinterpret_cast<u16*>(a.qkv_out) + (int64_t)v * 3 * HID;
+#pragma unroll
+    for (int b = 0; b < 6; ++b) {
+      const int ob = 6 * w + b;  // Q blocks 0-7, K 8-15, V 16-23
+      floatx4 x = ld4(V + NLV_Q + 16 * ob + 4 * g);
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+        x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag(NL_Q + MAT128 * (ob >> 3), ob & 7, s), hop.f[s], x, 0, 0, 0);
+      if (valid) st4(qo + 16 * ob + 4 * g, x);
+    }
+  }
+}
+
 // ================================================================ fused node layer
 // Every bias vector rides in its stage's LDS slot (init_vec_lds) and the node's own input row is
 // added right after the stage barrier, before the next stage's DMA is issued: a global load
@@ -1987,8 +2183,11 @@ extern "C" int di_node_layer(const di_graph* g, di_dtype dt, int final_layer, co
   hipStream_t s = (hipStream_t)stream;
   const dim3 grid = grid_of<NodeGeo>(a.Nt), block = block_of<NodeGeo>();
   if (dt == DI_BF16) {
-    if (final_layer) hipLaunchKernelGGL((k_node_layer<BF16T, true>), grid, block, 0, s, a);
-    else hipLaunchKernelGGL((k_node_layer<BF16T, false>), grid, block, 0, s, a);
+    // 16 destinations per 256-thread block, output features split over its waves (k_node_fast)
+    if (!g->src || !g->in_ptr) return DI_EINVAL;
+    const dim3 gf((unsigned)((a.Nt + NF_NODES - 1) / NF_NODES)), bf(256);
+    if (final_layer) hipLaunchKernelGGL((k_node_fast<true>), gf, bf, 0, s, a);
+    else hipLaunchKernelGGL((k_node_fast<false>), gf, bf, 0, s, a);
   } else {
     if (final_layer) hipLaunchKernelGGL((k_node_layer<F32T, true>), grid, block, 0, s, a);
     else hipLaunchKernelGGL((k_node_layer<F32T, false>), grid, block, 0, s, a);
