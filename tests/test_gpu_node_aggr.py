@@ -1,8 +1,10 @@
-"""Node-layer split (di_node_aggregate + di_node_update) vs the fused di_node_layer, and the CSR
-segment reduction itself vs an fp64 torch reference on ragged in-degrees.
+"""Node-layer split (di_node_aggregate + di_node_update) vs the fused di_node_layer (bf16:
+k_node_fast, 16 destinations per block with the update split over its waves; fp32: k_node_layer),
+and the CSR segment reduction itself vs an fp64 torch reference on ragged in-degrees.
 
-* split vs fused: bit-identical (same products, same edge order, same division), fp32 and bf16,
-  on the golden cases and on a full C3 micro-batch (8 x 2x1000 residues, k = 20);
+* split vs fused: bit-identical (same products, same edge order, same division, the same k-steps
+  of every linear), fp32 and bf16, on the golden cases and on a full C3 micro-batch (8 x 2x1000
+  residues, k = 20);
 * di_node_aggregate vs fp64 torch on a ragged CSR (in-degrees 0..40, i.e. empty segments and
   segments spanning several 16-edge chunks): <= 1e-5 relative for fp32 V, and for bf16 V (the
   bf16 values are exact in fp32; only the fp32 accumulation rounds).

@@ -5,7 +5,7 @@ one forward is run first). Per background kind: the pair stream's rate over the 
 background covers, and the background kernel's mean duration beside it, vs both alone.
 
 usage (GPU box): python tools/diag/interference.py [--jobs 12]
-One JSON line per background kind (none, init, edge0, node0, edge1, node1).
+One JSON line per background kind (none, init, init_res, edge0, node0, edge1, node1).
 """
 import argparse
 import ctypes
@@ -26,6 +26,7 @@ from deepinteract_amd.weights import seeded_state_dict  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--jobs", type=int, default=12)
+    ap.add_argument("--only", default=None, help="comma-separated background kinds")
     args = ap.parse_args()
     dev = torch.device("cuda")
     lib = _lib.load()
@@ -45,6 +46,9 @@ def main():
             rc = lib.di_embed_init_edge(g, dt, gb.node_f.shape[1], _ptr(gb.node_f), _ptr(p.embed[0]), _ptr(p.embed[1]),
                                         _ptr(h[0]), _ptr(qkv[0]), _ptr(gb.edge_f), _ptr(p.init[0]), _ptr(p.init[1]),
                                         _ptr(p.pos_src), _ptr(p.pos_dst), _ptr(f[0]), _ptr(None), -1, st)
+        elif kind == "init_res":
+            rc = lib.di_init_edge_resident(g, _ptr(gb.edge_f), _ptr(p.init[0]), _ptr(p.init[1]), _ptr(p.pos_src),
+                                           _ptr(p.pos_dst), _ptr(f[0]), st)
         elif kind in ("edge0", "edge1"):
             li = 0 if kind == "edge0" else 1
             em, ev = p.edge[li]
@@ -130,7 +134,11 @@ def main():
     base["rate"] = r0["pair_tb_s"]
     print(json.dumps(r0))
     # enough launches to cover ~80 % of the pair window (pair ~1 ms per job beside)
-    for kind, us in (("init", 140), ("edge0", 430), ("node0", 52), ("edge1", 330), ("node1", 45)):
+    kinds = sys.argv[sys.argv.index("--only") + 1].split(",") if "--only" in sys.argv else \
+        ["init", "init_res", "edge0", "node0", "edge1", "node1"]
+    est = {"init": 140, "init_res": 140, "edge0": 430, "node0": 52, "edge1": 330, "node1": 45}
+    for kind in kinds:
+        us = est[kind]
         print(json.dumps(beside(kind, 800.0 / us)), flush=True)
 
 
