@@ -1705,7 +1705,9 @@ __global__ __launch_bounds__(NodeRingGeo::THREADS, 1) void k_node_update_ring(No
 // so h / Q,K,V / hT are bit-identical to di_node_layer's fused and split forms.
 constexpr int NF_NODES = 16;  // destinations per block (16 lanes each in the aggregation)
 template <bool FINAL>
-__global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_eu(4)))
+// <= 120 VGPRs (amdgpu_num_vgpr counts register pairs): four waves per SIMD leave one pair-stream
+// wave room beside them
+__global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_eu(4), amdgpu_num_vgpr(60)))
 void k_node_fast(NodeArgs a) {
   __shared__ __attribute__((aligned(16))) float s_attn[NF_NODES * HID];  // aggregated rows (fp32)
   __shared__ __attribute__((aligned(16))) u16 s_n[NF_NODES * HID];       // n as a bf16 operand
@@ -1849,6 +1851,14 @@ void k_node_fast(NodeArgs a) {
 #pragma unroll
       for (int s = 0; s < 4; ++s) o.v[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f2[h][b][s], top.f[s], o.v[b], 0, 0, 0);
   }
+  // the first half of this wave's Q | K | V fragments, in flight across the h exchange below
+  bf16x8 fq[3][4];
+  if constexpr (!FINAL) {
+#pragma unroll
+    for (int b = 0; b < 3; ++b)
+#pragma unroll
+      for (int s = 0; s < 4; ++s) fq[b][s] = frag(NL_Q + MAT128 * ((6 * w + b) >> 3), (6 * w + b) & 7, s);
+  }
   add_(n, o);
   u16* hrow = reinterpret_cast<u16*>(a.h_out) + (int64_t)v * HID;
   if (valid) {
@@ -1877,7 +1887,8 @@ void k_node_fast(NodeArgs a) {
       floatx4 x = ld4(V + NLV_Q + 16 * ob + 4 * g);
 #pragma unroll
       for (int s = 0; s < 4; ++s)
-        x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag(NL_Q + MAT128 * (ob >> 3), ob & 7, s), hop.f[s], x, 0, 0, 0);
+        x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b < 3 ? fq[b][s] : frag(NL_Q + MAT128 * (ob >> 3), ob & 7, s),
+                                                    hop.f[s], x, 0, 0, 0);
       if (valid) st4(qo + 16 * ob + 4 * g, x);
     }
   }
