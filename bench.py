@@ -157,16 +157,20 @@ def max_over_ranks(ws, x):
     return float(t.item())
 
 
-def load_pmc_traffic(kernel):
+def load_pmc_traffic(kernel, alg_bytes_per_launch=None):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary (separate
-    --pmc passes, FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM), or None."""
+    --pmc passes, FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM), or None. The pair stream's
+    entry is a ratio to its algorithmic bytes (its launch covers a whole step's jobs, and it is
+    profiled standalone: tools/pmc_pair_ratio.py), scaled here to this run's launch."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as fh:
-            d = json.load(fh)
-        return d.get(kernel, {}).get("hbm_bytes_per_launch")
+            rec = json.load(fh).get(kernel, {})
     except (OSError, ValueError):
         return None
+    if "hbm_bytes_per_alg_byte" in rec:
+        return rec["hbm_bytes_per_alg_byte"] * alg_bytes_per_launch if alg_bytes_per_launch else None
+    return rec.get("hbm_bytes_per_launch")
 
 
 def cpu_baseline(n_res, k, sample, threads, warmup=3):
@@ -226,8 +230,8 @@ def allgather_record(ws, rank, complexes, n_res, k, dev, reps=3, per_rank=4):
     """Supplementary, outside the metric, two parts:
     1. the C4 driver end to end on REAL maps: distributed.predict_sharded over `per_rank` synthetic
        complexes per rank (device builder -> bf16 GeoT -> pair tensor -> bf16 head -> contact
-       probabilities), micro-batches of one complex, timed three ways: no collective (the compute
-       alone), the maps gathered round by round with asynchronous all-gathers overlapped with the
+       probabilities), micro-batches of one complex, timed three ways (each `reps` times, interleaved,
+       fastest run kept): no collective (the compute alone), the maps gathered round by round with asynchronous all-gathers overlapped with the
        next micro-batch (chunked, the default) and gathered once at the end; the collectives of the
        chunked plan are then timed alone, giving exposed = t(chunked) - t(compute) and hidden =
        t(collectives alone) - exposed. Every rank checks it holds every map, chunked == once;
@@ -252,9 +256,15 @@ def allgather_record(ws, rank, complexes, n_res, k, dev, reps=3, per_rank=4):
         torch.cuda.synchronize()
         return max_over_ranks(ws, time.perf_counter() - t0), maps, plan
 
-    t_none, mine, plan = run("none")
-    t_chunk, maps, _ = run("chunked")
-    t_once, maps_once, _ = run("once")
+    # each mode `reps` times, interleaved, the fastest run of each (one run is ~0.3 s and includes the
+    # host-side graph building, whose jitter is larger than the collectives)
+    best = {}
+    for _ in range(reps):
+        for mode in ("none", "chunked", "once"):
+            t_m, maps_m, plan = run(mode)
+            if mode not in best or t_m < best[mode][0]:
+                best[mode] = (t_m, maps_m)
+    (t_none, mine), (t_chunk, maps), (t_once, maps_once) = best["none"], best["chunked"], best["once"]
     identical = all(torch.equal(a, b) for a, b in zip(maps, maps_once))
     # the chunked plan's collectives alone, on the maps already computed
     sizes = [(n_res, n_res)] * len(cx)
@@ -632,7 +642,8 @@ def main():
     pmc_shape = (args.config, M, n_res, k, args.layers, args.dtype, args.overlap, args.geo_ref) == \
         ("c3", 8, 1000, 20, 2, "bf16", 1, 1)
     roof = roofline_of(kern, args.dtype)
-    roof["traffic"] = load_pmc_traffic(roof["kernel"]) if pmc_shape else None
+    roof["traffic"] = load_pmc_traffic(roof["kernel"], kern.get(roof["kernel"], {}).get("bytes_per_launch")) \
+        if pmc_shape else None
     bytes_c = algorithmic_bytes_per_complex(n_res, n_res, k, esz)
     hbm_frac = bytes_c * value / ws / (HBM_PEAK_GBS * 1e9)
     flops_c = algorithmic_flops_per_complex(n_res, n_res, k, args.layers)

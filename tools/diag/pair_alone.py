@@ -25,6 +25,8 @@ def main():
     ap.add_argument("--jobs", type=int, default=16)
     ap.add_argument("--complexes", type=int, default=8)
     ap.add_argument("--res", type=int, default=1000)
+    ap.add_argument("--stream-only", action="store_true",
+                    help="only the beside shape (128 x 4 stream): the PMC traffic pass (tools/pmc_pair_ratio.py)")
     args = ap.parse_args()
     lib, dev = _lib.load(), torch.device("cuda")
     H, M, L = 128, args.complexes, args.res
@@ -78,6 +80,11 @@ def main():
         return t, c
 
     out = []
+    if args.stream_only:
+        t, c = queue_run("stream", 128, 4)
+        print(json.dumps({"what": "di_pair_stream (bounded nt stores)", "blocks": 128, "waves": 4, "jobs_per_launch": args.jobs,
+                          "launches": 4, "us_per_job": 1e6 * t / args.jobs, "tb_s": job_bytes * args.jobs / t / 1e12}))
+        return
     for blocks, waves in ((128, 4), (256, 4), (128, 8), (256, 8), (64, 4)):
         t, c = queue_run("stream", blocks, waves)
         out.append({"what": "di_pair_stream (bounded nt stores)", "blocks": blocks, "waves": waves,

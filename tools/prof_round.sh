@@ -17,7 +17,7 @@ if [[ "$PH" == *a* ]]; then
   "smoke:200:python __graft_entry__.py smoke" \
   "bench:400:python bench.py --steps 20 --warmup 5 > $O/bench.json" \
   "bench_serial:300:python bench.py --overlap 0 --no-cpu > $O/bench_serial.json" \
-  "bench_dist:300:python bench.py --dist --no-cpu --no-sub --no-prologue --complexes 64 --steps 2 --warmup 1 > $O/bench_dist.json" \
+  "bench_dist:300:python bench.py --dist --no-cpu --no-sub --no-prologue --complexes 256 --steps 2 --warmup 1 > $O/bench_dist.json" \
   "bench_c5:400:python bench.py --config c5 --steps 3 --warmup 1 > $O/bench_c5.json" \
   || exit $?
 fi
