@@ -1282,15 +1282,35 @@ __device__ __forceinline__ void dma_piece(rsrc4 r, uint32_t lds, int voff, int s
       : "memory", "m0");
 }
 
+// What one ring stage loads: up to three runs of packed 512-element blocks (laid out back to back in
+// the slot) and an optional bias vector (128 floats, after the slot's blocks).
+struct RingPieces {
+  const u16* w;  // blob base
+  int off[3], n[3];
+  int np;
+  const float* v;  // bias vector or null
+};
+// the bf16 edge layer's stages (EL_ORDER / EL_SIZE / EL_VEC): one run each
 template <int NS, bool GC>
-struct RingStages {
-  char* base;          // RING_SLOTS x RingSlot::SLOT_BYTES
-  uint32_t* full;      // [RING_SLOTS]: stage uses published (1 per use)
-  uint32_t* freec;     // [RING_SLOTS]: wave releases (RING_NW per use)
+struct EdgeRingSrc {
   const u16* W;
   const float* V;
+  __device__ RingPieces operator()(int gs) const {
+    const int s = gs % NS;
+    const int si = GC ? s + 2 : s;
+    const int vo = (GC && s == 0) ? ELV_OM : EL_VEC[si];
+    return {W, {EL_ORDER[si], 0, 0}, {EL_SIZE[si], 0, 0}, 1, vo >= 0 ? V + vo : nullptr};
+  }
+};
+
+template <class SRC, int NW = RING_NW>
+struct RingStagesT {
+  char* base;          // RING_SLOTS x RingSlot::SLOT_BYTES
+  uint32_t* full;      // [RING_SLOTS]: stage uses published (1 per use)
+  uint32_t* freec;     // [RING_SLOTS]: wave releases (NW per use)
+  SRC src;             // global stage -> its weight runs and bias
   int wave;
-  int total;           // global stages of this block (tiles x NS)
+  int total;           // global stages of this block
   int g = 0;           // next stage to consume
   int issued = 0;      // stages [0, issued) are issued (by their owners)
   int pending = -1;    // a stage this wave issued and has not published yet
@@ -1299,35 +1319,36 @@ struct RingStages {
   __device__ float* slot_v(int sl) const {
     return reinterpret_cast<float*>(base + sl * RingSlot::SLOT_BYTES + EL_CAP * BLK * 2);
   }
-  // global stage gs is loaded and published by ONE wave, gs % RING_NW (its owner): all its 1-KiB
+  // global stage gs is loaded and published by ONE wave, gs % NW (its owner): all its 1-KiB
   // LDS-DMA pieces and the bias vector. Issued by inline asm: the compiler's waitcnt pass cannot tell a
   // ring slot (runtime index) from the one being read and would wait for every piece before the next
   // ds_read -- completion is what FULL tracks (the owner's vmcnt(0), then its publish).
   __device__ void issue_one(int gs) {
-    const int s = gs % NS;
-    const int si = GC ? s + 2 : s;
-    const int vo = (GC && s == 0) ? ELV_OM : EL_VEC[si];
+    const RingPieces p = src(gs);
     const int sl = gs % RING_SLOTS;
-    const uint32_t dst = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)slot_w(sl);
-    const int nkib = EL_SIZE[si];  // 512 bf16 elements = 1 KiB per block
+    uint32_t dst = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)slot_w(sl);
     const int loff = (threadIdx.x & 63) * 16;
-    const rsrc4 r = rsrc_of(W + EL_ORDER[si] * BLK);
-    for (int i = 0; i < nkib; ++i) dma_piece(r, dst + i * 1024, loff, i * 1024);
-    if (vo >= 0 && (threadIdx.x & 63) < 32) dma_piece(rsrc_of(V + vo), dst + EL_CAP * BLK * 2, loff, 0);
+    for (int k = 0; k < p.np; ++k) {
+      const rsrc4 r = rsrc_of(p.w + p.off[k] * BLK);
+      for (int i = 0; i < p.n[k]; ++i) dma_piece(r, dst + i * 1024, loff, i * 1024);  // 1 KiB per block
+      dst += p.n[k] * 1024;
+    }
+    if (p.v && (threadIdx.x & 63) < 32)
+      dma_piece(rsrc_of(p.v), (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)slot_v(sl), loff, 0);
     pending = gs;
   }
   // stages issued ahead of the one consumed, owners' slots permitting
   __device__ void issue_ahead() {
     for (; issued <= g + RING_AHEAD && issued < total; ++issued) {
-      if (issued % RING_NW != wave) continue;
+      if (issued % NW != wave) continue;
       const int prev = issued - RING_SLOTS;  // the stage that used this slot last
-      if (prev >= 0) lds_wait_ge(freec + issued % RING_SLOTS, (uint32_t)(RING_NW * (prev / RING_SLOTS + 1)));
+      if (prev >= 0) lds_wait_ge(freec + issued % RING_SLOTS, (uint32_t)(NW * (prev / RING_SLOTS + 1)));
       issue_one(issued);
     }
   }
   __device__ void fill() {
     for (; issued < RING_AHEAD && issued < total; ++issued)
-      if (issued % RING_NW == wave) issue_one(issued);
+      if (issued % NW == wave) issue_one(issued);
   }
   // settle(): an empty asm reading the rows the caller loaded just before this call (F rows, K / Q):
   // the compiler then waits for them HERE, after the vmcnt(0) that has landed them anyway -- not after
@@ -1354,6 +1375,8 @@ struct RingStages {
   }
   __device__ const float* v() const { return slot_v(cur); }
 };
+template <int NS, bool GC>
+using RingStages = RingStagesT<EdgeRingSrc<NS, GC>>;
 
 template <int MODE, bool GC>
 __global__ __attribute__((amdgpu_flat_work_group_size(1, EdgeRingGeo::THREADS), amdgpu_waves_per_eu(2, 2),
@@ -1368,7 +1391,7 @@ void k_edge_x32_ring(EdgeArgs a, int ntiles) {
   const int my_tiles = ((int)blockIdx.x < ntiles) ? (ntiles - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
   if (threadIdx.x < 2 * RING_SLOTS) counters[threadIdx.x] = 0;
   __syncthreads();
-  RingStages<NS, GC> st{lds, counters, counters + RING_SLOTS, reinterpret_cast<const u16*>(a.wmat), a.wvec, wave,
+  RingStages<NS, GC> st{lds, counters, counters + RING_SLOTS, {reinterpret_cast<const u16*>(a.wmat), a.wvec}, wave,
                         my_tiles * NS};
   st.fill();
 #pragma unroll 1
@@ -1703,21 +1726,28 @@ __global__ __launch_bounds__(NodeRingGeo::THREADS, 1) void k_node_update_ring(No
 // chain is covered by the others. Per output element the arithmetic is k_node_layer<BF16T>'s (the
 // same bias + residual initial value, the same k-steps in the same order, the same bf16 operands),
 // so h / Q,K,V / hT are bit-identical to di_node_layer's fused and split forms.
-constexpr int NF_NODES = 16;  // destinations per block (16 lanes each in the aggregation)
-template <bool FINAL>
+// NG node groups of 16 destinations per block and 4 NG waves: every wave computes its output blocks
+// for ALL the block's groups, so one A-fragment load from L2 feeds NG MFMAs (NG = 2 halves the L2
+// weight stream per node). Blocks per wave: O / FFN output 8 / (4 NG), hidden 16 / (4 NG),
+// Q|K|V 24 / (4 NG).
+constexpr int NF_NODES = 16;  // destinations per node group (16 lanes each in the aggregation)
+constexpr int NF_GROUPS = 1;  // node groups per block (the launch; 2 measured slower: each wave's chain doubles)
+template <bool FINAL, int NG>
 // <= 120 VGPRs (amdgpu_num_vgpr counts register pairs): four waves per SIMD leave one pair-stream
 // wave room beside them
-__global__ __attribute__((amdgpu_flat_work_group_size(1, 256), amdgpu_waves_per_eu(4), amdgpu_num_vgpr(60)))
+__global__ __attribute__((amdgpu_flat_work_group_size(1, 256 * NG), amdgpu_waves_per_eu(4), amdgpu_num_vgpr(60)))
 void k_node_fast(NodeArgs a) {
-  __shared__ __attribute__((aligned(16))) float s_attn[NF_NODES * HID];  // aggregated rows (fp32)
-  __shared__ __attribute__((aligned(16))) u16 s_n[NF_NODES * HID];       // n as a bf16 operand
-  __shared__ __attribute__((aligned(16))) u16 s_t[NF_NODES * 2 * HID];   // FFN hidden (bf16)
-  const int v0 = (int)blockIdx.x * NF_NODES;
+  constexpr int NWV = 4 * NG, BO = 8 / NWV, BH = 16 / NWV, BQ = 24 / NWV;
+  static_assert(8 % NWV == 0 && BQ >= 1, "node groups per block: 1 or 2");
+  __shared__ __attribute__((aligned(16))) float s_attn[NG * NF_NODES * HID];  // aggregated rows (fp32)
+  __shared__ __attribute__((aligned(16))) u16 s_n[NG * NF_NODES * HID];       // n as a bf16 operand
+  __shared__ __attribute__((aligned(16))) u16 s_t[NG * NF_NODES * 2 * HID];   // FFN hidden (bf16)
+  const int vb = (int)blockIdx.x * NG * NF_NODES;  // the block's first destination
   // ---- 1. wV / (z + 1e-6), 16 lanes per destination (k_node_aggr<BF16T>'s loop)
   {
     constexpr int U = AggrCfg<BF16T>::U, FPL = 8;
-    const int j = threadIdx.x & 15, nl = threadIdx.x >> 4;
-    const int v = v0 + nl;
+    const int j = threadIdx.x & 15, nl = threadIdx.x >> 4;  // nl: the block's destination 0 .. 16 NG - 1
+    const int v = vb + nl;
     float acc[FPL];
 #pragma unroll
     for (int f = 0; f < FPL; ++f) acc[f] = 0.f;
@@ -1760,136 +1790,161 @@ void k_node_fast(NodeArgs a) {
     st4(out, (floatx4){acc[0] / d, acc[1] / d, acc[2] / d, acc[3] / d});
     st4(out + 4, (floatx4){acc[4] / d, acc[5] / d, acc[6] / d, acc[7] / d});
   }
-  // ---- 2. the update, output features split over the waves
+  // ---- 2. the update: wave w computes its output blocks for every node group
   const int lane = lane_id(), g = lane >> 4, r = lane & 15;
   const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
-  const int v = v0 + r;
-  const bool valid = v < a.Nt;
-  const int vc = valid ? v : a.Nt - 1;
+  int vq[NG];
+  bool valid[NG];
+#pragma unroll
+  for (int q = 0; q < NG; ++q) {
+    vq[q] = vb + q * NF_NODES + r;
+    valid[q] = vq[q] < a.Nt;
+  }
   const u16* W = reinterpret_cast<const u16*>(a.wmat);
   const float* V = a.wvec;
   // A fragment (output block bo, k-step s) of the 128x128 matrix at packed block m, from L2
   auto frag = [&](int m, int bo, int s) {
     return *reinterpret_cast<const bf16x8*>(W + (m + bo * 4 + s) * BLK + lane * 8);
   };
-  // the bf16 operand of 16 rows stored row-major in LDS (make_op's packing of blocks 2s, 2s+1)
-  auto lds_op = [&](const u16* rows, int stride, int f0) {
+  // the bf16 operand of group q's 16 rows stored row-major in LDS (make_op's packing of blocks 2s, 2s+1)
+  auto lds_op = [&](const u16* rows, int stride, int q, int f0) {
     Op<BF16T, 4> o;
+    const u16* row = rows + (q * NF_NODES + r) * stride + f0;
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      const uint2 lo = *reinterpret_cast<const uint2*>(rows + r * stride + f0 + 32 * s + 4 * g);
-      const uint2 hi = *reinterpret_cast<const uint2*>(rows + r * stride + f0 + 32 * s + 16 + 4 * g);
+      const uint2 lo = *reinterpret_cast<const uint2*>(row + 32 * s + 4 * g);
+      const uint2 hi = *reinterpret_cast<const uint2*>(row + 32 * s + 16 + 4 * g);
       o.f[s] = __builtin_bit_cast(bf16x8, (uint4){lo.x, lo.y, hi.x, hi.y});
     }
     return o;
   };
-  auto put_slice = [&](u16* rows, int stride, int f, floatx4 x) {
-    *reinterpret_cast<uint2*>(rows + r * stride + f + 4 * g) = (uint2){pack_bf16x2(x[0], x[1]), pack_bf16x2(x[2], x[3])};
+  auto put_slice = [&](u16* rows, int stride, int q, int f, floatx4 x) {
+    *reinterpret_cast<uint2*>(rows + (q * NF_NODES + r) * stride + f + 4 * g) =
+        (uint2){pack_bf16x2(x[0], x[1]), pack_bf16x2(x[2], x[3])};
   };
-  // n = b_O + h_in + O(attn), this wave's blocks 2w, 2w+1
-  Act<2> n;
+  // n = b_O + h_in + O(attn): output blocks BO w .. BO w + BO - 1
+  Act<BO> n[NG];
 #pragma unroll
-  for (int b = 0; b < 2; ++b)
-    n.v[b] = ld4(V + NLV_ON + 16 * (2 * w + b) + 4 * g) +
-             ld4(reinterpret_cast<const u16*>(a.h_in) + (int64_t)vc * HID + 16 * (2 * w + b) + 4 * g);
-  bf16x8 fo[2][4];
+  for (int q = 0; q < NG; ++q)
 #pragma unroll
-  for (int b = 0; b < 2; ++b)
+    for (int b = 0; b < BO; ++b) {
+      const int ob = BO * w + b;
+      const int vc = valid[q] ? vq[q] : a.Nt - 1;
+      n[q].v[b] = ld4(V + NLV_ON + 16 * ob + 4 * g) +
+                  ld4(reinterpret_cast<const u16*>(a.h_in) + (int64_t)vc * HID + 16 * ob + 4 * g);
+    }
+  bf16x8 fo[BO][4];
 #pragma unroll
-    for (int s = 0; s < 4; ++s) fo[b][s] = frag(NL_ON, 2 * w + b, s);
+  for (int b = 0; b < BO; ++b)
+#pragma unroll
+    for (int s = 0; s < 4; ++s) fo[b][s] = frag(NL_ON, BO * w + b, s);
   __syncthreads();  // the aggregated rows
-  {
+#pragma unroll
+  for (int q = 0; q < NG; ++q) {
     Act<8> wv;
 #pragma unroll
-    for (int b = 0; b < 8; ++b) wv.v[b] = *reinterpret_cast<const floatx4*>(s_attn + r * HID + 16 * b + 4 * g);
+    for (int b = 0; b < 8; ++b)
+      wv.v[b] = *reinterpret_cast<const floatx4*>(s_attn + (q * NF_NODES + r) * HID + 16 * b + 4 * g);
     Op<BF16T, 4> op;
     make_op(op, wv);
 #pragma unroll
-    for (int b = 0; b < 2; ++b)
+    for (int b = 0; b < BO; ++b)
 #pragma unroll
-      for (int s = 0; s < 4; ++s) n.v[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fo[b][s], op.f[s], n.v[b], 0, 0, 0);
+      for (int s = 0; s < 4; ++s) n[q].v[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fo[b][s], op.f[s], n[q].v[b], 0, 0, 0);
+#pragma unroll
+    for (int b = 0; b < BO; ++b) put_slice(s_n, HID, q, 16 * (BO * w + b), n[q].v[b]);
   }
+  // FFN hidden: blocks hb = BH w + b of the 16 (half hb / 8, output block hb % 8 of that half)
+  bf16x8 f1[BH][4];
 #pragma unroll
-  for (int b = 0; b < 2; ++b) put_slice(s_n, HID, 16 * (2 * w + b), n.v[b]);
-  // FFN hidden: this wave's 64 features 64w.. (half hf = w / 2, output blocks 4 (w % 2) + b)
-  const int hf = w >> 1;
-  bf16x8 f1[4][4];
+  for (int b = 0; b < BH; ++b)
 #pragma unroll
-  for (int b = 0; b < 4; ++b)
+    for (int s = 0; s < 4; ++s) {
+      const int hb = BH * w + b;
+      f1[b][s] = frag(NL_F1 + MAT128 * (hb >> 3), hb & 7, s);
+    }
+  __syncthreads();  // n, all 128 features of every group
 #pragma unroll
-    for (int s = 0; s < 4; ++s) f1[b][s] = frag(NL_F1 + MAT128 * hf, 4 * (w & 1) + b, s);
-  Act<4> t;
+  for (int q = 0; q < NG; ++q) {
+    const Op<BF16T, 4> nop = lds_op(s_n, HID, q, 0);
+    Act<BH> tq;
 #pragma unroll
-  for (int b = 0; b < 4; ++b) t.v[b] = ld4(V + NLV_F1 + 64 * w + 16 * b + 4 * g);
-  __syncthreads();  // n, all 128 features
-  {
-    const Op<BF16T, 4> nop = lds_op(s_n, HID, 0);
+    for (int b = 0; b < BH; ++b) tq.v[b] = ld4(V + NLV_F1 + 16 * (BH * w + b) + 4 * g);
 #pragma unroll
-    for (int b = 0; b < 4; ++b)
+    for (int b = 0; b < BH; ++b)
 #pragma unroll
-      for (int s = 0; s < 4; ++s) t.v[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f1[b][s], nop.f[s], t.v[b], 0, 0, 0);
+      for (int s = 0; s < 4; ++s) tq.v[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f1[b][s], nop.f[s], tq.v[b], 0, 0, 0);
+    silu2_<BH, true>(tq);
+#pragma unroll
+    for (int b = 0; b < BH; ++b) put_slice(s_t, 2 * HID, q, 16 * (BH * w + b), tq.v[b]);
   }
-  silu2_<4, true>(t);
-#pragma unroll
-  for (int b = 0; b < 4; ++b) put_slice(s_t, 2 * HID, 64 * w + 16 * b, t.v[b]);
-  // FFN output (blocks 2w, 2w+1): both hidden halves in order, as k_node_layer
-  bf16x8 f2[2][2][4];
+  // FFN output (blocks BO w ..): both hidden halves in order, as k_node_layer
+  bf16x8 f2[2][BO][4];
 #pragma unroll
   for (int h = 0; h < 2; ++h)
 #pragma unroll
-    for (int b = 0; b < 2; ++b)
+    for (int b = 0; b < BO; ++b)
 #pragma unroll
-      for (int s = 0; s < 4; ++s) f2[h][b][s] = frag(NL_F2 + MAT128 * h, 2 * w + b, s);
-  __syncthreads();  // the hidden layer, all 256 features (and every wave is past its n operand)
-  Act<2> o;
-  zero(o);
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const Op<BF16T, 4> top = lds_op(s_t, 2 * HID, HID * h);
-#pragma unroll
-    for (int b = 0; b < 2; ++b)
-#pragma unroll
-      for (int s = 0; s < 4; ++s) o.v[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f2[h][b][s], top.f[s], o.v[b], 0, 0, 0);
-  }
+      for (int s = 0; s < 4; ++s) f2[h][b][s] = frag(NL_F2 + MAT128 * h, BO * w + b, s);
+  __syncthreads();  // the hidden layer, all 256 features (and every wave is past its n operands)
   // the first half of this wave's Q | K | V fragments, in flight across the h exchange below
-  bf16x8 fq[3][4];
+  constexpr int BQP = (BQ + 1) / 2;
+  bf16x8 fq[BQP][4];
   if constexpr (!FINAL) {
 #pragma unroll
-    for (int b = 0; b < 3; ++b)
+    for (int b = 0; b < BQP; ++b)
 #pragma unroll
-      for (int s = 0; s < 4; ++s) fq[b][s] = frag(NL_Q + MAT128 * ((6 * w + b) >> 3), (6 * w + b) & 7, s);
+      for (int s = 0; s < 4; ++s) fq[b][s] = frag(NL_Q + MAT128 * ((BQ * w + b) >> 3), (BQ * w + b) & 7, s);
   }
-  add_(n, o);
-  u16* hrow = reinterpret_cast<u16*>(a.h_out) + (int64_t)v * HID;
-  if (valid) {
 #pragma unroll
-    for (int b = 0; b < 2; ++b) st4(hrow + 16 * (2 * w + b) + 4 * g, n.v[b]);
-  }
-  if constexpr (FINAL) {
-    if (a.hT_out != nullptr && valid) {
-      u16* hT = reinterpret_cast<u16*>(a.hT_out);
+  for (int q = 0; q < NG; ++q) {
+    Act<BO> o;
+    zero(o);
 #pragma unroll
-      for (int b = 0; b < 2; ++b)
+    for (int h = 0; h < 2; ++h) {
+      const Op<BF16T, 4> top = lds_op(s_t, 2 * HID, q, HID * h);
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
-          hT[(int64_t)(16 * (2 * w + b) + 4 * g + q) * a.Nt + v] = (u16)(pack_bf16x2(n.v[b][q], 0.f) & 0xffffu);
+      for (int b = 0; b < BO; ++b)
+#pragma unroll
+        for (int s = 0; s < 4; ++s) o.v[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f2[h][b][s], top.f[s], o.v[b], 0, 0, 0);
     }
-  } else {
-    // next layer's Q | K | V from the new h: this wave's 6 output blocks 6w .. 6w+5 of the 24
+    add_(n[q], o);
+    if (valid[q]) {
+      u16* hrow = reinterpret_cast<u16*>(a.h_out) + (int64_t)vq[q] * HID;
 #pragma unroll
-    for (int b = 0; b < 2; ++b) put_slice(s_n, HID, 16 * (2 * w + b), n.v[b]);
+      for (int b = 0; b < BO; ++b) st4(hrow + 16 * (BO * w + b) + 4 * g, n[q].v[b]);
+    }
+    if constexpr (FINAL) {
+      if (a.hT_out != nullptr && valid[q]) {
+        u16* hT = reinterpret_cast<u16*>(a.hT_out);
+#pragma unroll
+        for (int b = 0; b < BO; ++b)
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            hT[(int64_t)(16 * (BO * w + b) + 4 * g + k) * a.Nt + vq[q]] = (u16)(pack_bf16x2(n[q].v[b][k], 0.f) & 0xffffu);
+      }
+    } else {
+#pragma unroll
+      for (int b = 0; b < BO; ++b) put_slice(s_n, HID, q, 16 * (BO * w + b), n[q].v[b]);
+    }
+  }
+  if constexpr (!FINAL) {
+    // next layer's Q | K | V from the new h: this wave's BQ output blocks of the 24 (Q 0-7, K 8-15, V 16-23)
     __syncthreads();  // the new h, all 128 features (s_n's previous readers finished before the last barrier)
-    const Op<BF16T, 4> hop = lds_op(s_n, HID, 0);
-    u16* qo = reinterpret_cast<u16*>(a.qkv_out) + (int64_t)v * 3 * HID;
 #pragma unroll
-    for (int b = 0; b < 6; ++b) {
-      const int ob = 6 * w + b;  // Q blocks 0-7, K 8-15, V 16-23
-      floatx4 x = ld4(V + NLV_Q + 16 * ob + 4 * g);
+    for (int q = 0; q < NG; ++q) {
+      const Op<BF16T, 4> hop = lds_op(s_n, HID, q, 0);
+      u16* qo = reinterpret_cast<u16*>(a.qkv_out) + (int64_t)vq[q] * 3 * HID;
 #pragma unroll
-      for (int s = 0; s < 4; ++s)
-        x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b < 3 ? fq[b][s] : frag(NL_Q + MAT128 * (ob >> 3), ob & 7, s),
-                                                    hop.f[s], x, 0, 0, 0);
-      if (valid) st4(qo + 16 * ob + 4 * g, x);
+      for (int b = 0; b < BQ; ++b) {
+        const int ob = BQ * w + b;
+        floatx4 x = ld4(V + NLV_Q + 16 * ob + 4 * g);
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b < BQP ? fq[b][s] : frag(NL_Q + MAT128 * (ob >> 3), ob & 7, s),
+                                                      hop.f[s], x, 0, 0, 0);
+        if (valid[q]) st4(qo + 16 * ob + 4 * g, x);
+      }
     }
   }
 }
@@ -2196,9 +2251,10 @@ extern "C" int di_node_layer(const di_graph* g, di_dtype dt, int final_layer, co
   if (dt == DI_BF16) {
     // 16 destinations per 256-thread block, output features split over its waves (k_node_fast)
     if (!g->src || !g->in_ptr) return DI_EINVAL;
-    const dim3 gf((unsigned)((a.Nt + NF_NODES - 1) / NF_NODES)), bf(256);
-    if (final_layer) hipLaunchKernelGGL((k_node_fast<true>), gf, bf, 0, s, a);
-    else hipLaunchKernelGGL((k_node_fast<false>), gf, bf, 0, s, a);
+    constexpr int NPB = NF_NODES * NF_GROUPS;
+    const dim3 gf((unsigned)((a.Nt + NPB - 1) / NPB)), bf(256 * NF_GROUPS);
+    if (final_layer) hipLaunchKernelGGL((k_node_fast<true, NF_GROUPS>), gf, bf, 0, s, a);
+    else hipLaunchKernelGGL((k_node_fast<false, NF_GROUPS>), gf, bf, 0, s, a);
   } else {
     if (final_layer) hipLaunchKernelGGL((k_node_layer<F32T, true>), grid, block, 0, s, a);
     else hipLaunchKernelGGL((k_node_layer<F32T, false>), grid, block, 0, s, a);

@@ -27,9 +27,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--jobs", type=int, default=12)
     ap.add_argument("--only", default=None, help="comma-separated background kinds")
+    ap.add_argument("--lib", default=None, help="a variant / diagnostic build of the library")
     args = ap.parse_args()
     dev = torch.device("cuda")
-    lib = _lib.load()
+    lib = _lib.load_variant(args.lib) if args.lib else _lib.load()
     M, L, H = 8, 1000, 128
     eng = GeoTEngine(seeded_state_dict(0, with_head=False), "bf16", device=dev)
     eng.split_node = False

@@ -1,9 +1,10 @@
 """Timing-diagnostic builds of the library from PATCHED COPIES of csrc/ (never -D knobs in the
 product sources): each diagnostic is a list of exact text substitutions applied to a copy of
 deepinteract_amd/csrc + include/, built into deepinteract_amd/lib/variants/diag_<name>/ and loaded
-with bench.py --lib. Every diagnostic computes WRONG results on purpose (timing only).
+with bench.py --lib. Every diagnostic computes WRONG results on purpose (timing only), except the
+A/B variants marked as such (one-line launch / pipeline changes measured against the product).
 
-usage: python tools/diag/patch_build.py nosilu nosync w0 ...
+usage: python tools/diag/patch_build.py nosilu nosync w0 initnopos initnostore initw0 ...
 """
 import os
 import shutil
@@ -30,6 +31,26 @@ DIAGS = {
     # hits L2 (same bytes, same instruction count; wrong weights)
     "w0": [("geot_kernels.hip", "    pipe.issue(W + EL_ORDER[si] * BLK, EL_SIZE[si], vo >= 0 ? V + vo : nullptr, 128);\n  }\n  __device__ const u16* next() {",
             "    pipe.issue(W, EL_SIZE[si], vo >= 0 ? V : nullptr, 128);\n  }\n  __device__ const u16* next() {", 1)],
+    # InitEdge (k_init_x32) without the positional-table gathers: acc starts at zero
+    "initnopos": [("geot_kernels.hip", "  init_acc_x32(acc, a, a.node_pos[a.src[e]], a.node_pos[a.dst[e]], h);\n  const bool with_fn",
+                   "  zero(acc);\n  const bool with_fn", 1)],
+    # InitEdge without its F row stores (kept alive by a never-true condition)
+    "initnostore": [("geot_kernels.hip", "  if (valid) store_row32(f, reinterpret_cast<u16*>(a.f_out) + (int64_t)e * HID, h);\n  if (!with_fn) return;",
+                     "  if (valid && f.v[0][0] == 1.2345e30f) store_row32(f, reinterpret_cast<u16*>(a.f_out) + (int64_t)e * HID, h);\n  if (!with_fn) return;", 1)],
+    # InitEdge's weight phases all DMA'd from the blob's first blocks (L2-resident; wrong weights)
+    "initw0": [("geot_kernels.hip", """    if (p == 0) pipe.issue(W + (IE_T0 + 40 * geo_t(0)) * BLK, 40);
+    else if (p < NT) pipe.issue(W + (IE_T0 + 40 * geo_t(p)) * BLK, 40);
+    else if (p == NT) pipe.issue(W + IE_GEO1 * BLK, 40);
+    else if (p == NT + 1) pipe.issue(W + IE_C1 * BLK, 16);""", """    if (p == 0) pipe.issue(W, 40);
+    else if (p < NT) pipe.issue(W, 40);
+    else if (p == NT) pipe.issue(W, 40);
+    else if (p == NT + 1) pipe.issue(W, 16);""", 1)],
+    # A/B variants with CORRECT results (timing comparisons of one-line changes, never shipped):
+    # k_node_fast with one 16-destination group per block
+    "ng1": [("geot_kernels.hip", "constexpr int NF_GROUPS = 2;", "constexpr int NF_GROUPS = 1;", 1)],
+    # the edge ring issuing each weight stage three stages ahead (two in the product)
+    "ahead3": [("geot_kernels.hip", "constexpr int RING_NW = 8, RING_SLOTS = 4, RING_AHEAD = 2;",
+                "constexpr int RING_NW = 8, RING_SLOTS = 4, RING_AHEAD = 3;", 1)],
 }
 
 
