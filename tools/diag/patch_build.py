@@ -46,11 +46,11 @@ DIAGS = {
     else if (p == NT) pipe.issue(W, 40);
     else if (p == NT + 1) pipe.issue(W, 16);""", 1)],
     # A/B variants with CORRECT results (timing comparisons of one-line changes, never shipped):
-    # k_node_fast with one 16-destination group per block
-    "ng1": [("geot_kernels.hip", "constexpr int NF_GROUPS = 2;", "constexpr int NF_GROUPS = 1;", 1)],
     # the edge ring issuing each weight stage three stages ahead (two in the product)
     "ahead3": [("geot_kernels.hip", "constexpr int RING_NW = 8, RING_SLOTS = 4, RING_AHEAD = 2;",
                 "constexpr int RING_NW = 8, RING_SLOTS = 4, RING_AHEAD = 3;", 1)],
+    # the beside store window: four stores in flight per pair wave (three in the product)
+    "inflight4": [("pair_tensor.hip", "constexpr int PAIR_INFLIGHT = 3;", "constexpr int PAIR_INFLIGHT = 4;", 1)],
 }
 
 
