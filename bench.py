@@ -39,7 +39,7 @@ H = 128
 
 
 # MACs the GeoT kernels actually issue on MFMA per edge (packed 16x32 weight blocks x 16 rows per
-# 16-edge tile / 16 = 512 MAC per block and edge; the same stage sequence in bf16 k_edge_lean and
+# 16-edge tile / 16 = 512 MAC per block and edge; the same stage sequence in the bf16 ring kernel and
 # fp32 k_edge_layer), by DI_GRAPH_GEO_REF: the reference-equivalent rates above count the
 # reference's work (incl. the neighbour-message branch that is exactly zero for reference-featurised
 # batches and the nbr_linear the reference applies to 4 gathered rows per edge); these count what runs
@@ -230,8 +230,8 @@ def allgather_record(ws, rank, complexes, n_res, k, dev, reps=3, per_rank=4):
     """Supplementary, outside the metric, two parts:
     1. the C4 driver end to end on REAL maps: distributed.predict_sharded over `per_rank` synthetic
        complexes per rank (device builder -> bf16 GeoT -> pair tensor -> bf16 head -> contact
-       probabilities), micro-batches of one complex, timed three ways (each `reps` times, interleaved,
-       fastest run kept): no collective (the compute alone), the maps gathered round by round with asynchronous all-gathers overlapped with the
+       probabilities), micro-batches of one complex, timed three ways (after one untimed run each,
+       five times interleaved, fastest run kept): no collective (the compute alone), the maps gathered round by round with asynchronous all-gathers overlapped with the
        next micro-batch (chunked, the default) and gathered once at the end; the collectives of the
        chunked plan are then timed alone, giving exposed = t(chunked) - t(compute) and hidden =
        t(collectives alone) - exposed. Every rank checks it holds every map, chunked == once;
@@ -259,7 +259,9 @@ def allgather_record(ws, rank, complexes, n_res, k, dev, reps=3, per_rank=4):
     # each mode `reps` times, interleaved, the fastest run of each (one run is ~0.3 s and includes the
     # host-side graph building, whose jitter is larger than the collectives)
     best = {}
-    for _ in range(reps):
+    for mode in ("none", "chunked", "once"):  # one untimed run each (the chunked plan's buffers, RCCL setup)
+        run(mode)
+    for _ in range(max(reps, 5)):
         for mode in ("none", "chunked", "once"):
             t_m, maps_m, plan = run(mode)
             if mode not in best or t_m < best[mode][0]:
