@@ -8,6 +8,7 @@ from __future__ import annotations
 
 import concurrent.futures as cf
 import glob
+import hashlib
 import json
 import os
 import subprocess
@@ -33,15 +34,24 @@ def _deps():
 
 
 def _stamp(defines=(), link_flags=()) -> str:
-    """What a build of the library depends on besides the sources' contents: compiler, flags, arch,
-    the -D defines of a variant and the link flags (written next to every built library)."""
-    return json.dumps({"hipcc": HIPCC, "cflags": CFLAGS, "arch": ARCH, "defines": list(defines),
-                       "link": list(link_flags)}, sort_keys=True)
+    """What a build of the library depends on (written next to every built library): compiler,
+    flags, arch, the -D defines of a variant, the link flags and a hash of every source / header /
+    this file's contents. Repo-relative, so a tree copied to another path (the GPU box's snapshot,
+    whose extraction need not keep mtimes) still matches the library built here."""
+    root = os.path.dirname(HERE)
+    h = hashlib.sha256()
+    for p in _deps():
+        h.update(os.path.relpath(p, root).encode())
+        with open(p, "rb") as fh:
+            h.update(fh.read())
+    cflags = [f.replace(root, "<repo>") for f in CFLAGS]
+    return json.dumps({"hipcc": HIPCC, "cflags": cflags, "arch": ARCH, "defines": list(defines),
+                       "link": list(link_flags), "sources": h.hexdigest()}, sort_keys=True)
 
 
 def _fresh(lib_path: str, defines=(), link_flags=()) -> bool:
-    """lib_path exists, is newer than every source / header / this file, and was built with the
-    same compiler, flags and defines (its .stamp file)."""
+    """lib_path exists and was built from the same sources with the same compiler, flags and
+    defines (its .stamp file)."""
     if not os.path.exists(lib_path):
         return False
     try:
@@ -50,8 +60,7 @@ def _fresh(lib_path: str, defines=(), link_flags=()) -> bool:
                 return False
     except OSError:
         return False
-    t = os.path.getmtime(lib_path)
-    return all(os.path.getmtime(p) <= t for p in _deps())
+    return True
 
 
 def up_to_date() -> bool:

@@ -190,3 +190,12 @@ def test_integration_stub_matches_header():
             d += {"(": 1, "[": 1, ")": -1, "]": -1}.get(ch, 0)
             n += ch == "," and d == 0
         assert n == decl[m.group(1)], (m.group(1), n, decl[m.group(1)])
+
+
+def test_build_stamp_is_path_independent():
+    """The in-tree library counts as built when the tree is copied elsewhere (the GPU box runs the
+    snapshot at another path, without building): the stamp holds no absolute repo path and the
+    library built here is current."""
+    root = os.path.dirname(build.HERE)
+    assert root not in build._stamp()
+    assert build.up_to_date()
