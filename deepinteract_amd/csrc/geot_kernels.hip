@@ -201,11 +201,12 @@ struct InitGeo : Geo<DT> {
 // (di_embed_init_edge): same stages and arithmetic as k_node_embed<BF16T> through InitEdge's single
 // 40-block LDS slot, so the two run side by side inside one launch instead of the embedding on a
 // side stream (whose blocks find no LDS beside InitEdge's until its tail).
-template <class DT>
-__device__ __forceinline__ void embed_block(const EmbedArgs& ea, WPipe<typename DT::T, InitGeo<DT>::NW, false, InitGeo<DT>::CAP>& pipe,
+// (NW: the launch's waves per block, 16 rows each)
+template <class DT, int NW = InitGeo<DT>::NW>
+__device__ __forceinline__ void embed_block(const EmbedArgs& ea, WPipe<typename DT::T, NW, false, InitGeo<DT>::CAP>& pipe,
                                             int blk, int lane, int g) {
   using T = typename DT::T;
-  const int r = blk * InitGeo<DT>::ROWS + (threadIdx.x >> 6) * ROWS_PER_WAVE + (lane & 15);
+  const int r = blk * ROWS_PER_WAVE * NW + (threadIdx.x >> 6) * ROWS_PER_WAVE + (lane & 15);
   const bool valid = r < ea.Nt;
   const int v = valid ? r : ea.Nt - 1;
   const T* W = reinterpret_cast<const T*>(ea.wmat);
@@ -364,8 +365,10 @@ constexpr int IR_T0 = 0, IR_DIST = 8, IR_AMIDE = 48, IR_GATE = 88, IR_C = 112;
 //   T0 (collapsed edge-message map, [128x32] 8 blk) -> geometric terms (dist, [dir, orient,] amide:
 //   [128x32] W_t0 + [128x128] combined_linear_0 slice, 40 blk each) -> gates (em1, dist1, [dir1,
 //   orient1,] amide1: [128x32] each) -> combined_linear_1/2 (8 + 8 blk) -> [layer-0 nbr_linear, 32 blk]
+constexpr int INIT_X32_NW = 4;  // waves per block (three waves per SIMD: 12 / NW blocks per CU)
 struct InitX32Geo {
-  static constexpr int NW = 4, THREADS = 64 * NW, ROWS_PER_WAVE = 32, ROWS = ROWS_PER_WAVE * NW;
+  static constexpr int NW = INIT_X32_NW, THREADS = 64 * NW, ROWS_PER_WAVE = 32, ROWS = ROWS_PER_WAVE * NW;
+  static constexpr int EMBED_ROWS = 16 * NW;  // node rows of one embedding block of the same launch
 };
 
 // one 32-row tile of InitEdge; wt(phase) returns the phase's weight blocks (LDS) and gate_off(t) the
@@ -478,12 +481,12 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, InitX32Geo::THREADS), a
 void k_init_x32(InitArgs a, EmbedArgs ea, int embed_blocks) {
   pq_signal_at_start(ea.sig_q, ea.sig_job);
   using G = InitGeo<BF16T>;
-  static_assert(G::NW == InitX32Geo::NW, "one LDS slot layout for both block kinds");
+  constexpr int NW = InitX32Geo::NW;
   __shared__ __attribute__((aligned(16))) u16 lds[G::CAP * BLK];
   const int lane = lane_id();
   if ((int)blockIdx.x < embed_blocks) {  // uniform per block
-    WPipe<u16, G::NW, false, G::CAP> epipe(lds);
-    embed_block<BF16T>(ea, epipe, blockIdx.x, lane, lane >> 4);
+    WPipe<u16, NW, false, G::CAP> epipe(lds);
+    embed_block<BF16T, NW>(ea, epipe, blockIdx.x, lane, lane >> 4);
     return;
   }
   const int h = lane >> 5;
@@ -492,7 +495,7 @@ void k_init_x32(InitArgs a, EmbedArgs ea, int embed_blocks) {
   const bool valid = r < a.Et;
   const int e = valid ? r : a.Et - 1;
   const u16* W = reinterpret_cast<const u16*>(a.wmat);
-  WPipe<u16, G::NW, false, G::CAP> pipe(lds);
+  WPipe<u16, NW, false, G::CAP> pipe(lds);
   pipe.issue(W + IE_T0 * BLK, 8);
   P32<2> gop;
   geo_op32<GC>(gop, a.edge_f, e, h);
@@ -2126,12 +2129,13 @@ extern "C" int di_init_edge(const di_graph* g, di_dtype dt, const float* edge_f,
 template <class DT>
 static void launch_embed_init(const InitArgs& a, const EmbedArgs& ea, hipStream_t s) {
   using G = InitGeo<DT>;
-  const int eb = (ea.Nt + G::ROWS - 1) / G::ROWS;
   if constexpr (DT::kBF16) {
+    const int eb = (ea.Nt + InitX32Geo::EMBED_ROWS - 1) / InitX32Geo::EMBED_ROWS;
     const int ib = (a.Et + InitX32Geo::ROWS - 1) / InitX32Geo::ROWS;
     hipLaunchKernelGGL((k_init_x32<true>), dim3((unsigned)(eb + ib)), dim3(InitX32Geo::THREADS), 0, s, a, ea, eb);
     return;
   }
+  const int eb = (ea.Nt + G::ROWS - 1) / G::ROWS;
   const int ib = (a.Et + G::ROWS - 1) / G::ROWS;
   hipLaunchKernelGGL((k_init_edge<DT, true>), dim3((unsigned)(eb + ib)), block_of<G>(), 0, s, a, ea, eb);
 }

@@ -4,7 +4,9 @@ each 5 times interleaved; for the chunked runs the host time inside ChunkedGathe
 and finish() and inside the forward calls, with and without a device synchronisation after every
 micro-batch.
 
-usage (GPU box): python tools/diag/gather_probe.py
+usage (GPU box): python tools/diag/gather_probe.py [--record]
+(--record: bench.py's allgather_record alone in a fresh process, to compare with the same record
+taken after the bench's timed steps)
 """
 import json
 import os
@@ -20,7 +22,18 @@ from deepinteract_amd.modules import LitGINI  # noqa: E402
 from deepinteract_amd.weights import seeded_state_dict  # noqa: E402
 
 
+def record():
+    """bench.py's own allgather_record, in a fresh process (no bench run before it)."""
+    import bench
+    ws, rank, local = bench.dist_setup(force=True)
+    dev = torch.device("cuda", local)
+    r = bench.allgather_record(ws, rank, 256, 1000, 20, dev)
+    print(json.dumps({"record_in_fresh_process": r["predict_sharded"]}))
+
+
 def main():
+    if "--record" in sys.argv:
+        return record()
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29533")
     dev = torch.device("cuda", 0)

@@ -49,6 +49,9 @@ DIAGS = {
     # the edge ring issuing each weight stage three stages ahead (two in the product)
     "ahead3": [("geot_kernels.hip", "constexpr int RING_NW = 8, RING_SLOTS = 4, RING_AHEAD = 2;",
                 "constexpr int RING_NW = 8, RING_SLOTS = 4, RING_AHEAD = 3;", 1)],
+    # InitEdge (k_init_x32) in 6-wave blocks, two per CU (four-wave blocks, three per CU, in the
+    # product): 192 instead of 128 edges per weight pass
+    "init6": [("geot_kernels.hip", "constexpr int INIT_X32_NW = 4;", "constexpr int INIT_X32_NW = 6;", 1)],
     # the beside store window: four stores in flight per pair wave (three in the product)
     "inflight4": [("pair_tensor.hip", "constexpr int PAIR_INFLIGHT = 3;", "constexpr int PAIR_INFLIGHT = 4;", 1)],
 }
