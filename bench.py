@@ -17,6 +17,7 @@ Prints ONE JSON line on rank 0.
 from __future__ import annotations
 
 import argparse
+import gc
 import json
 import math
 import os
@@ -634,11 +635,16 @@ def main():
 
     # ---- supplementary (outside the metric) ------------------------------------------------
     prologue = head_prologue_record(h1r, h2r, l1, l2, mbs[-1], eng, dev, tdt) if not args.no_prologue else None
-    gather = allgather_record(ws, rank, args.complexes, n_res, k, dev) if dist_on() and args.config == "c3" else None
-    nodes, edges = gb0.num_nodes, gb0.num_edges
+    nodes, edges, geo_ref0 = gb0.num_nodes, gb0.num_edges, gb0.geo_ref
     l1l2 = sum(2 * H * a * b * esz for a, b in zip(l1, l2))
-    kern = kernel_table(events, nodes, edges, l1l2, esz, args.dtype, gb0.geo_ref)
+    kern = kernel_table(events, nodes, edges, l1l2, esz, args.dtype, geo_ref0)
     kern = finish_kernel_table(kern, pair_bytes_per_launch(sch, info, kern, l1l2))
+    # the gather record runs on its own model and complexes: the timed schedule's buffers (pair
+    # sinks, resident micro-batches, engine workspaces) are released first
+    del sch, mbs, gb0, eng, events
+    gc.collect()
+    torch.cuda.empty_cache()
+    gather = allgather_record(ws, rank, args.complexes, n_res, k, dev) if dist_on() and args.config == "c3" else None
     # the committed PMC summary was collected on the default workload (C3, micro-batch 8, bf16, the
     # default schedule): any other shape reports traffic null rather than borrowing those bytes
     pmc_shape = (args.config, M, n_res, k, args.layers, args.dtype, args.overlap, args.geo_ref) == \
@@ -649,7 +655,7 @@ def main():
     bytes_c = algorithmic_bytes_per_complex(n_res, n_res, k, esz)
     hbm_frac = bytes_c * value / ws / (HBM_PEAK_GBS * 1e9)
     flops_c = algorithmic_flops_per_complex(n_res, n_res, k, args.layers)
-    xflops_c = executed_flops_per_complex(n_res, n_res, k, args.layers, gb0.geo_ref)
+    xflops_c = executed_flops_per_complex(n_res, n_res, k, args.layers, geo_ref0)
     mfma_frac = flops_c * value / ws / (MFMA_PEAK_TFLOPS[args.dtype] * 1e12)
     xmfma_frac = xflops_c * value / ws / (MFMA_PEAK_TFLOPS[args.dtype] * 1e12)
     if args.overlap:
@@ -713,9 +719,8 @@ def main():
     if not args.no_sub and args.config == "c3":
         # supplementary C3 lines outside the metric (same schedule and kernels): the reference's
         # precision (fp32, deepinteract_utils.py:1088) and the general path with the neighbour-edge
-        # gathers live (DI_GRAPH_GEO_REF cleared, deepinteract_modules.py:384-418)
-        del sch
-        torch.cuda.empty_cache()
+        # gathers live (DI_GRAPH_GEO_REF cleared, deepinteract_modules.py:384-418); the timed
+        # schedule's buffers were released above
         out["sub_records"] = [
             sub_record("fp32 C3 (the reference's precision), same schedule", "f32", True, 128, pool_gb, P, M,
                        n_res, k, args, dev, sd, cfg, s_geot, s_pair),

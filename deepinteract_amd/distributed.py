@@ -173,6 +173,9 @@ class ChunkedGather:
             for dst, m in zip(self.slots(c), maps):
                 if dst.data_ptr() != m.data_ptr():
                     dst.copy_(m)
+        self._issue(c)
+
+    def _issue(self, c):
         work = dist.all_gather_into_tensor(self.recv[c], self.send[c], group=self.group, async_op=True)
         self.pending.append((c, self.recv[c], self.send[c], work))
 
@@ -181,7 +184,7 @@ class ChunkedGather:
         done = {c for c, *_ in self.pending}
         for c in range(len(self.rounds)):
             if c not in done:
-                self.put(c)
+                self._issue(c)
         out = [None] * len(self.sizes)
         for c, recv, _send, work in sorted(self.pending, key=lambda t: t[0]):
             work.wait()

@@ -4,7 +4,7 @@ each 5 times interleaved; for the chunked runs the host time inside ChunkedGathe
 and finish() and inside the forward calls, with and without a device synchronisation after every
 micro-batch.
 
-usage (GPU box): python tools/diag/gather_probe.py [--record]
+usage (GPU box): python tools/diag/gather_probe.py [--record [--extra-streams N]]
 (--record: bench.py's allgather_record alone in a fresh process, to compare with the same record
 taken after the bench's timed steps)
 """
@@ -27,8 +27,15 @@ def record():
     import bench
     ws, rank, local = bench.dist_setup(force=True)
     dev = torch.device("cuda", local)
+    extra = int(sys.argv[sys.argv.index("--extra-streams") + 1]) if "--extra-streams" in sys.argv else 0
+    keep = [torch.cuda.Stream(dev) for _ in range(extra)]  # each one takes a hardware queue slot
+    for s in keep:
+        with torch.cuda.stream(s):
+            torch.zeros(1, device=dev).add_(1)
+    torch.cuda.synchronize()
     r = bench.allgather_record(ws, rank, 256, 1000, 20, dev)
-    print(json.dumps({"record_in_fresh_process": r["predict_sharded"]}))
+    print(json.dumps({"record_in_fresh_process": r["predict_sharded"], "extra_streams": extra,
+                      "GPU_MAX_HW_QUEUES": os.environ.get("GPU_MAX_HW_QUEUES")}))
 
 
 def main():
