@@ -4,7 +4,7 @@ each 5 times interleaved; for the chunked runs the host time inside ChunkedGathe
 and finish() and inside the forward calls, with and without a device synchronisation after every
 micro-batch.
 
-usage (GPU box): python tools/diag/gather_probe.py [--record [--extra-streams N]]
+usage (GPU box): python tools/diag/gather_probe.py [--record [--extra-streams N] [--compute-stream] [--lib variant.so]]
 (--record: bench.py's allgather_record alone in a fresh process, to compare with the same record
 taken after the bench's timed steps)
 """
@@ -24,6 +24,9 @@ from deepinteract_amd.weights import seeded_state_dict  # noqa: E402
 
 def record():
     """bench.py's own allgather_record, in a fresh process (no bench run before it)."""
+    if "--lib" in sys.argv:  # an A/B build (tools/diag/patch_build.py)
+        from deepinteract_amd import _lib
+        _lib.load_variant(sys.argv[sys.argv.index("--lib") + 1])
     import bench
     ws, rank, local = bench.dist_setup(force=True)
     dev = torch.device("cuda", local)
@@ -33,8 +36,13 @@ def record():
         with torch.cuda.stream(s):
             torch.zeros(1, device=dev).add_(1)
     torch.cuda.synchronize()
-    r = bench.allgather_record(ws, rank, 256, 1000, 20, dev)
+    if "--compute-stream" in sys.argv:  # the whole record on a pool stream instead of the null stream
+        with torch.cuda.stream(torch.cuda.Stream(dev)):
+            r = bench.allgather_record(ws, rank, 256, 1000, 20, dev)
+    else:
+        r = bench.allgather_record(ws, rank, 256, 1000, 20, dev)
     print(json.dumps({"record_in_fresh_process": r["predict_sharded"], "extra_streams": extra,
+                      "compute_stream": "--compute-stream" in sys.argv,
                       "GPU_MAX_HW_QUEUES": os.environ.get("GPU_MAX_HW_QUEUES")}))
 
 

@@ -52,6 +52,10 @@ DIAGS = {
     # InitEdge (k_init_x32) in 6-wave blocks, two per CU (four-wave blocks, three per CU, in the
     # product): 192 instead of 128 edges per weight pass
     "init6": [("geot_kernels.hip", "constexpr int INIT_X32_NW = 4;", "constexpr int INIT_X32_NW = 6;", 1)],
+    # the persistent edge ring on 8 CUs fewer than the device has: room for a collective's blocks
+    # beside it (the chunked gather's exposure)
+    "ring248": [("geot_kernels.hip", "const dim3 grid((unsigned)(ntiles < cus ? ntiles : cus)), block(EdgeRingGeo::THREADS);",
+                 "const dim3 grid((unsigned)(ntiles < cus - 8 ? ntiles : cus - 8)), block(EdgeRingGeo::THREADS);", 1)],
     # the beside store window: four stores in flight per pair wave (three in the product)
     "inflight4": [("pair_tensor.hip", "constexpr int PAIR_INFLIGHT = 3;", "constexpr int PAIR_INFLIGHT = 4;", 1)],
 }
