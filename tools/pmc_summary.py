@@ -64,7 +64,14 @@ def main(tag, src=os.path.join(ROOT, "gpurun_out"), prefix="prof", traffic_json=
             if name:
                 traffic[name] = {"hbm_bytes_per_launch": hbm, "fetch_kib": f, "write_kib": wr, "source": f"{tag}_pmc.csv"}
     if traffic_json:
-        with open(os.path.join(prof, "pmc_traffic.json"), "w") as fh:
+        # the pair stream's standalone ratio (tools/pmc_pair_ratio.py) is kept over this run's
+        # figure for it: rocprofv3 --pmc serialises the overlapped schedule's dispatches
+        path = os.path.join(prof, "pmc_traffic.json")
+        if os.path.exists(path):
+            for k, v in json.load(open(path)).items():
+                if "hbm_bytes_per_alg_byte" in v:
+                    traffic[k] = v
+        with open(path, "w") as fh:
             json.dump(traffic, fh, indent=1)
     print(json.dumps(traffic, indent=1))
 
