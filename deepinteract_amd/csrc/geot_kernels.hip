@@ -1899,6 +1899,10 @@ void k_node_fast(NodeArgs a) {
 #pragma unroll
       for (int s = 0; s < 4; ++s) fq[b][s] = frag(NL_Q + MAT128 * ((BQ * w + b) >> 3), (BQ * w + b) & 7, s);
   }
+  // the second half, issued as soon as the last group's FFN-output MFMAs no longer need f2's
+  // registers: in flight across the h stores and the exchange barrier (global loads are not
+  // moved across s_barrier by the compiler)
+  bf16x8 fq2[BQ - BQP][4];
 #pragma unroll
   for (int q = 0; q < NG; ++q) {
     Act<BO> o;
@@ -1910,6 +1914,15 @@ void k_node_fast(NodeArgs a) {
       for (int b = 0; b < BO; ++b)
 #pragma unroll
         for (int s = 0; s < 4; ++s) o.v[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f2[h][b][s], top.f[s], o.v[b], 0, 0, 0);
+    }
+    if constexpr (!FINAL) {
+      if (q == NG - 1) {
+#pragma unroll
+        for (int b = BQP; b < BQ; ++b)
+#pragma unroll
+          for (int s = 0; s < 4; ++s)
+            fq2[b - BQP][s] = frag(NL_Q + MAT128 * ((BQ * w + b) >> 3), (BQ * w + b) & 7, s);
+      }
     }
     add_(n[q], o);
     if (valid[q]) {
@@ -1944,8 +1957,7 @@ void k_node_fast(NodeArgs a) {
         floatx4 x = ld4(V + NLV_Q + 16 * ob + 4 * g);
 #pragma unroll
         for (int s = 0; s < 4; ++s)
-          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b < BQP ? fq[b][s] : frag(NL_Q + MAT128 * (ob >> 3), ob & 7, s),
-                                                      hop.f[s], x, 0, 0, 0);
+          x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b < BQP ? fq[b][s] : fq2[b - BQP][s], hop.f[s], x, 0, 0, 0);
         if (valid[q]) st4(qo + 16 * ob + 4 * g, x);
       }
     }

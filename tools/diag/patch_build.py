@@ -56,6 +56,20 @@ DIAGS = {
     # beside it (the chunked gather's exposure)
     "ring248": [("geot_kernels.hip", "const dim3 grid((unsigned)(ntiles < cus ? ntiles : cus)), block(EdgeRingGeo::THREADS);",
                  "const dim3 grid((unsigned)(ntiles < cus - 8 ? ntiles : cus - 8)), block(EdgeRingGeo::THREADS);", 1)],
+    # k_node_fast's second half of Q|K|V fragments loaded inside the Q|K|V loop (after the last
+    # barrier) instead of right after the FFN-output MFMAs
+    "qkvjit": [("geot_kernels.hip", """    if constexpr (!FINAL) {
+      if (q == NG - 1) {
+#pragma unroll
+        for (int b = BQP; b < BQ; ++b)
+#pragma unroll
+          for (int s = 0; s < 4; ++s)
+            fq2[b - BQP][s] = frag(NL_Q + MAT128 * ((BQ * w + b) >> 3), (BQ * w + b) & 7, s);
+      }
+    }
+    add_(n[q], o);""", """    add_(n[q], o);""", 1),
+               ("geot_kernels.hip", "b < BQP ? fq[b][s] : fq2[b - BQP][s], hop.f[s], x, 0, 0, 0);",
+                "b < BQP ? fq[b][s] : frag(NL_Q + MAT128 * (ob >> 3), ob & 7, s), hop.f[s], x, 0, 0, 0);", 1)],
     # the beside store window: four stores in flight per pair wave (three in the product)
     "inflight4": [("pair_tensor.hip", "constexpr int PAIR_INFLIGHT = 3;", "constexpr int PAIR_INFLIGHT = 4;", 1)],
 }
