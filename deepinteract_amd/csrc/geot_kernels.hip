@@ -88,6 +88,15 @@ struct NodeArgs {
 };
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+// A bijection of [0, n) that turns slot j, run on XCD j mod 8 (blocks are dealt round-robin over
+// the 8 XCDs: b and b + 8 share one -- speed only, correct under any placement), into
+// base(j mod 8) + j / 8: the slots of one XCD cover one contiguous range, so neighbouring rows
+// (a destination range's gathered K / Q / V rows) stay in that XCD's L2.
+// (n = 8q + r: XCD y holds q + [y < r] slots, so base(x) = x q + min(x, r))
+__device__ __forceinline__ int xcd_slot(int j, int n) {
+  const int x = j & 7;
+  return x * (n >> 3) + min(x, n & 7) + (j >> 3);
+}
 template <int NW>
 __device__ __forceinline__ int row_id() {
   return blockIdx.x * (NW * ROWS_PER_WAVE) + (threadIdx.x >> 6) * ROWS_PER_WAVE + (threadIdx.x & 15);
@@ -1399,7 +1408,10 @@ void k_edge_x32_ring(EdgeArgs a, int ntiles) {
   st.fill();
 #pragma unroll 1
   for (int i = 0; i < my_tiles; ++i) {
-    const int tile = (int)blockIdx.x + i * (int)gridDim.x;
+    // slot j = b + i G: with G a multiple of 8, slot j runs on block b's XCD (j mod 8), and
+    // xcd_slot gives each XCD one contiguous eighth of the edges (every block keeps its tile count)
+    const int j = (int)blockIdx.x + i * (int)gridDim.x;
+    const int tile = (gridDim.x & 7) == 0 ? xcd_slot(j, ntiles) : j;
     const int r = tile * EdgeRingGeo::ROWS + wave * EdgeRingGeo::ROWS_PER_WAVE + (lane & 31);
     const bool valid = r < a.Et;
     const int e = valid ? r : a.Et - 1;
