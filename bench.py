@@ -129,12 +129,21 @@ def dist_setup(force=False):
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # DI_BENCH_REHEARSE=1: every rank on cuda:0 over gloo -- the multi-rank path (barriers, max over
+    # ranks, rank-0 line, the gather record) rehearsed on a one-GPU box; RCCL refuses two ranks on
+    # one device. Never set for a measurement.
+    rehearse = os.environ.get("DI_BENCH_REHEARSE") == "1"
+    if rehearse:
+        local = 0
     torch.cuda.set_device(local)
     if ws > 1 or force:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29531")
-        dist.init_process_group("nccl", rank=rank, world_size=ws, device_id=torch.device("cuda", local))
+        if rehearse:
+            dist.init_process_group("gloo", rank=rank, world_size=ws)
+        else:
+            dist.init_process_group("nccl", rank=rank, world_size=ws, device_id=torch.device("cuda", local))
     return ws, rank, local
 
 
