@@ -70,9 +70,6 @@ DIAGS = {
     add_(n[q], o);""", """    add_(n[q], o);""", 1),
                ("geot_kernels.hip", "b < BQP ? fq[b][s] : fq2[b - BQP][s], hop.f[s], x, 0, 0, 0);",
                 "b < BQP ? fq[b][s] : frag(NL_Q + MAT128 * (ob >> 3), ob & 7, s), hop.f[s], x, 0, 0, 0);", 1)],
-    # the XCD-contiguous tile order for the final edge layer only (the first keeps tile = j)
-    "xcdfinal": [("geot_kernels.hip", "    const int tile = (gridDim.x & 7) == 0 ? xcd_slot(j, ntiles) : j;",
-                  "    const int tile = FINAL && (gridDim.x & 7) == 0 ? xcd_slot(j, ntiles) : j;", 1)],
     # the beside store window: four stores in flight per pair wave (three in the product)
     "inflight4": [("pair_tensor.hip", "constexpr int PAIR_INFLIGHT = 3;", "constexpr int PAIR_INFLIGHT = 4;", 1)],
 }
