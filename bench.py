@@ -382,7 +382,8 @@ def timed(sch, steps, warmup, ws=1, kernel_events="dominant"):
         sch.check()
         queue = {"stream_bytes": c1["stream_bytes"] - c0["stream_bytes"], "help_bytes": c1["help_bytes"] - c0["help_bytes"],
                  "gave_up": c1["gave_up"] - c0["gave_up"]}
-    return elapsed, events, {"host_issue_s": host_issue_s, "host_issue_idle_s": host_issue_idle_s, "queue": queue}
+    return elapsed, events, {"host_issue_s": host_issue_s, "host_issue_idle_s": host_issue_idle_s, "queue": queue,
+                             "mode": getattr(sch, "mode", "serial")}
 
 
 def kernel_table(events, nodes, edges, l1l2, esz, dtype, geo_ref):
@@ -436,10 +437,11 @@ def make_schedule(args, eng, mbs, h1r, h2r, l1, l2, tdt, dev, s_geot, s_pair):
     if args.overlap:
         from deepinteract_amd.pipeline import OverlappedSchedule
         sinks = [torch.empty(numel, dtype=tdt, device=dev) for _ in range(2)]
+        # two rotating sinks: the bench never reads the pair tensors back (the parity tests do)
         sch = OverlappedSchedule(eng, mbs, h1r, h2r, l1, l2, sinks, s_geot, s_pair, ring=args.ring,
                                  help_every=args.help_every, stream_blocks=args.pair_blocks,
                                  stream_waves=args.pair_waves, patience_ms=args.patience_ms,
-                                 jobs_per_launch=args.jobs_per_launch)
+                                 jobs_per_launch=args.jobs_per_launch, discard_outputs=True)
         return sch
     from deepinteract_amd.engine import PairTensorOp
     pair = PairTensorOp(dev, kernel=args.pair_kernel, blocks=args.pair_blocks, waves_per_block=args.pair_waves)
@@ -635,8 +637,13 @@ def main():
     tdt = torch.bfloat16 if args.dtype == "bf16" else torch.float32
     esz = 2 if args.dtype == "bf16" else 4
 
-    s_geot = torch.cuda.current_stream(dev)
-    s_pair = torch.cuda.Stream(dev) if args.overlap else s_geot
+    if args.overlap:
+        # two streams on hardware queues of their own (deepinteract_amd.pipeline, "Hardware queues"):
+        # ordinary streams can share one in a process that holds an RCCL communicator
+        from deepinteract_amd.pipeline import schedule_streams
+        s_geot, s_pair = schedule_streams(dev)
+    else:
+        s_geot = s_pair = torch.cuda.current_stream(dev)
     sch = make_schedule(args, eng, mbs, h1r, h2r, l1, l2, tdt, dev, s_geot, s_pair)
     elapsed, events, info = timed(sch, args.steps, args.warmup, ws, args.kernel_events)
     total = args.complexes * args.steps * ws
@@ -667,19 +674,22 @@ def main():
     xflops_c = executed_flops_per_complex(n_res, n_res, k, args.layers, geo_ref0)
     mfma_frac = flops_c * value / ws / (MFMA_PEAK_TFLOPS[args.dtype] * 1e12)
     xmfma_frac = xflops_c * value / ws / (MFMA_PEAK_TFLOPS[args.dtype] * 1e12)
-    if args.overlap:
+    if args.overlap and info["mode"] == "ordered":
+        streams = ("ORDERED (the two streams did not run concurrently, di_streams_concurrent): GeoT, then each "
+                   "micro-batch's pair tensors by a full-chip help launch on the same stream")
+    elif args.overlap:
         streams = (f"GeoT || pair tensor: GeoT on one HIP stream (each micro-batch signalled by the next GeoT launch), the "
                    f"pair tensors on ONE persistent di_pair_stream launch per step on a second stream "
                    f"({args.pair_blocks or 'CUs/2'} blocks x {args.pair_waves or 4} waves, bounded nt stores, "
                    f"device-queue tickets), di_pair_help on the GeoT stream every {args.help_every} micro-batches "
                    f"(hT ring of {args.ring}) and a drain at the end of the timed steps; no host events between "
-                   f"the streams")
+                   f"the streams; both streams on hardware queues of their own (CU-masked)")
     else:
         streams = f"1 stream: GeoT then the pair tensor ({args.pair_kernel} kernel) per micro-batch"
     queue = info["queue"]
     if queue is not None:
         tot = queue["stream_bytes"] + queue["help_bytes"]
-        queue = dict(queue, help_fraction=round(queue["help_bytes"] / tot, 4) if tot else None,
+        queue = dict(queue, mode=info["mode"], help_fraction=round(queue["help_bytes"] / tot, 4) if tot else None,
                      pair_rate_GBs=round(tot / elapsed / 1e9, 1), help_launches_per_step=args.complexes // M // args.help_every)
 
     out = {

@@ -39,7 +39,7 @@ class DiPairLaunch(ctypes.Structure):
 
 
 DI_PAIR_AUTO, DI_PAIR_ROWS, DI_PAIR_VECTOR, DI_PAIR_LINES = 0, 1, 2, 3
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 
 class DiPairJob(ctypes.Structure):
@@ -79,6 +79,9 @@ _SIGS = {
     "di_pair_signal": ([_P, _I, _P], ctypes.c_int),
     "di_pair_stream": ([_I, _P, _I, _I, _I, _P, ctypes.POINTER(DiPairLaunch), ctypes.c_float, _P], ctypes.c_int),
     "di_pair_help": ([_I, _P, _I, _I, _I, _P, ctypes.POINTER(DiPairLaunch), _I, _P], ctypes.c_int),
+    "di_stream_create_dedicated": ([ctypes.POINTER(ctypes.c_void_p)], ctypes.c_int),
+    "di_stream_destroy": ([_P], ctypes.c_int),
+    "di_streams_concurrent": ([_P, _P, _P, ctypes.c_float, ctypes.POINTER(ctypes.c_int32)], ctypes.c_int),
     "di_head_prologue": ([_I, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, ctypes.c_float, _P, _P, _P],
                          ctypes.c_int),
     "di_head_prologue_work_bytes": ([_I, _I, _I, _I], ctypes.c_int64),

@@ -1725,6 +1725,55 @@ __global__ __launch_bounds__(NodeRingGeo::THREADS, 1) void k_node_update_ring(No
   }
 }
 
+// The CSR segment sum of ONE destination by its 16-lane group (lane j: features 8j .. 8j + 7, head
+// j / 4): acc = sum_e alpha[e, head] * V[src e], z = sum_e alpha[e, head] over e in [e0, e1), edge by
+// edge in order -- k_node_aggr's products and order, so the row is bit-identical to it for any chunk
+// size U. Every load of a chunk is issued unconditionally (a slot past e1 re-reads edge c's alpha and
+// a valid V row and adds it with weight 0, which is exact), so a chunk is one batch of buffer loads
+// (32-bit offsets from SGPR descriptors) and one wait, with no per-edge branch. On entry lane j of the
+// group holds id_first = src[e0 + j] (j < U; 0 past e1). U = 10: k = 20 in-edges are two chunks.
+constexpr int SEG_U = 10;
+// LDS row strides of the node kernels' exchange buffers, padded so that a row is 4 banks (mod 64)
+// after the previous one: the 16 rows r a quarter-wave reads at one feature offset (ds_read_b128 of
+// the fp32 rows, ds_read_b64 of the bf16 operands) fall on 16 distinct bank quads instead of one
+// (unpadded, every row starts on bank 0: 16-way conflicts on every exchange read and write)
+constexpr int LDS_ATTN = HID + 4;       // fp32 aggregated rows: 132 words
+constexpr int LDS_N = HID + 8;          // bf16 n / h rows: 68 words
+constexpr int LDS_T = 2 * HID + 8;      // bf16 FFN-hidden rows: 132 words
+template <int U>
+__device__ __forceinline__ void seg_sum16(__amdgpu_buffer_rsrc_t vr, __amdgpu_buffer_rsrc_t ar, const int* __restrict__ src,
+                                          int e0, int e1, int j, int lane_base, int id_first, float (&acc)[8], float& z) {
+  static_assert(U >= 1 && U <= 16, "a chunk's ids come from the group's 16 lanes");
+  const int head = j >> 2;
+  int id_next = id_first;
+#pragma unroll 1
+  for (int c = e0; c < e1; c += U) {
+    const int n = min(U, e1 - c);
+    const int id_cur = id_next;
+    float al[U];
+    uint4 vv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int id = __shfl(id_cur, lane_base + u, 64);
+      const int eu = u < n ? c + u : c;
+      al[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ar, (eu * 4 + head) * 4, 0, 0));
+      vv[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(vr, id * (3 * HID * 2) + 16 * j, 0, 0));
+    }
+    if (c + U < e1) id_next = c + U + j < e1 && j < U ? src[c + U + j] : 0;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const float w = u < n ? al[u] : 0.f;
+      const uint32_t x[4] = {vv[u].x, vv[u].y, vv[u].z, vv[u].w};
+#pragma unroll
+      for (int f = 0; f < 8; ++f) {
+        const uint32_t b = f & 1 ? (x[f >> 1] & 0xffff0000u) : (x[f >> 1] << 16);
+        acc[f] += w * __builtin_bit_cast(float, b);
+      }
+      z += w;
+    }
+  }
+}
+
 // ================================================================ node layer at full occupancy (bf16)
 // The bf16 di_node_layer (the overlapped schedule's node layer, round 5). k_node_layer runs 16
 // destinations per wave and one 4-wave block per CU (a C3 micro-batch's 16 k nodes are 250 blocks):
@@ -1754,13 +1803,13 @@ __global__ __attribute__((amdgpu_flat_work_group_size(1, 256 * NG), amdgpu_waves
 void k_node_fast(NodeArgs a) {
   constexpr int NWV = 4 * NG, BO = 8 / NWV, BH = 16 / NWV, BQ = 24 / NWV;
   static_assert(8 % NWV == 0 && BQ >= 1, "node groups per block: 1 or 2");
-  __shared__ __attribute__((aligned(16))) float s_attn[NG * NF_NODES * HID];  // aggregated rows (fp32)
-  __shared__ __attribute__((aligned(16))) u16 s_n[NG * NF_NODES * HID];       // n as a bf16 operand
-  __shared__ __attribute__((aligned(16))) u16 s_t[NG * NF_NODES * 2 * HID];   // FFN hidden (bf16)
+  __shared__ __attribute__((aligned(16))) float s_attn[NG * NF_NODES * LDS_ATTN];  // aggregated rows (fp32)
+  __shared__ __attribute__((aligned(16))) u16 s_n[NG * NF_NODES * LDS_N];       // n as a bf16 operand
+  __shared__ __attribute__((aligned(16))) u16 s_t[NG * NF_NODES * LDS_T];   // FFN hidden (bf16)
   const int vb = (int)blockIdx.x * NG * NF_NODES;  // the block's first destination
   // ---- 1. wV / (z + 1e-6), 16 lanes per destination (k_node_aggr<BF16T>'s loop)
   {
-    constexpr int U = AggrCfg<BF16T>::U, FPL = 8;
+    constexpr int FPL = 8;
     const int j = threadIdx.x & 15, nl = threadIdx.x >> 4;  // nl: the block's destination 0 .. 16 NG - 1
     const int v = vb + nl;
     float acc[FPL];
@@ -1768,40 +1817,12 @@ void k_node_fast(NodeArgs a) {
     for (int f = 0; f < FPL; ++f) acc[f] = 0.f;
     float z = 0.f;
     if (v < a.Nt) {  // uniform per 16-lane group (the shuffles stay inside the group)
-      const int head = (FPL * j) >> 5;
-      const u16* vbase = reinterpret_cast<const u16*>(a.qkv) + 2 * HID + FPL * j;
       const int e0 = a.in_ptr[v], e1 = a.in_ptr[v + 1];
-      const int lane_base = threadIdx.x & 48;
-      int id_next = e0 + j < e1 ? a.src[e0 + j] : 0;
-#pragma unroll 1
-      for (int c = e0; c < e1; c += U) {
-        const int n = min(U, e1 - c);
-        const int id_cur = id_next;
-        int ids[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) ids[u] = __shfl(id_cur, lane_base + (u & 15), 64);
-        float al[U];
-        u16 vv[U][FPL];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          if (u < n) {
-            al[u] = a.alpha[(int64_t)(c + u) * 4 + head];
-            *reinterpret_cast<uint4*>(vv[u]) = *reinterpret_cast<const uint4*>(vbase + (int64_t)ids[u] * 3 * HID);
-          }
-        }
-        if (c + U < e1) id_next = c + U + j < e1 && j < U ? a.src[c + U + j] : 0;
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          if (u < n) {
-#pragma unroll
-            for (int f = 0; f < FPL; ++f) acc[f] += al[u] * __builtin_bit_cast(float, (uint32_t)vv[u][f] << 16);
-            z += al[u];
-          }
-        }
-      }
+      seg_sum16<SEG_U>(buf_rsrc(reinterpret_cast<const u16*>(a.qkv) + 2 * HID), buf_rsrc(a.alpha), a.src, e0, e1, j,
+                       threadIdx.x & 48, e0 + j < e1 ? a.src[e0 + j] : 0, acc, z);
     }
     const float d = z + 1e-6f;
-    float* out = s_attn + nl * HID + FPL * j;
+    float* out = s_attn + nl * LDS_ATTN + FPL * j;
     st4(out, (floatx4){acc[0] / d, acc[1] / d, acc[2] / d, acc[3] / d});
     st4(out + 4, (floatx4){acc[4] / d, acc[5] / d, acc[6] / d, acc[7] / d});
   }
@@ -1859,7 +1880,7 @@ void k_node_fast(NodeArgs a) {
     Act<8> wv;
 #pragma unroll
     for (int b = 0; b < 8; ++b)
-      wv.v[b] = *reinterpret_cast<const floatx4*>(s_attn + (q * NF_NODES + r) * HID + 16 * b + 4 * g);
+      wv.v[b] = *reinterpret_cast<const floatx4*>(s_attn + (q * NF_NODES + r) * LDS_ATTN + 16 * b + 4 * g);
     Op<BF16T, 4> op;
     make_op(op, wv);
 #pragma unroll
@@ -1867,7 +1888,7 @@ void k_node_fast(NodeArgs a) {
 #pragma unroll
       for (int s = 0; s < 4; ++s) n[q].v[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fo[b][s], op.f[s], n[q].v[b], 0, 0, 0);
 #pragma unroll
-    for (int b = 0; b < BO; ++b) put_slice(s_n, HID, q, 16 * (BO * w + b), n[q].v[b]);
+    for (int b = 0; b < BO; ++b) put_slice(s_n, LDS_N, q, 16 * (BO * w + b), n[q].v[b]);
   }
   // FFN hidden: blocks hb = BH w + b of the 16 (half hb / 8, output block hb % 8 of that half)
   bf16x8 f1[BH][4];
@@ -1881,7 +1902,7 @@ void k_node_fast(NodeArgs a) {
   __syncthreads();  // n, all 128 features of every group
 #pragma unroll
   for (int q = 0; q < NG; ++q) {
-    const Op<BF16T, 4> nop = lds_op(s_n, HID, q, 0);
+    const Op<BF16T, 4> nop = lds_op(s_n, LDS_N, q, 0);
     Act<BH> tq;
 #pragma unroll
     for (int b = 0; b < BH; ++b) tq.v[b] = ld4(V + NLV_F1 + 16 * (BH * w + b) + 4 * g);
@@ -1891,7 +1912,7 @@ void k_node_fast(NodeArgs a) {
       for (int s = 0; s < 4; ++s) tq.v[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f1[b][s], nop.f[s], tq.v[b], 0, 0, 0);
     silu2_<BH, true>(tq);
 #pragma unroll
-    for (int b = 0; b < BH; ++b) put_slice(s_t, 2 * HID, q, 16 * (BH * w + b), tq.v[b]);
+    for (int b = 0; b < BH; ++b) put_slice(s_t, LDS_T, q, 16 * (BH * w + b), tq.v[b]);
   }
   // FFN output (blocks BO w ..): both hidden halves in order, as k_node_layer
   bf16x8 f2[2][BO][4];
@@ -1921,7 +1942,7 @@ void k_node_fast(NodeArgs a) {
     zero(o);
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      const Op<BF16T, 4> top = lds_op(s_t, 2 * HID, q, HID * h);
+      const Op<BF16T, 4> top = lds_op(s_t, LDS_T, q, HID * h);
 #pragma unroll
       for (int b = 0; b < BO; ++b)
 #pragma unroll
@@ -1953,7 +1974,7 @@ void k_node_fast(NodeArgs a) {
       }
     } else {
 #pragma unroll
-      for (int b = 0; b < BO; ++b) put_slice(s_n, HID, q, 16 * (BO * w + b), n[q].v[b]);
+      for (int b = 0; b < BO; ++b) put_slice(s_n, LDS_N, q, 16 * (BO * w + b), n[q].v[b]);
     }
   }
   if constexpr (!FINAL) {
@@ -1961,7 +1982,7 @@ void k_node_fast(NodeArgs a) {
     __syncthreads();  // the new h, all 128 features (s_n's previous readers finished before the last barrier)
 #pragma unroll
     for (int q = 0; q < NG; ++q) {
-      const Op<BF16T, 4> hop = lds_op(s_n, HID, q, 0);
+      const Op<BF16T, 4> hop = lds_op(s_n, LDS_N, q, 0);
       u16* qo = reinterpret_cast<u16*>(a.qkv_out) + (int64_t)vq[q] * 3 * HID;
 #pragma unroll
       for (int b = 0; b < BQ; ++b) {
@@ -1971,6 +1992,208 @@ void k_node_fast(NodeArgs a) {
         for (int s = 0; s < 4; ++s)
           x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b < BQP ? fq[b][s] : fq2[b - BQP][s], hop.f[s], x, 0, 0, 0);
         if (valid[q]) st4(qo + 16 * ob + 4 * g, x);
+      }
+    }
+  }
+}
+
+// ================================================================ node layer, weights stationary (bf16)
+// The bf16 di_node_layer since round 6. k_node_fast streams the whole layer's weights (256 KiB) from
+// L2 into every 16-destination block: 1000 blocks, 256 MB of L2 -> CU fragment traffic per C3
+// micro-batch, each wave's chain waiting on its fragment loads, beside a pair stream that pushes
+// ~4 TB/s of stores through the same L2s. Here the weights are loaded ONCE per CU and stay:
+//   * one persistent 8-wave block per CU (two waves per SIMD) walks tiles of 32 destinations
+//     (XCD-contiguous tile order, as the edge ring);
+//   * wave w keeps its slice of O (output block w), the FFN hidden layer (blocks 2w, 2w+1 of 16) and
+//     the FFN output (block w, both K halves) in registers for the whole launch (80 VGPRs), and the
+//     next layer's Q|K|V (96 KiB) sits in LDS, DMA'd once at entry (wave w: blocks 3w..3w+2 of 24);
+//   * per tile: (1) the CSR segment sum, 16 lanes per destination, exactly k_node_fast's loop (same
+//     products, same order: bit-identical rows) into LDS -- 32 destinations x 16 lanes = the block;
+//     (2) O_node + residual, FFN, Q|K|V as two 16-destination MFMA column groups, every register
+//     fragment feeding both groups, activations exchanged through LDS as bf16 operands.
+// Per output element the arithmetic is k_node_fast's (the same bias + residual initial value, the
+// same k-steps in the same order, the same bf16 operands): h / Q,K,V / hT are bit-identical.
+constexpr int NWS_NW = 8;        // waves per block
+constexpr int NWS_TILE = 32;     // destinations per tile (2 MFMA column groups of 16)
+static_assert(NWS_TILE * 16 == 64 * NWS_NW, "16 aggregation lanes per destination of a tile");
+// <= 240 VGPRs (amdgpu_num_vgpr counts register pairs): two waves per SIMD leave a pair-stream wave
+// (32 VGPRs) room beside them, as the edge ring
+template <bool FINAL>
+__global__ __attribute__((amdgpu_flat_work_group_size(1, 64 * NWS_NW), amdgpu_waves_per_eu(2, 2),
+                          amdgpu_num_vgpr(120)))
+void k_node_ws(NodeArgs a, int ntiles) {
+  constexpr int NG = NWS_TILE / 16;
+  __shared__ __attribute__((aligned(16))) float s_attn[NWS_TILE * LDS_ATTN];  // aggregated rows (fp32), 16 KiB
+  __shared__ __attribute__((aligned(16))) u16 s_n[NWS_TILE * LDS_N];       // n / new h as a bf16 operand, 8 KiB
+  __shared__ __attribute__((aligned(16))) u16 s_t[NWS_TILE * LDS_T];   // FFN hidden (bf16), 16 KiB
+  __shared__ __attribute__((aligned(16))) u16 s_q[FINAL ? 8 : 3 * MAT128 * BLK];  // Q|K|V weights, 96 KiB
+  const int lane = lane_id(), g = lane >> 4, r = lane & 15;
+  const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+  const u16* W = reinterpret_cast<const u16*>(a.wmat);
+  const float* V = a.wvec;
+  if constexpr (!FINAL) dma_blocks<NWS_NW>(s_q, W + NL_Q * BLK, 3 * MAT128);
+  // this wave's register-resident weights (A fragments: output block bo, k-step s of a 128x128 matrix)
+  auto frag = [&](int m, int bo, int s) {
+    return *reinterpret_cast<const bf16x8*>(W + (m + bo * 4 + s) * BLK + lane * 8);
+  };
+  bf16x8 fo[4], f1[2][4], f2[2][4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    fo[s] = frag(NL_ON, w, s);
+#pragma unroll
+    for (int b = 0; b < 2; ++b) f1[b][s] = frag(NL_F1 + MAT128 * ((2 * w + b) >> 3), (2 * w + b) & 7, s);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) f2[h][s] = frag(NL_F2 + MAT128 * h, w, s);
+  }
+  auto lds_op = [&](const u16* rows, int stride, int q, int f0) {
+    Op<BF16T, 4> o;
+    const u16* row = rows + (q * 16 + r) * stride + f0;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const uint2 lo = *reinterpret_cast<const uint2*>(row + 32 * s + 4 * g);
+      const uint2 hi = *reinterpret_cast<const uint2*>(row + 32 * s + 16 + 4 * g);
+      o.f[s] = __builtin_bit_cast(bf16x8, (uint4){lo.x, lo.y, hi.x, hi.y});
+    }
+    return o;
+  };
+  auto put_slice = [&](u16* rows, int stride, int q, int f, floatx4 x) {
+    *reinterpret_cast<uint2*>(rows + (q * 16 + r) * stride + f + 4 * g) =
+        (uint2){pack_bf16x2(x[0], x[1]), pack_bf16x2(x[2], x[3])};
+  };
+  bool qkv_landed = FINAL;
+  const int j = threadIdx.x & 15, nl = threadIdx.x >> 4;  // aggregation: destination nl of the tile, lane j
+  auto tile_of = [&](int i) { return (gridDim.x & 7) == 0 ? xcd_slot(i, ntiles) : i; };
+  // this lane's CSR range and first source id of a tile's destination (issued a tile ahead)
+  int e0 = 0, e1 = 0, id0 = 0;
+  auto seg_head = [&](int i) {
+    const int v = tile_of(i) * NWS_TILE + nl;
+    e0 = e1 = id0 = 0;
+    if (i < ntiles && v < a.Nt) {
+      e0 = a.in_ptr[v];
+      e1 = a.in_ptr[v + 1];
+    }
+  };
+  auto seg_id0 = [&]() { id0 = e0 + j < e1 ? a.src[e0 + j] : 0; };
+  seg_head((int)blockIdx.x);
+  seg_id0();
+#pragma unroll 1
+  for (int i = (int)blockIdx.x; i < ntiles; i += (int)gridDim.x) {
+    const int vb = tile_of(i) * NWS_TILE;
+    // ---- 1. wV / (z + 1e-6), 16 lanes per destination (k_node_fast's sums)
+    {
+      constexpr int FPL = 8;
+      float acc[FPL];
+#pragma unroll
+      for (int f = 0; f < FPL; ++f) acc[f] = 0.f;
+      float z = 0.f;
+      // empty past Nt (e0 == e1): the shuffles stay inside the 16-lane group
+      seg_sum16<SEG_U>(buf_rsrc(reinterpret_cast<const u16*>(a.qkv) + 2 * HID), buf_rsrc(a.alpha), a.src, e0, e1, j,
+                       threadIdx.x & 48, id0, acc, z);
+      seg_head(i + (int)gridDim.x);  // the next tile's CSR range, in flight under this tile's update
+      const float d = z + 1e-6f;
+      float* out = s_attn + nl * LDS_ATTN + FPL * j;
+      st4(out, (floatx4){acc[0] / d, acc[1] / d, acc[2] / d, acc[3] / d});
+      st4(out + 4, (floatx4){acc[4] / d, acc[5] / d, acc[6] / d, acc[7] / d});
+    }
+    // ---- 2. the update: wave w's output blocks for both column groups
+    int vq[NG];
+    bool valid[NG];
+    Act<1> n[NG];
+#pragma unroll
+    for (int q = 0; q < NG; ++q) {
+      vq[q] = vb + q * 16 + r;
+      valid[q] = vq[q] < a.Nt;
+      const int vc = valid[q] ? vq[q] : a.Nt - 1;
+      n[q].v[0] = ld4(V + NLV_ON + 16 * w + 4 * g) + ld4(reinterpret_cast<const u16*>(a.h_in) + (int64_t)vc * HID + 16 * w + 4 * g);
+    }
+    __syncthreads();  // the aggregated rows (and, tile > 0, every wave past the previous tile's reads)
+    // n = b_O + h_in + O(attn)
+#pragma unroll
+    for (int q = 0; q < NG; ++q) {
+      Act<8> wv;
+#pragma unroll
+      for (int b = 0; b < 8; ++b)
+        wv.v[b] = *reinterpret_cast<const floatx4*>(s_attn + (q * 16 + r) * LDS_ATTN + 16 * b + 4 * g);
+      Op<BF16T, 4> op;
+      make_op(op, wv);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) n[q].v[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fo[s], op.f[s], n[q].v[0], 0, 0, 0);
+      put_slice(s_n, LDS_N, q, 16 * w, n[q].v[0]);
+    }
+    floatx4 b1[2];
+#pragma unroll
+    for (int b = 0; b < 2; ++b) b1[b] = ld4(V + NLV_F1 + 16 * (2 * w + b) + 4 * g);
+    seg_id0();  // the next tile's first source ids
+    __syncthreads();  // n, all 128 features of both groups
+    // FFN hidden: blocks 2w, 2w + 1 of the 16
+#pragma unroll
+    for (int q = 0; q < NG; ++q) {
+      const Op<BF16T, 4> nop = lds_op(s_n, LDS_N, q, 0);
+      Act<2> tq;
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        tq.v[b] = b1[b];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) tq.v[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f1[b][s], nop.f[s], tq.v[b], 0, 0, 0);
+      }
+      silu2_<2, true>(tq);
+#pragma unroll
+      for (int b = 0; b < 2; ++b) put_slice(s_t, LDS_T, q, 16 * (2 * w + b), tq.v[b]);
+    }
+    __syncthreads();  // the hidden layer, all 256 features (and every wave is past its n operands)
+    // FFN output block w: both hidden halves in order, as k_node_fast
+#pragma unroll
+    for (int q = 0; q < NG; ++q) {
+      Act<1> o;
+      zero(o);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const Op<BF16T, 4> top = lds_op(s_t, LDS_T, q, HID * h);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) o.v[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f2[h][s], top.f[s], o.v[0], 0, 0, 0);
+      }
+      add_(n[q], o);
+      if (valid[q]) st4(reinterpret_cast<u16*>(a.h_out) + (int64_t)vq[q] * HID + 16 * w + 4 * g, n[q].v[0]);
+      if constexpr (FINAL) {
+        if (a.hT_out != nullptr && valid[q]) {
+          u16* hT = reinterpret_cast<u16*>(a.hT_out);
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            hT[(int64_t)(16 * w + 4 * g + k) * a.Nt + vq[q]] = (u16)(pack_bf16x2(n[q].v[0][k], 0.f) & 0xffffu);
+        }
+      } else {
+        put_slice(s_n, LDS_N, q, 16 * w, n[q].v[0]);
+      }
+    }
+    if constexpr (!FINAL) {
+      floatx4 bq[3];
+#pragma unroll
+      for (int b = 0; b < 3; ++b) bq[b] = ld4(V + NLV_Q + 16 * (3 * w + b) + 4 * g);
+      if (!qkv_landed) {  // first tile only: this wave's pieces of the Q|K|V weights, before the barrier
+        lds_dma_wait();
+        qkv_landed = true;
+      }
+      __syncthreads();  // the new h, all 128 features (s_n's previous readers finished before the last barrier)
+      // next layer's Q | K | V: blocks 3w .. 3w + 2 of the 24 (Q 0-7, K 8-15, V 16-23)
+      bf16x8 fq[3][4];
+#pragma unroll
+      for (int b = 0; b < 3; ++b)
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const int ob = 3 * w + b;
+          fq[b][s] = *reinterpret_cast<const bf16x8*>(s_q + (MAT128 * (ob >> 3) + (ob & 7) * 4 + s) * BLK + lane * 8);
+        }
+#pragma unroll
+      for (int q = 0; q < NG; ++q) {
+        const Op<BF16T, 4> hop = lds_op(s_n, LDS_N, q, 0);
+        u16* qo = reinterpret_cast<u16*>(a.qkv_out) + (int64_t)vq[q] * 3 * HID;
+#pragma unroll
+        for (int b = 0; b < 3; ++b) {
+          floatx4 x = bq[b];
+#pragma unroll
+          for (int s = 0; s < 4; ++s) x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fq[b][s], hop.f[s], x, 0, 0, 0);
+          if (valid[q]) st4(qo + 16 * (3 * w + b) + 4 * g, x);
+        }
       }
     }
   }
@@ -2277,12 +2500,13 @@ extern "C" int di_node_layer(const di_graph* g, di_dtype dt, int final_layer, co
   hipStream_t s = (hipStream_t)stream;
   const dim3 grid = grid_of<NodeGeo>(a.Nt), block = block_of<NodeGeo>();
   if (dt == DI_BF16) {
-    // 16 destinations per 256-thread block, output features split over its waves (k_node_fast)
+    // persistent weight-stationary blocks, one per CU, 32-destination tiles (k_node_ws)
     if (!g->src || !g->in_ptr) return DI_EINVAL;
-    constexpr int NPB = NF_NODES * NF_GROUPS;
-    const dim3 gf((unsigned)((a.Nt + NPB - 1) / NPB)), bf(256 * NF_GROUPS);
-    if (final_layer) hipLaunchKernelGGL((k_node_fast<true, NF_GROUPS>), gf, bf, 0, s, a);
-    else hipLaunchKernelGGL((k_node_fast<false, NF_GROUPS>), gf, bf, 0, s, a);
+    const int ntiles = (a.Nt + NWS_TILE - 1) / NWS_TILE;
+    const int cus = device_cus();
+    const dim3 gw((unsigned)(ntiles < cus ? ntiles : cus)), bw(64 * NWS_NW);
+    if (final_layer) hipLaunchKernelGGL((k_node_ws<true>), gw, bw, 0, s, a, ntiles);
+    else hipLaunchKernelGGL((k_node_ws<false>), gw, bw, 0, s, a, ntiles);
   } else {
     if (final_layer) hipLaunchKernelGGL((k_node_layer<F32T, true>), grid, block, 0, s, a);
     else hipLaunchKernelGGL((k_node_layer<F32T, false>), grid, block, 0, s, a);

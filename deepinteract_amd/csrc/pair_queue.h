@@ -2,7 +2,7 @@
 // signal, shared by the queue kernels (pair_tensor.hip) and the GeoT launches that carry the signal
 // (geot_kernels.hip: the node embedding / fused embedding + InitEdge of the next micro-batch).
 // Words (uint32): READY at 0 (jobs signalled, monotonic), ERROR at 32 (bit 0: a help completion wait
-// timed out), GAVE_UP at 33, stream / help bytes (u64) at 40 / 42; job k's record at 64 + 64 k words
+// timed out, bit 1: a stream wave read a non-increasing ticket), GAVE_UP at 33, stream / help bytes (u64) at 40 / 42; job k's record at 64 + 64 k words
 // (256 B): TICKET at +0, DONE at +32 (on its own 128-B line).
 #pragma once
 #include <hip/hip_runtime.h>

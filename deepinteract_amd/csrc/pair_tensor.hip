@@ -376,6 +376,7 @@ void k_pair_stream(const di_pair_job* __restrict__ jobs, int hidden, uint32_t* _
     const di_pair_job J = uni(jobs[k]);
     uint32_t* tick = pq_ticket(q, k);
     uint64_t bytes = 0;
+    uint32_t done = 0, bad = 0;
     uint32_t t = pq_take(tick, lane);
     while (t < (uint32_t)J.items) {
       di_pair_desc d;
@@ -386,9 +387,20 @@ void k_pair_stream(const di_pair_job* __restrict__ jobs, int hidden, uint32_t* _
                                                 reinterpret_cast<T*>(J.out), lane, [&] { tn = pq_take_async(tick); });
       bytes += r1 > r0 ? (uint64_t)(r1 - r0) * d.l2 * sizeof(T) : 0;
       // >= PAIR_INFLIGHT + 1 stores after the atomic and a vmcnt(PAIR_INFLIGHT) after the last one
-      t = pq_read(tn, after > PAIR_INFLIGHT);
-      if (lane == 0) __hip_atomic_fetch_add(pq_done(q, k), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint32_t next = pq_read(tn, after > PAIR_INFLIGHT);
+      // tickets of one counter only grow: a repeated or smaller one means the asynchronous atomic's
+      // register was read before its result landed (pq_take_async's contract broken by codegen)
+      bad |= next <= t;
+      t = next;
+      ++done;
     }
+    if (done) {
+      // DONE counts items whose stores have completed (acknowledged by L2): the help launch that waits
+      // for DONE and the kernel boundary after it then publish them to every later launch
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane == 0) __hip_atomic_fetch_add(pq_done(q, k), done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (lane == 0 && bad) __hip_atomic_fetch_or(q + PQ_ERROR, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (lane == 0 && bytes)
       __hip_atomic_fetch_add(reinterpret_cast<uint64_t*>(q + PQ_SBYTES), bytes, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
@@ -404,6 +416,7 @@ void k_pair_help(const di_pair_job* __restrict__ jobs, int hidden, uint32_t* __r
   for (int k = first; k <= last; ++k) {
     const di_pair_job J = uni(jobs[k]);
     uint32_t* tick = pq_ticket(q, k);
+    uint32_t done = 0;
     for (uint32_t t = pq_take(tick, lane); t < (uint32_t)J.items; t = pq_take(tick, lane)) {
       di_pair_desc d;
       int c = 0, r0 = 0, r1 = 0;
@@ -412,7 +425,11 @@ void k_pair_help(const di_pair_job* __restrict__ jobs, int hidden, uint32_t* __r
                                  reinterpret_cast<T*>(J.out), lane, [] {});
         bytes += (uint64_t)(r1 - r0) * d.l2 * sizeof(T);
       }
-      if (lane == 0) __hip_atomic_fetch_add(pq_done(q, k), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      ++done;
+    }
+    if (done) {  // as in k_pair_stream: DONE only for items whose stores have completed
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane == 0) __hip_atomic_fetch_add(pq_done(q, k), done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
   if (lane == 0 && bytes)

@@ -17,6 +17,19 @@ previous job is done before the slot is rewritten -- which also stores pair item
 rate whenever GeoT has run `ring` jobs ahead. finish() drains every job (the end of a run).
 Correctness never depends on the two streams running concurrently (a stream wave that waits longer
 than `patience_ms` gives up and the help launches complete the job).
+
+Hardware queues (round 6). The persistent pair-stream launch is issued BEFORE the GeoT launches that
+signal its jobs, so it only overlaps them when the two streams reach the GPU through different
+hardware queues. HIP multiplexes a process's streams onto GPU_MAX_HW_QUEUES (4 on the box) in-order
+queues per priority, least-used first, so an ordinary stream's queue depends on every stream created
+before it: in a process with an RCCL communicator (bench.py under torchrun, or --dist) torch's pool
+stream landed on the NULL stream's queue, the pair launch sat in front of the GeoT launches and every
+stream wave waited out its patience (round 5: 3767 complexes/s, gave_up 1024). The schedule therefore
+runs on `schedule_streams(device)`: two streams created with a CU mask covering every CU, which the HIP
+runtime places on hardware queues of their own (di_stream_create_dedicated), and it measures the
+property at construction (di_streams_concurrent). If two given streams do not run concurrently the
+schedule does not launch the pair stream at all (no wave can wait behind its own producer): every job
+is completed by a help launch right after its forward ("ordered" mode, the serial rate).
 """
 from __future__ import annotations
 
@@ -63,21 +76,68 @@ class PairQueue:
                 "help_bytes": u64(_lib.PQ_HBYTES)}
 
 
+_STREAMS = {}
+
+
+def schedule_streams(device=None):
+    """(GeoT stream, pair stream) of the overlapped schedule on `device`: two torch ExternalStreams on
+    hardware queues of their own (di_stream_create_dedicated), created once per process and device and
+    shared by every schedule. Nothing else should be issued on the NULL stream while a step runs (the
+    streams are blocking streams)."""
+    dev = torch.device(device if device is not None else "cuda")
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    if idx not in _STREAMS:
+        lib = _lib.load()
+        handles = []
+        with torch.cuda.device(idx):
+            for _ in range(2):
+                h = ctypes.c_void_p()
+                _lib.check(lib.di_stream_create_dedicated(ctypes.byref(h)), "di_stream_create_dedicated")
+                handles.append(h.value)
+        _STREAMS[idx] = tuple(torch.cuda.ExternalStream(h, device=torch.device("cuda", idx)) for h in handles)
+    return _STREAMS[idx]
+
+
+def streams_concurrent(a, b, patience_ms: float = 200.0) -> bool:
+    """Whether work issued on stream b runs while a kernel issued earlier on stream a is still running
+    (di_streams_concurrent: the two streams are on different hardware queues). Synchronises both."""
+    lib = _lib.load()
+    work = torch.zeros(64, dtype=torch.int32, device=a.device)
+    torch.cuda.synchronize(a.device)
+    out = ctypes.c_int32(-1)
+    _lib.check(lib.di_streams_concurrent(ctypes.c_void_p(a.cuda_stream), ctypes.c_void_p(b.cuda_stream), _ptr(work),
+                                         float(patience_ms), ctypes.byref(out)), "di_streams_concurrent")
+    return out.value == 1
+
+
 class OverlappedSchedule:
     """GeoT || pair tensor over resident micro-batches (graph batches of equal shape).
 
     eng: GeoTEngine; mbs: list of GraphBatch (one step = every micro-batch once); h1r/h2r/l1/l2: the
     per-complex pair descriptors (rows in the micro-batch, chain lengths), the same for every
     micro-batch; sinks: output buffers, job j writes sinks[j % len(sinks)] (a list with one buffer per
-    job keeps every pair tensor). s_geot / s_pair: the two HIP streams."""
+    job keeps every pair tensor). Up to `ring` jobs are in flight, so with fewer than `ring` sinks two
+    jobs in flight may write one buffer at once: that needs discard_outputs=True (a benchmark that never
+    reads them). s_geot / s_pair: the two HIP streams (None: schedule_streams(device), the default);
+    streams that turn out not to run concurrently put the schedule in "ordered" mode (module doc).
+    tap(job, h, e): called right after each micro-batch's forward is issued, with the engine's node /
+    edge feature outputs of that forward, while the GeoT stream is current (stream-ordered copies taken
+    there see exactly what the schedule computed, before the workspace is reused)."""
 
-    def __init__(self, eng, mbs, h1r, h2r, l1, l2, sinks, s_geot, s_pair, ring=16, help_every=4,
+    def __init__(self, eng, mbs, h1r, h2r, l1, l2, sinks, s_geot=None, s_pair=None, ring=16, help_every=4,
                  stream_blocks=0, stream_waves=0, help_blocks=0, help_waves=0, patience_ms=20.0,
-                 capacity_steps=64, jobs_per_launch=0):
+                 capacity_steps=64, jobs_per_launch=0, discard_outputs=False, tap=None):
         if help_every < 1 or ring < 2 * help_every:
             raise ValueError("need ring >= 2 * help_every")
         self.eng, self.mbs = eng, mbs
+        if s_geot is None or s_pair is None:
+            g, p = schedule_streams(eng.device)
+            s_geot, s_pair = s_geot or g, s_pair or p
         self.s_geot, self.s_pair = s_geot, s_pair
+        self.tap, self.discard_outputs = tap, bool(discard_outputs)
+        # the property the persistent pair launch needs (module doc); measured, not assumed
+        self.concurrent = s_geot is not s_pair and streams_concurrent(s_pair, s_geot)
+        self.mode = "overlapped" if self.concurrent else "ordered"
         self.ring, self.help_every, self.patience = ring, help_every, float(patience_ms)
         # pair-stream launches cover this many jobs each (0: one launch per step)
         self.jobs_per_launch = int(jobs_per_launch) or len(mbs)
@@ -151,26 +211,41 @@ class OverlappedSchedule:
         launch (dict key "pair_tensor"); geot_events: around every GeoT launch (per-kernel timing)."""
         self._rollover()
         j0, n = self.next_job, len(self.mbs)
-        with torch.cuda.stream(self.s_pair):
-            tick = _Ticker(events)
-            for a in range(j0, j0 + n, self.jobs_per_launch):
-                tick("pair_tensor")
-                self._stream(a, min(a + self.jobs_per_launch, j0 + n), ctypes.c_void_p(self.s_pair.cuda_stream))
-            tick(None)
+        if len(self.sinks) < self.ring and j0 + n > len(self.sinks) and not self.discard_outputs:
+            raise ValueError(f"{len(self.sinks)} sinks for up to {self.ring} jobs in flight: job {len(self.sinks)} "
+                             f"would overwrite job 0's pair tensors while it may still be written (pass "
+                             f"discard_outputs=True if they are never read)")
+        if self.concurrent:
+            with torch.cuda.stream(self.s_pair):
+                tick = _Ticker(events)
+                for a in range(j0, j0 + n, self.jobs_per_launch):
+                    tick("pair_tensor")
+                    self._stream(a, min(a + self.jobs_per_launch, j0 + n), ctypes.c_void_p(self.s_pair.cuda_stream))
+                tick(None)
         with torch.cuda.stream(self.s_geot):
             st = ctypes.c_void_p(self.s_geot.cuda_stream)
             for m, gb in enumerate(self.mbs):
                 j = j0 + m
-                if j % self.help_every == 0:
+                if self.concurrent and j % self.help_every == 0:
                     # jobs j .. j + help_every - 1 reuse the ring slots of jobs up to j + help_every - 1 - ring
                     last = j + self.help_every - 1 - self.ring
                     if last >= self.helped:
                         self._help(self.helped, last, st)
                         self.helped = last + 1
                 # this forward's first launch signals job j - 1 unless a help launch just did
-                self.eng.forward(gb, clone=False, events=geot_events, hT_out=self.hT[j % self.ring],
-                                 signal=(self.queue.state, self.pending) if self.pending >= 0 else None)
+                h, e = self.eng.forward(gb, clone=False, events=geot_events, hT_out=self.hT[j % self.ring],
+                                        signal=(self.queue.state, self.pending) if self.pending >= 0 else None)
+                if self.tap is not None:
+                    self.tap(j, h, e)
                 self.pending = j
+                if not self.concurrent:
+                    # ordered mode: the job's pair tensors by a help launch right behind its forward
+                    # (which also signals it); no launch ever waits on the device for a later one
+                    tick = _Ticker(events)
+                    tick("pair_tensor")
+                    self._help(j, j, st)
+                    tick(None)
+                    self.helped = j + 1
         self.next_job = j0 + n
 
     def finish(self):
@@ -184,14 +259,21 @@ class OverlappedSchedule:
                 _lib.check(self.eng.lib.di_pair_signal(self._q(), self.pending, st), "di_pair_signal")
                 self.pending = -1
 
-    def check(self):
-        """Raise if a help launch's completion wait timed out (host read of the queue's error word)."""
+    def check(self, allow_gave_up=False):
+        """Host read of the queue's counters (synchronises). Raises if a help launch's completion wait
+        timed out or a stream wave read a non-increasing ticket (error word), and -- unless
+        allow_gave_up -- if any stream wave gave up waiting for a signal: the outputs are still complete
+        then (the help launches wrote them), but the overlap the schedule exists for did not happen."""
         c = self.queue.counters()
         if c["error"]:
             raise RuntimeError(f"pair queue error {c}")
+        if c["gave_up"] and not allow_gave_up:
+            raise RuntimeError(f"pair stream waves gave up waiting for their signal (the streams did not run "
+                               f"concurrently): {c}")
         return c
 
-    def views(self, job):
-        """The [1, 2H, L1, L2] pair tensors job `job` wrote (valid until its sink is reused)."""
-        out, H = self.sinks[job % len(self.sinks)], self.hidden
+    def views(self, job, buf=None):
+        """The [1, 2H, L1, L2] pair tensors job `job` wrote (valid until its sink is reused, i.e. until
+        job + len(sinks) is issued), or the same views of `buf` (a copy of its sink)."""
+        out, H = (self.sinks[job % len(self.sinks)] if buf is None else buf), self.hidden
         return [out[o:o + 2 * H * a * b].view(1, 2 * H, a, b) for o, a, b in zip(self.offs, self.l1, self.l2)]

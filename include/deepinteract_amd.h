@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define DI_ABI_VERSION 7
+#define DI_ABI_VERSION 8
 
 /* activation / weight storage type of the GeoT kernels (accumulation is always fp32). A plain
  * int32 (not a C enum type): a foreign caller may pass any value, and every entry point refuses
@@ -231,7 +231,8 @@ int di_pair_tensor_check(int32_t num_complexes, int32_t max_l1, int32_t max_l2, 
  * take the job's items (complex, channel, 64-row block) from the queue's per-job ticket counter, with
  * the bounded non-temporal stores of di_pair_launch.beside. di_pair_help takes the remaining items of
  * its jobs with plain stores on the whole chip and returns (on the device) once every item of them is
- * done, whoever took it. Completion never depends on di_pair_stream running concurrently: a stream
+ * done, whoever took it: a wave counts its items DONE only after its stores have completed, so every
+ * launch ordered after a help launch on its stream reads the jobs' final bytes. Completion never depends on di_pair_stream running concurrently: a stream
  * wave that waits longer than patience_ms for a signal gives up and the help launches do the rest. The
  * bytes written are those of di_pair_tensor(aligned = 1) for the same descriptors.
  * Preconditions (the kernels cannot check device-resident jobs): every job's descs are 16-B aligned
@@ -247,7 +248,8 @@ typedef struct {
   int32_t items;              /* di_pair_job_items(num_complexes, max_l1, hidden) */
 } di_pair_job;
 /* device bytes of a queue for jobs 0 .. num_jobs-1 (zero it before first use; -1 for num_jobs <= 0).
- * Words (uint32): [0] jobs signalled, [32] error bits (1: a help launch's completion wait timed out),
+ * Words (uint32): [0] jobs signalled, [32] error bits (1: a help launch's completion wait timed out,
+ * 2: a stream wave read a non-increasing ticket),
  * [33] stream waves that gave up waiting, [40..41] / [42..43] bytes written by stream / help launches
  * (uint64), then 256 B per job (ticket, arrive, done; csrc/pair_queue.h). */
 int64_t di_pair_queue_bytes(int32_t num_jobs);
@@ -264,6 +266,24 @@ int di_pair_stream(di_dtype dt, const di_pair_job* jobs, int32_t job_begin, int3
  * launch's start (as di_node_embed's signal) */
 int di_pair_help(di_dtype dt, const di_pair_job* jobs, int32_t first_job, int32_t last_job, int32_t hidden,
                  void* queue, const di_pair_launch* launch, int32_t signal_job, void* stream);
+
+/* ---- streams of the overlapped schedule (ABI 8; host calls, synchronous) ---------------------------
+ * di_pair_stream waits on the device for signals that launches on the producer's stream raise, so the
+ * two streams must reach the GPU through DIFFERENT hardware queues. HIP multiplexes a process's
+ * streams onto at most GPU_MAX_HW_QUEUES in-order queues per priority (least-used first once the pool
+ * is full), so which queue an ordinary stream gets depends on every stream created before it (an RCCL
+ * communicator creates several); two streams on one queue run one after the other and every stream
+ * wave waits out its patience.
+ * di_stream_create_dedicated: a normal-priority stream whose CU mask covers every CU -- the runtime
+ * gives each CU-masked stream a hardware queue of its own, never shared with another stream. Like every
+ * stream created with default flags it synchronises with the legacy NULL stream: issue nothing on the
+ * NULL stream while a pair-stream launch is in flight.
+ * di_streams_concurrent: measures the property: a one-wave kernel on `a` waits (at most patience_ms,
+ * <= 10000) for a word that a kernel on `b`, issued after it, raises; *concurrent (host) = 1 if it saw
+ * it, else 0. work: >= 256 device bytes, overwritten. Synchronises both streams. */
+int di_stream_create_dedicated(void** stream);
+int di_stream_destroy(void* stream);
+int di_streams_concurrent(void* a, void* b, void* work, float patience_ms, int32_t* concurrent);
 
 /* Fused head prologue: x = ELU(InstanceNorm2d(conv2d_1(T))) of the contact
  * head (ResNet2DInputWithOptAttention.forward, deepinteract_modules.py:1181-1184, 1228-1232) for a

@@ -25,7 +25,7 @@ def test_library_builds_and_exports_all_declared_symbols():
 
 def test_abi_version_and_blob_sizes():
     lib = _lib.load()
-    assert lib.di_abi_version() == _lib.ABI_VERSION == 7
+    assert lib.di_abi_version() == _lib.ABI_VERSION == 8
     for kind, (nblk, nvec) in packing.BLOB_SIZES.items():
         assert lib.di_blob_bytes(kind, _lib.DI_F32, 0) == nblk * 512 * 4
         assert lib.di_blob_bytes(kind, _lib.DI_BF16, 0) == nblk * 512 * 2
@@ -128,6 +128,21 @@ def test_pair_queue_host_contract():
     assert lib.di_pair_help(_lib.DI_BF16, p, 4, 3, 128, p, None, -1, None) == -1
     assert lib.di_pair_help(_lib.DI_F32, None, 0, 3, 128, p, None, -1, None) == -1
     assert lib.di_pair_help(_lib.DI_F32, p, 0, 3, 128, p, ctypes.byref(bad), -1, None) == -1
+
+
+def test_stream_helpers_host_contract():
+    """ABI 8's stream helpers refuse bad arguments before touching the device."""
+    lib = _lib.load()
+    assert lib.di_stream_create_dedicated(None) == -1
+    assert lib.di_stream_destroy(None) == -1
+    out = ctypes.c_int32(7)
+    p, q = ctypes.c_void_p(16), ctypes.c_void_p(32)
+    assert lib.di_streams_concurrent(p, q, None, 100.0, ctypes.byref(out)) == -1       # no work buffer
+    assert lib.di_streams_concurrent(p, q, p, 0.0, ctypes.byref(out)) == -1            # no patience
+    assert lib.di_streams_concurrent(p, q, p, 20000.0, ctypes.byref(out)) == -1        # too long
+    assert lib.di_streams_concurrent(p, p, p, 100.0, ctypes.byref(out)) == -1          # one stream
+    assert lib.di_streams_concurrent(p, q, p, 100.0, None) == -1
+    assert out.value == 7
 
 
 def _declared_struct_fields(name):

@@ -92,3 +92,53 @@ def test_aggregate_ragged_csr(dtype):
     print(f"di_node_aggregate {dtype} ragged: {err:.3e}")
     assert err < 1e-5
     assert (got[deg == 0] == 0).all()
+
+
+@pytest.mark.parametrize("final", [False, True])
+def test_node_layer_ragged_csr_matches_split(final):
+    """The bf16 di_node_layer (k_node_ws: persistent weight-stationary blocks, 32-destination tiles)
+    on a ragged CSR -- in-degrees 0..40 (empty destinations, segments over several 8-edge chunks), a
+    node count that leaves the last tile partial and more tiles than blocks -- bit-identical to the
+    split form (di_node_aggregate + di_node_update) in h, Q|K|V and hT."""
+    from deepinteract_amd import _lib
+    lib = _lib.load()
+    eng = _engine("bf16")
+    nm, nv = eng.packed.node[1 if final else 0]
+    g = torch.Generator().manual_seed(11)
+    n = 32 * 300 + 13
+    deg = torch.randint(0, 41, (n,), generator=g)
+    deg[:6] = torch.tensor([0, 1, 8, 9, 17, 40])
+    in_ptr = torch.zeros(n + 1, dtype=torch.int32)
+    in_ptr[1:] = torch.cumsum(deg, 0)
+    E = int(in_ptr[-1])
+    src = torch.randint(0, n, (E,), generator=g, dtype=torch.int32)
+    alpha = torch.exp(torch.empty(E, 4).uniform_(-5, 5, generator=g))
+    dev = torch.device("cuda")
+    qkv = torch.randn(n, 384, generator=g).to(torch.bfloat16).to(dev)
+    h_in = torch.randn(n, 128, generator=g).to(torch.bfloat16).to(dev)
+    d_src, d_ptr, d_alpha = src.to(dev), in_ptr.to(dev), alpha.to(dev)
+    cg = _lib.DiGraph(n, E, d_src.data_ptr(), None, None, None, d_ptr.data_ptr())
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    outs = []
+    for split in (False, True):
+        h_out = torch.full((n, 128), float("nan"), dtype=torch.bfloat16, device=dev)
+        q_out = None if final else torch.full((n, 384), float("nan"), dtype=torch.bfloat16, device=dev)
+        hT = torch.full((128, n), float("nan"), dtype=torch.bfloat16, device=dev) if final else None
+        p = lambda t: None if t is None else t.data_ptr()  # noqa: E731
+        if split:
+            attn = torch.empty(n, 128, device=dev)
+            assert lib.di_node_aggregate(ctypes.byref(cg), _lib.DI_BF16, p(d_alpha), p(qkv), p(attn), st) == 0
+            assert lib.di_node_update(ctypes.byref(cg), _lib.DI_BF16, int(final), p(attn), p(h_in), p(nm), p(nv),
+                                      p(h_out), p(q_out), p(hT), st) == 0
+        else:
+            assert lib.di_node_layer(ctypes.byref(cg), _lib.DI_BF16, int(final), p(d_alpha), p(h_in), p(qkv), p(nm),
+                                     p(nv), p(h_out), p(q_out), p(hT), st) == 0
+        torch.cuda.synchronize()
+        outs.append((h_out, q_out, hT))
+    (h0, q0, t0), (h1, q1, t1) = outs
+    assert torch.isfinite(h0.float()).all()
+    assert torch.equal(h0, h1)
+    if final:
+        assert torch.equal(t0, t1) and torch.equal(t0, h0.t())
+    else:
+        assert torch.equal(q0, q1)

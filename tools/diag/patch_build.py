@@ -70,6 +70,13 @@ DIAGS = {
     add_(n[q], o);""", """    add_(n[q], o);""", 1),
                ("geot_kernels.hip", "b < BQP ? fq[b][s] : fq2[b - BQP][s], hop.f[s], x, 0, 0, 0);",
                 "b < BQP ? fq[b][s] : frag(NL_Q + MAT128 * (ob >> 3), ob & 7, s), hop.f[s], x, 0, 0, 0);", 1)],
+    # round 6: the bf16 node layer as k_node_fast (16-destination blocks streaming the weights from L2)
+    # instead of the weight-stationary k_node_ws
+    "nodefast": [("geot_kernels.hip", """    if (final_layer) hipLaunchKernelGGL((k_node_ws<true>), gw, bw, 0, s, a, ntiles);
+    else hipLaunchKernelGGL((k_node_ws<false>), gw, bw, 0, s, a, ntiles);""", """    (void)gw; (void)bw;
+    const dim3 gf((unsigned)((a.Nt + NF_NODES - 1) / NF_NODES)), bf(256);
+    if (final_layer) hipLaunchKernelGGL((k_node_fast<true, 1>), gf, bf, 0, s, a);
+    else hipLaunchKernelGGL((k_node_fast<false, 1>), gf, bf, 0, s, a);""", 1)],
     # the beside store window: four stores in flight per pair wave (three in the product)
     "inflight4": [("pair_tensor.hip", "constexpr int PAIR_INFLIGHT = 3;", "constexpr int PAIR_INFLIGHT = 4;", 1)],
 }

@@ -1,0 +1,15 @@
+#!/bin/bash
+# round 6, session 4 (sessions 2-3: the same script on earlier trees; here padded LDS strides): the weight-stationary node layer (k_node_ws) vs k_node_fast (diag_nodefast)
+set -e
+O=gpurun_out; mkdir -p $O
+V=deepinteract_amd/lib/variants/diag_nodefast/libdeepinteract_amd.so
+timeout -k 10 600 python -u -m pytest tests/test_gpu_node_aggr.py tests/test_gpu_c3.py -x -v --timeout 300 --timeout-method thread -p no:cacheprovider > $O/r6_04_pytest.log 2>&1
+tail -3 $O/r6_04_pytest.log
+for r in 1 2; do
+  timeout -k 10 240 python bench.py --steps 3 --warmup 1 --complexes 512 --no-cpu --no-sub --no-prologue > $O/r6_04_ws_$r.json
+  timeout -k 10 240 python bench.py --steps 3 --warmup 1 --complexes 512 --no-cpu --no-sub --no-prologue --lib $V > $O/r6_04_fast_$r.json
+  python tools/show_bench.py $O/r6_04_ws_$r.json $O/r6_04_fast_$r.json
+done
+timeout -k 10 240 python bench.py --steps 3 --warmup 1 --complexes 256 --no-cpu --no-sub --no-prologue --overlap 0 --node-kernel fused > $O/r6_04_ws_serial.json
+timeout -k 10 240 python bench.py --steps 3 --warmup 1 --complexes 256 --no-cpu --no-sub --no-prologue --overlap 0 --node-kernel fused --lib $V > $O/r6_04_fast_serial.json
+python tools/show_bench.py $O/r6_04_ws_serial.json $O/r6_04_fast_serial.json
