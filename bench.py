@@ -666,6 +666,11 @@ def main():
     pmc_shape = (args.config, M, n_res, k, args.layers, args.dtype, args.overlap, args.geo_ref) == \
         ("c3", 8, 1000, 20, 2, "bf16", 1, 1)
     roof = roofline_of(kern, args.dtype)
+    if args.overlap and roof["kernel"] == "pair_tensor" and info["mode"] == "overlapped":
+        # one persistent launch spans the step: its duration includes the waves' waits for each job's
+        # signal, so this is the stream's rate over the step, a lower bound on its store bandwidth
+        # (the standalone rate of the same launch shape: tools/diag/pair_alone.py)
+        roof["achieved_is"] = "bytes the pair-stream launch stored / its whole duration (waits for signals included)"
     roof["traffic"] = load_pmc_traffic(roof["kernel"], kern.get(roof["kernel"], {}).get("bytes_per_launch")) \
         if pmc_shape else None
     bytes_c = algorithmic_bytes_per_complex(n_res, n_res, k, esz)

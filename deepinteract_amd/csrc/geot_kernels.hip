@@ -1730,9 +1730,53 @@ __global__ __launch_bounds__(NodeRingGeo::THREADS, 1) void k_node_update_ring(No
 // edge in order -- k_node_aggr's products and order, so the row is bit-identical to it for any chunk
 // size U. Every load of a chunk is issued unconditionally (a slot past e1 re-reads edge c's alpha and
 // a valid V row and adds it with weight 0, which is exact), so a chunk is one batch of buffer loads
-// (32-bit offsets from SGPR descriptors) and one wait, with no per-edge branch. On entry lane j of the
-// group holds id_first = src[e0 + j] (j < U; 0 past e1). U = 10: k = 20 in-edges are two chunks.
-constexpr int SEG_U = 10;
+// (32-bit offsets from SGPR descriptors) and one wait, with no per-edge branch. A chunk's source ids
+// arrive as two per-lane registers (lane j of the group: src[c + j] and src[c + 16 + j], 0 past e1),
+// loaded one chunk ahead; on entry (ida, idb) hold chunk e0's.
+template <int U>
+__device__ __forceinline__ void seg_ids(const int* __restrict__ src, int c, int e1, int j, int& ida, int& idb) {
+  ida = c + j < e1 && j < U ? src[c + j] : 0;
+  if constexpr (U > 16) idb = c + 16 + j < e1 && 16 + j < U ? src[c + 16 + j] : 0;
+}
+template <int U>
+__device__ __forceinline__ void seg_sum16(__amdgpu_buffer_rsrc_t vr, __amdgpu_buffer_rsrc_t ar, const int* __restrict__ src,
+                                          int e0, int e1, int j, int lane_base, int ida, int idb, float (&acc)[8],
+                                          float& z) {
+  static_assert(U >= 1 && U <= 32, "a chunk's ids come from two registers of the group's 16 lanes");
+  const int head = j >> 2;
+#pragma unroll 1
+  for (int c = e0; c < e1; c += U) {
+    const int n = min(U, e1 - c);
+    const int id_a = ida, id_b = idb;
+    float al[U];
+    uint4 vv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int id = __shfl(u < 16 ? id_a : id_b, lane_base + (u & 15), 64);
+      const int eu = u < n ? c + u : c;
+      al[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ar, (eu * 4 + head) * 4, 0, 0));
+      vv[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(vr, id * (3 * HID * 2) + 16 * j, 0, 0));
+    }
+    if (c + U < e1) seg_ids<U>(src, c + U, e1, j, ida, idb);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const float w = u < n ? al[u] : 0.f;
+      const uint32_t x[4] = {vv[u].x, vv[u].y, vv[u].z, vv[u].w};
+#pragma unroll
+      for (int f = 0; f < 8; ++f) {
+        const uint32_t b = f & 1 ? (x[f >> 1] & 0xffff0000u) : (x[f >> 1] << 16);
+        acc[f] += w * __builtin_bit_cast(float, b);
+      }
+      z += w;
+    }
+  }
+}
+
+constexpr int SEG_U = 10;     // k_node_fast (<= 120 VGPRs): k = 20 in-edges are two chunks
+// k_node_ws: chunks of 10 as well. One chunk of 20 (one memory latency per tile) spills 5 VGPRs at
+// the 240 cap and measured slower: node layers beside the pair stream 47 / 27-29 vs 43 / 26-29 us,
+// 7953 / 7918 vs 8038 / 7993 complexes/s (round 6, tools/sessions/r6_05_wsu.sh)
+constexpr int SEG_U_WS = 10;
 // LDS row strides of the node kernels' exchange buffers, padded so that a row is 4 banks (mod 64)
 // after the previous one: the 16 rows r a quarter-wave reads at one feature offset (ds_read_b128 of
 // the fp32 rows, ds_read_b64 of the bf16 operands) fall on 16 distinct bank quads instead of one
@@ -1818,8 +1862,10 @@ void k_node_fast(NodeArgs a) {
     float z = 0.f;
     if (v < a.Nt) {  // uniform per 16-lane group (the shuffles stay inside the group)
       const int e0 = a.in_ptr[v], e1 = a.in_ptr[v + 1];
+      int ida = 0, idb = 0;
+      seg_ids<SEG_U>(a.src, e0, e1, j, ida, idb);
       seg_sum16<SEG_U>(buf_rsrc(reinterpret_cast<const u16*>(a.qkv) + 2 * HID), buf_rsrc(a.alpha), a.src, e0, e1, j,
-                       threadIdx.x & 48, e0 + j < e1 ? a.src[e0 + j] : 0, acc, z);
+                       threadIdx.x & 48, ida, idb, acc, z);
     }
     const float d = z + 1e-6f;
     float* out = s_attn + nl * LDS_ATTN + FPL * j;
@@ -2064,16 +2110,16 @@ void k_node_ws(NodeArgs a, int ntiles) {
   const int j = threadIdx.x & 15, nl = threadIdx.x >> 4;  // aggregation: destination nl of the tile, lane j
   auto tile_of = [&](int i) { return (gridDim.x & 7) == 0 ? xcd_slot(i, ntiles) : i; };
   // this lane's CSR range and first source id of a tile's destination (issued a tile ahead)
-  int e0 = 0, e1 = 0, id0 = 0;
+  int e0 = 0, e1 = 0, ida = 0, idb = 0;
   auto seg_head = [&](int i) {
     const int v = tile_of(i) * NWS_TILE + nl;
-    e0 = e1 = id0 = 0;
+    e0 = e1 = 0;
     if (i < ntiles && v < a.Nt) {
       e0 = a.in_ptr[v];
       e1 = a.in_ptr[v + 1];
     }
   };
-  auto seg_id0 = [&]() { id0 = e0 + j < e1 ? a.src[e0 + j] : 0; };
+  auto seg_id0 = [&]() { seg_ids<SEG_U_WS>(a.src, e0, e1, j, ida, idb); };
   seg_head((int)blockIdx.x);
   seg_id0();
 #pragma unroll 1
@@ -2087,8 +2133,8 @@ void k_node_ws(NodeArgs a, int ntiles) {
       for (int f = 0; f < FPL; ++f) acc[f] = 0.f;
       float z = 0.f;
       // empty past Nt (e0 == e1): the shuffles stay inside the 16-lane group
-      seg_sum16<SEG_U>(buf_rsrc(reinterpret_cast<const u16*>(a.qkv) + 2 * HID), buf_rsrc(a.alpha), a.src, e0, e1, j,
-                       threadIdx.x & 48, id0, acc, z);
+      seg_sum16<SEG_U_WS>(buf_rsrc(reinterpret_cast<const u16*>(a.qkv) + 2 * HID), buf_rsrc(a.alpha), a.src, e0, e1, j,
+                          threadIdx.x & 48, ida, idb, acc, z);
       seg_head(i + (int)gridDim.x);  // the next tile's CSR range, in flight under this tile's update
       const float d = z + 1e-6f;
       float* out = s_attn + nl * LDS_ATTN + FPL * j;
@@ -2502,6 +2548,8 @@ extern "C" int di_node_layer(const di_graph* g, di_dtype dt, int final_layer, co
   if (dt == DI_BF16) {
     // persistent weight-stationary blocks, one per CU, 32-destination tiles (k_node_ws)
     if (!g->src || !g->in_ptr) return DI_EINVAL;
+    // the segment sums address V rows and alphas by 32-bit buffer offsets
+    if ((int64_t)a.Nt * 3 * HID * 2 >= (1LL << 31) || (int64_t)g->num_edges * 16 >= (1LL << 31)) return DI_ERANGE;
     const int ntiles = (a.Nt + NWS_TILE - 1) / NWS_TILE;
     const int cus = device_cus();
     const dim3 gw((unsigned)(ntiles < cus ? ntiles : cus)), bw(64 * NWS_NW);

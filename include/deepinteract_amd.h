@@ -152,7 +152,9 @@ int di_edge_layer(const di_graph* g, di_dtype dt, int final_layer, const float* 
                   const void* wmat, const float* wvec,
                   float* alpha_out /*[Et,4]*/, void* f_out, void* fn_out, void* stream);
 
-/* hT_out (optional, may be NULL): also write h_out transposed, [128, Nt] (pair-tensor input) */
+/* hT_out (optional, may be NULL): also write h_out transposed, [128, Nt] (pair-tensor input).
+ * bf16: DI_ERANGE when Nt * 768 or Et * 16 reaches 2^31 (the segment sums use 32-bit byte offsets;
+ * split such a batch, or use di_node_aggregate + di_node_update). */
 int di_node_layer(const di_graph* g, di_dtype dt, int final_layer, const float* alpha,
                   const void* h_in, const void* qkv, const void* wmat, const float* wvec,
                   void* h_out, void* qkv_out, void* hT_out, void* stream);

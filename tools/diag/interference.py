@@ -76,7 +76,8 @@ def main():
     q.set_jobs([_lib.DiPairJob(hT.data_ptr(), d_descs.data_ptr(), sinks[j % 2].data_ptr(), n_rows, M, L, items)
                 for j in range(args.jobs)])
     launch_cfg = _lib.DiPairLaunch(_lib.DI_PAIR_ROWS, 0, 0, 1)
-    s_pair, s_geot = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    from deepinteract_amd.pipeline import schedule_streams
+    s_geot, s_pair = schedule_streams(dev)  # hardware queues of their own
     job_bytes = 2 * off
 
     def ev():

@@ -25,9 +25,14 @@ def main():
     ap.add_argument("--jobs", type=int, default=16)
     ap.add_argument("--complexes", type=int, default=8)
     ap.add_argument("--res", type=int, default=1000)
+    ap.add_argument("--shapes", default=None,
+                    help="only di_pair_stream at these grids, e.g. '256x4,256x8' (XCD-restricted variants)")
     ap.add_argument("--stream-only", action="store_true",
                     help="only the beside shape (128 x 4 stream): the PMC traffic pass (tools/pmc_pair_ratio.py)")
+    ap.add_argument("--lib", default=None, help="a variant / diagnostic build of the library")
     args = ap.parse_args()
+    if args.lib:
+        _lib.load_variant(args.lib)
     lib, dev = _lib.load(), torch.device("cuda")
     H, M, L = 128, args.complexes, args.res
     n_rows = 2 * M * L
@@ -80,6 +85,14 @@ def main():
         return t, c
 
     out = []
+    if args.shapes:
+        for shape in args.shapes.split(","):
+            blocks, waves = (int(x) for x in shape.split("x"))
+            t, c = queue_run("stream", blocks, waves)
+            print(json.dumps({"what": "di_pair_stream (bounded nt stores)", "blocks": blocks, "waves": waves,
+                              "us_per_job": 1e6 * t / args.jobs, "tb_s": job_bytes * args.jobs / t / 1e12,
+                              "gave_up": c["gave_up"], "stream_bytes": c["stream_bytes"]}))
+        return
     if args.stream_only:
         t, c = queue_run("stream", 128, 4)
         print(json.dumps({"what": "di_pair_stream (bounded nt stores)", "blocks": 128, "waves": 4, "jobs_per_launch": args.jobs,

@@ -77,6 +77,23 @@ DIAGS = {
     const dim3 gf((unsigned)((a.Nt + NF_NODES - 1) / NF_NODES)), bf(256);
     if (final_layer) hipLaunchKernelGGL((k_node_fast<true, 1>), gf, bf, 0, s, a);
     else hipLaunchKernelGGL((k_node_fast<false, 1>), gf, bf, 0, s, a);""", 1)],
+    # k_node_ws's segment sums in one chunk of 20 in-edges (one memory latency per tile; 5 VGPRs
+    # spilled) instead of two chunks of 10 (round 6: slower, tools/sessions/r6_05_wsu.sh)
+    "wsu20": [("geot_kernels.hip", "constexpr int SEG_U_WS = 10;", "constexpr int SEG_U_WS = 20;", 1)],
+    # the pair stream's blocks on the first N XCDs only (block b runs on XCD b mod 8; the others exit at
+    # once): can a few XCDs' L2s and fabric links carry the store stream? (round-5 verdict item 4)
+    **{f"pairxcd{n}": [("pair_tensor.hip", """  const int lane = threadIdx.x & 63;
+  for (int k = job_begin; k < job_end; ++k) {
+    if (!pq_wait(q + PQ_READY, (uint32_t)k + 1, patience)) {""", f"""  const int lane = threadIdx.x & 63;
+  if ((int)(blockIdx.x & 7) >= {n}) return;
+  for (int k = job_begin; k < job_end; ++k) {{
+    if (!pq_wait(q + PQ_READY, (uint32_t)k + 1, patience)) {{""", 1)] for n in (1, 2, 3, 4, 6)},
+    # the LDS-resident InitEdge capped at 160 VGPRs (three waves per SIMD + one pair-stream wave fit;
+    # uncapped it allocates 168, so a CU hosting a pair-stream block cannot take its 12-wave block)
+    "initres160": [("geot_kernels.hip", """__global__ __attribute__((amdgpu_flat_work_group_size(1, 64 * IRX_NW), amdgpu_waves_per_eu(IRX_NW / 4, IRX_NW / 4)))
+void k_init_res_x32(InitArgs a, int ntiles) {""", """__global__ __attribute__((amdgpu_flat_work_group_size(1, 64 * IRX_NW), amdgpu_waves_per_eu(IRX_NW / 4, IRX_NW / 4),
+                          amdgpu_num_vgpr(80)))
+void k_init_res_x32(InitArgs a, int ntiles) {""", 1)],
     # the beside store window: four stores in flight per pair wave (three in the product)
     "inflight4": [("pair_tensor.hip", "constexpr int PAIR_INFLIGHT = 3;", "constexpr int PAIR_INFLIGHT = 4;", 1)],
 }
