@@ -1777,13 +1777,16 @@ constexpr int SEG_U = 10;     // k_node_fast (<= 120 VGPRs): k = 20 in-edges are
 // the 240 cap and measured slower: node layers beside the pair stream 47 / 27-29 vs 43 / 26-29 us,
 // 7953 / 7918 vs 8038 / 7993 complexes/s (round 6, tools/sessions/r6_05_wsu.sh)
 constexpr int SEG_U_WS = 10;
-// LDS row strides of the node kernels' exchange buffers, padded so that a row is 4 banks (mod 64)
-// after the previous one: the 16 rows r a quarter-wave reads at one feature offset (ds_read_b128 of
-// the fp32 rows, ds_read_b64 of the bf16 operands) fall on 16 distinct bank quads instead of one
-// (unpadded, every row starts on bank 0: 16-way conflicts on every exchange read and write)
-constexpr int LDS_ATTN = HID + 4;       // fp32 aggregated rows: 132 words
-constexpr int LDS_N = HID + 8;          // bf16 n / h rows: 68 words
-constexpr int LDS_T = 2 * HID + 8;      // bf16 FFN-hidden rows: 132 words
+// LDS row strides of the node kernels' exchange buffers, padded for the banking of the instructions
+// that touch them (MI355X_MICROARCH.md §LDS): the fp32 aggregated rows are read by ds_read_b128 (four
+// 16-lane groups, bank = word mod 64) -- a 136-word stride puts every group's 16 lanes (rows r, lane
+// groups g) on distinct bank quads; the bf16 operand rows are read by ds_read2_b64 and written by
+// ds_write_b64 (16 contiguous lanes per access, bank = word mod 32, 2 words per lane) -- 66 / 130-word
+// strides put 16 rows on 32 distinct banks. Unpadded (128 / 64 / 128 words) every row starts on bank
+// 0: 16-way conflicts on each exchange access (round 6, first k_node_ws build: 2x slower).
+constexpr int LDS_ATTN = HID + 8;       // fp32 aggregated rows: 136 words
+constexpr int LDS_N = HID + 4;          // bf16 n / h rows: 66 words
+constexpr int LDS_T = 2 * HID + 4;      // bf16 FFN-hidden rows: 130 words
 template <int U>
 __device__ __forceinline__ void seg_sum16(__amdgpu_buffer_rsrc_t vr, __amdgpu_buffer_rsrc_t ar, const int* __restrict__ src,
                                           int e0, int e1, int j, int lane_base, int id_first, float (&acc)[8], float& z) {

@@ -94,6 +94,13 @@ DIAGS = {
 void k_init_res_x32(InitArgs a, int ntiles) {""", """__global__ __attribute__((amdgpu_flat_work_group_size(1, 64 * IRX_NW), amdgpu_waves_per_eu(IRX_NW / 4, IRX_NW / 4),
                           amdgpu_num_vgpr(80)))
 void k_init_res_x32(InitArgs a, int ntiles) {""", 1)],
+    # the node kernels' LDS exchange rows at round 6's first padding (132 / 68 / 132 words: 2-way
+    # conflicts left) instead of the conflict-free 136 / 66 / 130
+    "ldspad4": [("geot_kernels.hip", """constexpr int LDS_ATTN = HID + 8;       // fp32 aggregated rows: 136 words
+constexpr int LDS_N = HID + 4;          // bf16 n / h rows: 66 words
+constexpr int LDS_T = 2 * HID + 4;      // bf16 FFN-hidden rows: 130 words""", """constexpr int LDS_ATTN = HID + 4;
+constexpr int LDS_N = HID + 8;
+constexpr int LDS_T = 2 * HID + 8;""", 1)],
     # the beside store window: four stores in flight per pair wave (three in the product)
     "inflight4": [("pair_tensor.hip", "constexpr int PAIR_INFLIGHT = 3;", "constexpr int PAIR_INFLIGHT = 4;", 1)],
 }
