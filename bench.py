@@ -570,7 +570,11 @@ def main():
         # nn.Embedding(max_num_graph_nodes=2304) cannot index 4000 residues, so the synthetic model is
         # built with max_num_graph_nodes=4096 (a LitGINI hyper-parameter); a [256,4000,4000] bf16
         # pair tensor is 8.19 GB, so micro-batches of 2 complexes.
-        for key, val in (("residues", 4000), ("knn", 30), ("layers", 4), ("node_limit", 4096)):
+        # the pair stream on 192 blocks x 4 waves (C3: 128): C5's GeoT stream is shorter than its pair
+        # stream (16.4 GB per micro-batch of 2), so a larger grid beside GeoT pays -- round 6, session
+        # r6_12: 128 / 160 / 192 / 224 blocks 528 / 551 / 551 / 536 complexes/s, pair roofline 0.487 /
+        # 0.549 / 0.557 / -- (192: help launches write 1.2 % of the bytes instead of 10 %)
+        for key, val in (("residues", 4000), ("knn", 30), ("layers", 4), ("node_limit", 4096), ("pair_blocks", 192)):
             if getattr(args, key) in (None, ap.get_default(key)):
                 setattr(args, key, val)
         if args.complexes == ap.get_default("complexes"):

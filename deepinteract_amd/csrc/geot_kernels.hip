@@ -1495,7 +1495,7 @@ __global__ __launch_bounds__(16 * AGG_NODES) void k_node_aggr(AggrArgs a) {
           float x;
           if constexpr (DT::kBF16) x = __builtin_bit_cast(float, (uint32_t)vv[u][f] << 16);
           else x = vv[u][f];
-          acc[f] += al[u] * x;
+          acc[f] = __builtin_fmaf(al[u], x, acc[f]);
         }
         z += al[u];
       }
@@ -1577,7 +1577,7 @@ __device__ __forceinline__ void node_gather(Act<8>& wv, const NodeArgs& a, int v
       Act<8> vv;
       vr[u].to_act(vv);
 #pragma unroll
-      for (int b = 0; b < 8; ++b) wv.v[b] += al[u][b >> 1] * vv.v[b];
+      for (int b = 0; b < 8; ++b) wv.v[b] = __builtin_elementwise_fma((floatx4)al[u][b >> 1], vv.v[b], wv.v[b]);
       z += al[u];
     }
   }
@@ -1587,7 +1587,7 @@ __device__ __forceinline__ void node_gather(Act<8>& wv, const NodeArgs& a, int v
     Act<8> vv;
     load_row(vv, qkv + (int64_t)a.src[e] * 3 * HID + 2 * HID, g);
 #pragma unroll
-    for (int b = 0; b < 8; ++b) wv.v[b] += al[b >> 1] * vv.v[b];
+    for (int b = 0; b < 8; ++b) wv.v[b] = __builtin_elementwise_fma((floatx4)al[b >> 1], vv.v[b], wv.v[b]);
     z += al;
   }
 #pragma unroll
@@ -1728,7 +1728,10 @@ __global__ __launch_bounds__(NodeRingGeo::THREADS, 1) void k_node_update_ring(No
 // The CSR segment sum of ONE destination by its 16-lane group (lane j: features 8j .. 8j + 7, head
 // j / 4): acc = sum_e alpha[e, head] * V[src e], z = sum_e alpha[e, head] over e in [e0, e1), edge by
 // edge in order -- k_node_aggr's products and order, so the row is bit-identical to it for any chunk
-// size U. Every load of a chunk is issued unconditionally (a slot past e1 re-reads edge c's alpha and
+// size U. Every product is added with an explicit fused multiply-add (here, in k_node_aggr and in
+// node_gather): a plain a += w * x is llvm.fmuladd, which the backend may fuse in one kernel and split
+// into a multiply and an add in another (round 6: a build with specialised aggregation waves differed
+// from the split form by one bf16 ulp on 1 row in 96 until its sums were explicit FMAs). Every load of a chunk is issued unconditionally (a slot past e1 re-reads edge c's alpha and
 // a valid V row and adds it with weight 0, which is exact), so a chunk is one batch of buffer loads
 // (32-bit offsets from SGPR descriptors) and one wait, with no per-edge branch. A chunk's source ids
 // arrive as two per-lane registers (lane j of the group: src[c + j] and src[c + 16 + j], 0 past e1),
@@ -1765,7 +1768,7 @@ __device__ __forceinline__ void seg_sum16(__amdgpu_buffer_rsrc_t vr, __amdgpu_bu
 #pragma unroll
       for (int f = 0; f < 8; ++f) {
         const uint32_t b = f & 1 ? (x[f >> 1] & 0xffff0000u) : (x[f >> 1] << 16);
-        acc[f] += w * __builtin_bit_cast(float, b);
+        acc[f] = __builtin_fmaf(w, __builtin_bit_cast(float, b), acc[f]);
       }
       z += w;
     }
@@ -1814,7 +1817,7 @@ __device__ __forceinline__ void seg_sum16(__amdgpu_buffer_rsrc_t vr, __amdgpu_bu
 #pragma unroll
       for (int f = 0; f < 8; ++f) {
         const uint32_t b = f & 1 ? (x[f >> 1] & 0xffff0000u) : (x[f >> 1] << 16);
-        acc[f] += w * __builtin_bit_cast(float, b);
+        acc[f] = __builtin_fmaf(w, __builtin_bit_cast(float, b), acc[f]);
       }
       z += w;
     }

@@ -1,6 +1,6 @@
-"""Node-layer split (di_node_aggregate + di_node_update) vs the fused di_node_layer (bf16:
-k_node_fast, 16 destinations per block with the update split over its waves; fp32: k_node_layer),
-and the CSR segment reduction itself vs an fp64 torch reference on ragged in-degrees.
+"""Node-layer split (di_node_aggregate + di_node_update) vs the fused di_node_layer (bf16, round 6:
+k_node_ws -- persistent weight-stationary blocks over 32-destination tiles; fp32: k_node_layer), and the CSR segment reduction itself vs an fp64 torch
+reference on ragged in-degrees.
 
 * split vs fused: bit-identical (same products, same edge order, same division, the same k-steps
   of every linear), fp32 and bf16, on the golden cases and on a full C3 micro-batch (8 x 2x1000
