@@ -24,6 +24,8 @@ NAMES = {
     "k_edge_lean<0": "edge_layer", "k_edge_lean<1": "edge_layer_final", "k_node_aggr<di::BF16T>": "node_aggr",
     "k_edge_x32_ring<0": "edge_layer", "k_edge_x32_ring<1": "edge_layer_final", "k_init_x32": "init_edge",
     "k_init_res_x32": "init_edge",
+    "k_node_ws<false>": "node_layer", "k_node_ws<true>": "node_layer_final",
+    "k_node_fast<false": "node_layer", "k_node_fast<true": "node_layer_final",
     "k_node_update_ring<false>": "node_layer", "k_node_update_ring<true>": "node_layer_final", "k_pair_lines": "pair_tensor", "k_pair_rows": "pair_tensor", "k_pair_vec": "pair_tensor",
     "k_pair_flat": "pair_tensor", "k_pair_stream": "pair_tensor", "k_pair_help": "pair_help",
     "k_prologue_rows": "head_prologue_rows", "k_prologue_tables": "head_prologue_tables",
