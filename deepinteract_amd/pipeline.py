@@ -33,6 +33,7 @@ is completed by a help launch right after its forward ("ordered" mode, the seria
 """
 from __future__ import annotations
 
+import atexit
 import ctypes
 
 import torch
@@ -79,6 +80,22 @@ class PairQueue:
 _STREAMS = {}
 
 
+def _destroy_streams():
+    """atexit: drain and destroy the dedicated streams while the HIP runtime is still up (left to the
+    runtime's own teardown they crashed the process at exit under rocprofv3)."""
+    if not _STREAMS:
+        return
+    lib = _lib.load()
+    for idx, pair in list(_STREAMS.items()):
+        try:
+            torch.cuda.synchronize(idx)
+        except RuntimeError:
+            pass
+        for st in pair:
+            lib.di_stream_destroy(ctypes.c_void_p(st.cuda_stream))
+    _STREAMS.clear()
+
+
 def schedule_streams(device=None):
     """(GeoT stream, pair stream) of the overlapped schedule on `device`: two torch ExternalStreams on
     hardware queues of their own (di_stream_create_dedicated), created once per process and device and
@@ -88,6 +105,8 @@ def schedule_streams(device=None):
     idx = dev.index if dev.index is not None else torch.cuda.current_device()
     if idx not in _STREAMS:
         lib = _lib.load()
+        if not _STREAMS:
+            atexit.register(_destroy_streams)
         handles = []
         with torch.cuda.device(idx):
             for _ in range(2):
