@@ -103,7 +103,32 @@ constexpr int LDS_N = HID + 8;
 constexpr int LDS_T = 2 * HID + 8;""", 1)],
     # the beside store window: four stores in flight per pair wave (three in the product)
     "inflight4": [("pair_tensor.hip", "constexpr int PAIR_INFLIGHT = 3;", "constexpr int PAIR_INFLIGHT = 4;", 1)],
+    # round 6, static issue priority (MI355X_MICROARCH.md, two waves per SIMD, item 4): the edge ring's
+    # second-dispatched half (waves 4-7) at s_setprio 1 for the whole launch / the first half instead
+    "prio47": [("geot_kernels.hip", "  st.fill();\n#pragma unroll 1\n", "  if (wave >= 4) __builtin_amdgcn_s_setprio(1);\n  st.fill();\n#pragma unroll 1\n", 1)],
+    "prio03": [("geot_kernels.hip", "  st.fill();\n#pragma unroll 1\n", "  if (wave < 4) __builtin_amdgcn_s_setprio(1);\n  st.fill();\n#pragma unroll 1\n", 1)],
+    # the edge ring's waves 4-7 start ~512 cycles late (a stagger against lockstep SIMD partners, item 9)
+    "stag": [("geot_kernels.hip", "  st.fill();\n#pragma unroll 1\n", "  st.fill();\n  if (wave >= 4) __builtin_amdgcn_s_sleep(8);\n#pragma unroll 1\n", 1)],
+    # k_node_ws's waves 4-7 at s_setprio 1
+    "nodeprio": [("geot_kernels.hip", "  if constexpr (!FINAL) dma_blocks<NWS_NW>(s_q, W + NL_Q * BLK, 3 * MAT128);\n  // this wave's",
+                  "  if (w >= 4) __builtin_amdgcn_s_setprio(1);\n  if constexpr (!FINAL) dma_blocks<NWS_NW>(s_q, W + NL_Q * BLK, 3 * MAT128);\n  // this wave's", 1)],
+    # the pair stream's waves at s_setprio 2: their store instructions win issue over the GeoT waves
+    # sharing their SIMD
+    "pairprio": [("pair_tensor.hip", """  const int lane = threadIdx.x & 63;
+  for (int k = job_begin; k < job_end; ++k) {
+    if (!pq_wait(q + PQ_READY, (uint32_t)k + 1, patience)) {""", """  const int lane = threadIdx.x & 63;
+  __builtin_amdgcn_s_setprio(2);
+  for (int k = job_begin; k < job_end; ++k) {
+    if (!pq_wait(q + PQ_READY, (uint32_t)k + 1, patience)) {""", 1)],
+    # InitEdge's positional rows read at half their bytes (features 0..63 twice: the traffic a bf16
+    # copy of the fp32 tables would gather; timing only)
+    "posh": [("geot_kernels.hip", """      const int f = 32 * b + 8 * q + 4 * h;
+      set_quad(acc.v[b], q, ld4(rs + f) + ld4(rd + f));""", """      const int f = 32 * (b & 1) + 8 * q + 4 * h;
+      set_quad(acc.v[b], q, ld4(rs + f) + ld4(rd + f));""", 1)],
 }
+# combinations (every substitution of each part)
+DIAGS["prio47node"] = DIAGS["prio47"] + DIAGS["nodeprio"]
+DIAGS["prio47pair"] = DIAGS["prio47"] + DIAGS["pairprio"]
 
 
 def build_diag(name):
