@@ -125,6 +125,23 @@ constexpr int LDS_T = 2 * HID + 8;""", 1)],
     "posh": [("geot_kernels.hip", """      const int f = 32 * b + 8 * q + 4 * h;
       set_quad(acc.v[b], q, ld4(rs + f) + ld4(rd + f));""", """      const int f = 32 * (b & 1) + 8 * q + 4 * h;
       set_quad(acc.v[b], q, ld4(rs + f) + ld4(rd + f));""", 1)],
+    # CU-level spatial split of the two dedicated streams (environment-driven, diagnostic only):
+    # DI_DIAG_GMASK=m takes m CUs per XCD away from the GeoT stream (and sizes its persistent grids to
+    # the CUs left), DI_DIAG_PMASK=m puts the pair stream on exactly those m CUs per XCD (0: all CUs).
+    # The set is balanced per XCD whether mask bit c maps to XCD c % 8 or to XCD c / 32: bit
+    # c = 32 x + 8 j + y is in it iff (y - x) mod 8 < m / 4.
+    "cusplit": [("streams.hip", """  std::vector<uint32_t> mask((size_t)(cus + 31) / 32, 0u);
+  for (int c = 0; c < cus; ++c) mask[(size_t)c >> 5] |= 1u << (c & 31);""", """  static int calls = 0;
+  const int which = calls++ & 1;  // 0: the GeoT stream, 1: the pair stream (schedule_streams order)
+  const char* ev = getenv(which ? "DI_DIAG_PMASK" : "DI_DIAG_GMASK");
+  const int m = ev ? atoi(ev) : 0;
+  std::vector<uint32_t> mask((size_t)(cus + 31) / 32, 0u);
+  for (int c = 0; c < cus; ++c) {
+    const bool in = m > 0 && ((((c & 7) - (c >> 5)) & 7) < m / 4);
+    if (which ? (m == 0 || in) : !in) mask[(size_t)c >> 5] |= 1u << (c & 31);
+  }""", 1),
+                ("geot_kernels.hip", "const int cus = device_cus();",
+                 'const int cus = device_cus() - 8 * (getenv("DI_DIAG_GMASK") ? atoi(getenv("DI_DIAG_GMASK")) : 0);', 3)],
 }
 # combinations (every substitution of each part)
 DIAGS["prio47node"] = DIAGS["prio47"] + DIAGS["nodeprio"]
