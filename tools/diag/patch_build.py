@@ -142,6 +142,17 @@ constexpr int LDS_T = 2 * HID + 8;""", 1)],
   }""", 1),
                 ("geot_kernels.hip", "const int cus = device_cus();",
                  'const int cus = device_cus() - 8 * (getenv("DI_DIAG_GMASK") ? atoi(getenv("DI_DIAG_GMASK")) : 0);', 3)],
+    # the edge ring's three re-reads of the edge's own F row (res_connect, final_linear, O_edge) from
+    # rows 0..31 instead (always L2-hot): the most keeping F on chip could buy (timing only)
+    "reread0": [("geot_kernels.hip", "  const u16* f_row = reinterpret_cast<const u16*>(a.f_in) + (int64_t)e * HID;\n  const u16* qkv",
+                 "  const u16* f_row = reinterpret_cast<const u16*>(a.f_in) + (int64_t)e * HID;\n"
+                 "  const u16* f_row0 = reinterpret_cast<const u16*>(a.f_in) + (int64_t)(e & 31) * HID;\n  const u16* qkv", 1),
+                ("geot_kernels.hip", "  fr.load(f_row, h);\n  w = st.next([&] { settle(fr); });  // res_connect_linear",
+                 "  fr.load(f_row0, h);\n  w = st.next([&] { settle(fr); });  // res_connect_linear", 1),
+                ("geot_kernels.hip", "  fr.load(f_row, h);\n  w = st.next([&] { settle(fr); });  // final_linear",
+                 "  fr.load(f_row0, h);\n  w = st.next([&] { settle(fr); });  // final_linear", 1),
+                ("geot_kernels.hip", "    fr.load(f_row, h);                 // O_edge: re-read",
+                 "    fr.load(f_row0, h);                 // O_edge: re-read", 1)],
 }
 # combinations (every substitution of each part)
 DIAGS["prio47node"] = DIAGS["prio47"] + DIAGS["nodeprio"]
