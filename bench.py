@@ -529,8 +529,8 @@ def main():
     ap.add_argument("--pair-kernel", default="auto", choices=["auto", "lines", "rows", "vector"],
                     help="--overlap 0: the per-micro-batch pair-tensor kernel (auto: row streaming)")
     ap.add_argument("--pair-blocks", type=int, default=0,
-                    help="pair-stream blocks (0: half the CUs; --overlap 0: resident blocks, 0 = one per CU)")
-    ap.add_argument("--pair-waves", type=int, default=0, help="waves per pair block (0: 4)")
+                    help="pair-stream blocks (0: one per CU; --overlap 0: resident blocks, 0 = one per CU)")
+    ap.add_argument("--pair-waves", type=int, default=0, help="waves per pair block (0: 2 on the pair stream, 4 with --overlap 0)")
     ap.add_argument("--ring", type=int, default=16, help="hT ring slots of the overlapped schedule")
     ap.add_argument("--help-every", type=int, default=4,
                     help="the GeoT stream issues a pair help launch every this many micro-batches")
@@ -570,11 +570,13 @@ def main():
         # nn.Embedding(max_num_graph_nodes=2304) cannot index 4000 residues, so the synthetic model is
         # built with max_num_graph_nodes=4096 (a LitGINI hyper-parameter); a [256,4000,4000] bf16
         # pair tensor is 8.19 GB, so micro-batches of 2 complexes.
-        # the pair stream on 192 blocks x 4 waves (C3: 128): C5's GeoT stream is shorter than its pair
-        # stream (16.4 GB per micro-batch of 2), so a larger grid beside GeoT pays -- round 6, session
-        # r6_12: 128 / 160 / 192 / 224 blocks 528 / 551 / 551 / 536 complexes/s, pair roofline 0.487 /
-        # 0.549 / 0.557 / -- (192: help launches write 1.2 % of the bytes instead of 10 %)
-        for key, val in (("residues", 4000), ("knn", 30), ("layers", 4), ("node_limit", 4096), ("pair_blocks", 192)):
+        # the pair stream on 192 blocks x 4 waves (C3: one 2-wave block per CU): C5's GeoT stream is
+        # shorter than its pair stream (16.4 GB per micro-batch of 2), so more store waves beside GeoT
+        # pay -- round 6, session r6_12: 128 / 160 / 192 / 224 blocks x 4 528 / 551 / 551 / 536
+        # complexes/s, pair roofline 0.487 / 0.549 / 0.557 / -- (192: help launches write 1.2 % of the
+        # bytes instead of 10 %)
+        for key, val in (("residues", 4000), ("knn", 30), ("layers", 4), ("node_limit", 4096), ("pair_blocks", 192),
+                         ("pair_waves", 4)):
             if getattr(args, key) in (None, ap.get_default(key)):
                 setattr(args, key, val)
         if args.complexes == ap.get_default("complexes"):
@@ -689,7 +691,7 @@ def main():
     elif args.overlap:
         streams = (f"GeoT || pair tensor: GeoT on one HIP stream (each micro-batch signalled by the next GeoT launch), the "
                    f"pair tensors on ONE persistent di_pair_stream launch per step on a second stream "
-                   f"({args.pair_blocks or 'CUs/2'} blocks x {args.pair_waves or 4} waves, bounded nt stores, "
+                   f"({args.pair_blocks or 'one per CU'} blocks x {args.pair_waves or 2} waves, bounded nt stores, "
                    f"device-queue tickets), di_pair_help on the GeoT stream every {args.help_every} micro-batches "
                    f"(hT ring of {args.ring}) and a drain at the end of the timed steps; no host events between "
                    f"the streams; both streams on hardware queues of their own (CU-masked)")

@@ -76,7 +76,7 @@ def _run_schedule(c3, steps, ring, help_every, patience_ms=20.0, allow_gave_up=F
     cus = torch.cuda.get_device_properties(0).multi_processor_count
     taps = {}
     sch = OverlappedSchedule(eng, mbs, c3["h1r"], c3["h2r"], [N_RES] * M, [N_RES] * M, sinks, ring=ring,
-                             help_every=help_every, stream_blocks=cus // 2, stream_waves=4, patience_ms=patience_ms,
+                             help_every=help_every, stream_blocks=cus, stream_waves=2, patience_ms=patience_ms,
                              tap=lambda j, h, e: taps.__setitem__(j, (h.clone(), e.clone())))
     assert sch.concurrent and sch.mode == "overlapped"
     for _ in range(steps):

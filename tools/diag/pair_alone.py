@@ -94,11 +94,13 @@ def main():
                               "gave_up": c["gave_up"], "stream_bytes": c["stream_bytes"]}))
         return
     if args.stream_only:
-        t, c = queue_run("stream", 128, 4)
-        print(json.dumps({"what": "di_pair_stream (bounded nt stores)", "blocks": 128, "waves": 4, "jobs_per_launch": args.jobs,
+        # the product's beside shape: one 2-wave block per CU (di_pair_stream's default)
+        cus = torch.cuda.get_device_properties(0).multi_processor_count
+        t, c = queue_run("stream", cus, 2)
+        print(json.dumps({"what": "di_pair_stream (bounded nt stores)", "blocks": cus, "waves": 2, "jobs_per_launch": args.jobs,
                           "launches": 4, "us_per_job": 1e6 * t / args.jobs, "tb_s": job_bytes * args.jobs / t / 1e12}))
         return
-    for blocks, waves in ((128, 4), (256, 4), (128, 8), (256, 8), (64, 4)):
+    for blocks, waves in ((256, 2), (512, 1), (128, 4), (256, 4), (128, 8), (64, 4)):
         t, c = queue_run("stream", blocks, waves)
         out.append({"what": "di_pair_stream (bounded nt stores)", "blocks": blocks, "waves": waves,
                     "us_per_job": 1e6 * t / args.jobs, "tb_s": job_bytes * args.jobs / t / 1e12, "gave_up": c["gave_up"]})
