@@ -104,6 +104,7 @@ constexpr int LDS_T = 2 * HID + 8;""", 1)],
     # the beside store window: four stores in flight per pair wave (three in the product)
     "inflight4": [("pair_tensor.hip", "constexpr int PAIR_INFLIGHT = 3;", "constexpr int PAIR_INFLIGHT = 4;", 1)],
     "inflight2": [("pair_tensor.hip", "constexpr int PAIR_INFLIGHT = 3;", "constexpr int PAIR_INFLIGHT = 2;", 1)],
+    "inflight6": [("pair_tensor.hip", "constexpr int PAIR_INFLIGHT = 3;", "constexpr int PAIR_INFLIGHT = 6;", 1)],
     # round 6, static issue priority (MI355X_MICROARCH.md, two waves per SIMD, item 4): the edge ring's
     # second-dispatched half (waves 4-7) at s_setprio 1 for the whole launch / the first half instead
     "prio47": [("geot_kernels.hip", "  st.fill();\n#pragma unroll 1\n", "  if (wave >= 4) __builtin_amdgcn_s_setprio(1);\n  st.fill();\n#pragma unroll 1\n", 1)],
