@@ -479,6 +479,7 @@ def sub_record(what, dtype, geo_ref, complexes, pool_gb, P, M, n_res, k, args, d
     eng.split_node = args.node_kernel == "split"
     eng.fold_attn = args.node_kernel == "fold"
     eng.fuse_embed_init = args.init_kernel == "fused"
+    eng.resident_init = not args.overlap  # beside the pair stream: the staged InitEdge (OverlappedSchedule)
     mbs = [select_graphs(pool_gb, [2 * ((m * M + j) % P) + s for j in range(M) for s in (0, 1)]).with_geo_ref(geo_ref)
            for m in range(complexes // M)]
     gb0 = mbs[0]
@@ -606,6 +607,7 @@ def main():
     eng.split_node = args.node_kernel == "split"
     eng.fold_attn = args.node_kernel == "fold"
     eng.fuse_embed_init = args.init_kernel == "fused"
+    eng.resident_init = not args.overlap  # beside the pair stream: the staged InitEdge (OverlappedSchedule)
 
     # ---- inputs: a pool of distinct complexes built on the device (kNN + features + ids) ----
     P = min(args.pool, args.complexes)

@@ -99,6 +99,11 @@ class GeoTEngine:
         # (di_embed_init_edge, bf16 or fp32) instead of a separate launch (default, round 4: serial
         # 101 us for both vs 19 + 108 us with the resident InitEdge after the embedding)
         self.fuse_embed_init = True
+        # with fuse_embed_init off: bf16 reference-featurised batches run InitEdge with its weights
+        # resident in LDS (di_init_edge_resident: one 12-wave block per CU at 168 VGPRs), else the
+        # staged di_init_edge. The resident block cannot share a SIMD with a pair-stream wave, so the
+        # overlapped schedule needs it off (pipeline.OverlappedSchedule checks)
+        self.resident_init = True
 
     def _check_blob_sizes(self):
         p, dt = self.packed, _DI_DT[self.dtype]
@@ -197,7 +202,7 @@ class GeoTEngine:
             _lib.check(lib.di_node_embed(g, dt, gb.node_f.shape[1], _ptr(gb.node_f), _ptr(p.embed[0]),
                                          _ptr(p.embed[1]), _ptr(h[0]), _ptr(qkv[0]), sq, sjob, st), "di_node_embed")
             tick("init_edge")
-            if self.dtype == "bf16" and gb.geo_ref:
+            if self.dtype == "bf16" and gb.geo_ref and self.resident_init:
                 # the path's InitEdge weights resident in LDS (one block per CU): faster alone than the
                 # staged kernel
                 _lib.check(lib.di_init_edge_resident(g, _ptr(gb.edge_f), _ptr(p.init[0]), _ptr(p.init[1]),

@@ -148,6 +148,12 @@ class OverlappedSchedule:
                  capacity_steps=64, jobs_per_launch=0, discard_outputs=False, tap=None):
         if help_every < 1 or ring < 2 * help_every:
             raise ValueError("need ring >= 2 * help_every")
+        if eng.dtype == "bf16" and not eng.fuse_embed_init and eng.resident_init:
+            # its 12-wave block (3 x 168 VGPRs per SIMD) does not fit on a SIMD holding a pair-stream
+            # wave, and the default pair launch puts store waves on every CU: InitEdge would wait for
+            # the pair waves to give up (measured: gave_up on every wave)
+            raise ValueError("the LDS-resident InitEdge (engine.resident_init) cannot run beside the pair "
+                             "stream: set eng.resident_init = False or keep eng.fuse_embed_init")
         self.eng, self.mbs = eng, mbs
         if s_geot is None or s_pair is None:
             g, p = schedule_streams(eng.device)
