@@ -693,7 +693,8 @@ def main():
     elif args.overlap:
         streams = (f"GeoT || pair tensor: GeoT on one HIP stream (each micro-batch signalled by the next GeoT launch), the "
                    f"pair tensors on ONE persistent di_pair_stream launch per step on a second stream "
-                   f"({args.pair_blocks or 'one per CU'} blocks x {args.pair_waves or 2} waves, bounded nt stores, "
+                   f"({args.pair_blocks or ('CUs/2' if args.dtype == 'f32' else 'one per CU')} blocks x "
+                   f"{args.pair_waves or (4 if args.dtype == 'f32' else 2)} waves, bounded nt stores, "
                    f"device-queue tickets), di_pair_help on the GeoT stream every {args.help_every} micro-batches "
                    f"(hT ring of {args.ring}) and a drain at the end of the timed steps; no host events between "
                    f"the streams; both streams on hardware queues of their own (CU-masked)")

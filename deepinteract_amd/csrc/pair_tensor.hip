@@ -651,11 +651,14 @@ extern "C" int di_pair_stream(di_dtype dt, const di_pair_job* jobs, int32_t job_
   if (!jobs || !queue || job_begin < 0 || job_end <= job_begin || hidden <= 0 || (dt != DI_BF16 && dt != DI_F32) ||
       !(patience_ms > 0.f))
     return DI_EINVAL;
-  // default shape: one 2-wave block per CU (512 store waves on 256 CUs). Round 6, beside the
+  // default shape, bf16: one 2-wave block per CU (512 store waves on 256 CUs). Round 6, beside the
   // persistent edge ring and the weight-stationary node layers: 256 x 2 and 512 x 1 beat round 3's
-  // 128 x 4 (4 waves on half the CUs) by 2 % on two boxes; more than 512 waves slow GeoT
-  const int blocks = launch && launch->blocks > 0 ? launch->blocks : device_cus();
-  const int waves = launch && launch->waves_per_block > 0 ? launch->waves_per_block : 2;
+  // 128 x 4 (4 waves on half the CUs) by 2 % on two boxes; more than 512 waves slow GeoT. fp32 keeps
+  // 128 x 4 beside its 4-wave edge blocks (1831 / 1805 vs 1857 / 1851 complexes/s)
+  const int cus = device_cus();
+  const bool f32 = dt == DI_F32;
+  const int blocks = launch && launch->blocks > 0 ? launch->blocks : (f32 ? (cus + 1) / 2 : cus);
+  const int waves = launch && launch->waves_per_block > 0 ? launch->waves_per_block : (f32 ? 4 : 2);
   if (waves > 16) return DI_EINVAL;
   const dim3 g((unsigned)blocks), b((unsigned)(64 * waves));
   hipStream_t s = (hipStream_t)stream;

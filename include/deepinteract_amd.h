@@ -260,7 +260,8 @@ int32_t di_pair_job_items(int32_t num_complexes, int32_t max_l1, int32_t hidden)
 /* the job's hT is complete (stream order of `stream`): raises the queue's signalled count to job + 1 */
 int di_pair_signal(void* queue, int32_t job, void* stream);
 /* persistent pair stream over jobs [job_begin, job_end) (jobs: device array indexed by job number);
- * launch: blocks (0: one per CU), waves_per_block (0: 2); always the beside store policy */
+ * launch: blocks (0: one per CU; fp32: half the CUs), waves_per_block (0: 2; fp32: 4); always the beside
+ * store policy */
 int di_pair_stream(di_dtype dt, const di_pair_job* jobs, int32_t job_begin, int32_t job_end, int32_t hidden,
                    void* queue, const di_pair_launch* launch, float patience_ms, void* stream);
 /* complete jobs [first_job, last_job] (all produced before this call in `stream` order); launch:
