@@ -155,6 +155,11 @@ constexpr int LDS_T = 2 * HID + 8;""", 1)],
                  "  fr.load(f_row0, h);\n  w = st.next([&] { settle(fr); });  // final_linear", 1),
                 ("geot_kernels.hip", "    fr.load(f_row, h);                 // O_edge: re-read",
                  "    fr.load(f_row0, h);                 // O_edge: re-read", 1)],
+    # the edge ring's weight stages DMA'd at half their blocks (the slot's second half keeps stale
+    # weights; timing only): how much of the edge layers' cost to the pair stream is their L2 -> LDS
+    # weight stream (~16 TB/s of L2 reads chip-wide while the ring runs)
+    "whalf": [("geot_kernels.hip", "    return {W, {EL_ORDER[si], 0, 0}, {EL_SIZE[si], 0, 0}, 1, vo >= 0 ? V + vo : nullptr};",
+               "    return {W, {EL_ORDER[si], 0, 0}, {EL_SIZE[si] / 2, 0, 0}, 1, vo >= 0 ? V + vo : nullptr};", 1)],
 }
 # combinations (every substitution of each part)
 DIAGS["prio47node"] = DIAGS["prio47"] + DIAGS["nodeprio"]
