@@ -160,6 +160,10 @@ constexpr int LDS_T = 2 * HID + 8;""", 1)],
     # weight stream (~16 TB/s of L2 reads chip-wide while the ring runs)
     "whalf": [("geot_kernels.hip", "    return {W, {EL_ORDER[si], 0, 0}, {EL_SIZE[si], 0, 0}, 1, vo >= 0 ? V + vo : nullptr};",
                "    return {W, {EL_ORDER[si], 0, 0}, {EL_SIZE[si] / 2, 0, 0}, 1, vo >= 0 ? V + vo : nullptr};", 1)],
+    # the edge ring's weight stages all DMA'd from the blob's first blocks (same bytes, a 36-KiB
+    # footprint that always hits L2; timing only): separates the stream's L2 misses from its bytes
+    "ringw0": [("geot_kernels.hip", "    return {W, {EL_ORDER[si], 0, 0}, {EL_SIZE[si], 0, 0}, 1, vo >= 0 ? V + vo : nullptr};",
+                "    return {W, {0, 0, 0}, {EL_SIZE[si], 0, 0}, 1, vo >= 0 ? V + vo : nullptr};", 1)],
 }
 # combinations (every substitution of each part)
 DIAGS["prio47node"] = DIAGS["prio47"] + DIAGS["nodeprio"]
