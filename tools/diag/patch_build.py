@@ -164,6 +164,41 @@ constexpr int LDS_T = 2 * HID + 8;""", 1)],
     # footprint that always hits L2; timing only): separates the stream's L2 misses from its bytes
     "ringw0": [("geot_kernels.hip", "    return {W, {EL_ORDER[si], 0, 0}, {EL_SIZE[si], 0, 0}, 1, vo >= 0 ? V + vo : nullptr};",
                 "    return {W, {0, 0, 0}, {EL_SIZE[si], 0, 0}, 1, vo >= 0 ? V + vo : nullptr};", 1)],
+    # the edge ring's blocks of one XCD kept in step: after each tile (but a block's last ones), wave 0
+    # adds to its XCD's counter and waits (<= 20 us) until every block of the XCD has finished that
+    # tile, so the 32 blocks stay within one tile of each other and fewer of the layer's weight stages
+    # are live in the XCD's L2 at once (the stream's L2 misses). Results
+    # unchanged (A/B variant, correct outputs)
+    "xcdbar": [("geot_kernels.hip", """  const int* in_ptr = nullptr;
+};
+
+struct NodeArgs {""", """  const int* in_ptr = nullptr;
+  uint32_t* xbar = nullptr;  // diag xcdbar: per-XCD tile counters (16 words apart)
+};
+
+struct NodeArgs {""", 1),
+               ("geot_kernels.hip", """    edge_x32_tile<MODE, GC>(a, st, e, valid, lane, h);
+  }
+}""", """    edge_x32_tile<MODE, GC>(a, st, e, valid, lane, h);
+    const int G = (int)gridDim.x, x = (int)(blockIdx.x & 7);
+    if (a.xbar && wave == 0 && (G & 7) == 0 && i + 1 < ntiles / G) {
+      uint32_t* c = a.xbar + 16 * x;
+      const uint32_t need = (uint32_t)((i + 1) * (G / 8));
+      if (lane == 0) __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need &&
+             __builtin_amdgcn_s_memrealtime() - t0 < 2000)
+        __builtin_amdgcn_s_sleep(2);
+    }
+  }
+}""", 1),
+               ("geot_kernels.hip", """    const dim3 grid((unsigned)(ntiles < cus ? ntiles : cus)), block(EdgeRingGeo::THREADS);
+    if (final_layer && gc) hipLaunchKernelGGL((k_edge_x32_ring<1, true>), grid, block, 0, s, a, ntiles);""",
+                """    const dim3 grid((unsigned)(ntiles < cus ? ntiles : cus)), block(EdgeRingGeo::THREADS);
+    static uint32_t* xbar = nullptr;
+    if (!xbar && hipMalloc(&xbar, 8 * 16 * sizeof(uint32_t)) != hipSuccess) xbar = nullptr;
+    if (xbar && hipMemsetAsync(xbar, 0, 8 * 16 * sizeof(uint32_t), s) == hipSuccess) a.xbar = xbar;
+    if (final_layer && gc) hipLaunchKernelGGL((k_edge_x32_ring<1, true>), grid, block, 0, s, a, ntiles);""", 1)],
 }
 # combinations (every substitution of each part)
 DIAGS["prio47node"] = DIAGS["prio47"] + DIAGS["nodeprio"]
